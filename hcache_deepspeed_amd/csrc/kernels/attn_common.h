@@ -1,0 +1,91 @@
+// MFMA / LDS building blocks shared by the attention kernels (flash_attn.hip, paged_attn.hip).
+//
+// All attention math uses v_mfma_f32_32x32x16_bf16 with the "query (or key) on the lane"
+// orientation: for S^T = K . Q^T the accumulator column (lane & 31) is the query, so every
+// softmax row statistic is lane-local (one cross-half exchange, no LDS round trip), and the
+// accumulator registers are directly the B operand of the following P.V product
+// (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+//
+// K/V/Q/dO tiles live in LDS as 64 rows x 256 B (head_dim 128, bf16) in the XOR layout
+//   off(row, ch) = 256*row + 16*(ch ^ (((row & 3) << 2) | ((row >> 2) & 3)))
+// which serves both the row reads (ds_read_b128, A operand K-rows) and the transposed reads
+// (ds_read_b64_tr_b16, A operand V^T) without bank conflicts (guide §5.5 T10 image (b)).
+// Tiles are filled with global_load_lds_dwordx4 (LDS-DMA): the destination is lane-linear,
+// so the XOR swizzle is applied to the per-lane GLOBAL source address (guide rule 21).
+#pragma once
+#include "hds_common.h"
+
+namespace hds {
+namespace attn {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int tile_off(int row, int ch) { return row * 256 + 16 * (ch ^ swz(row)); }
+
+// row index of accumulator register r (0..15) for lane half h in a 32x32 MFMA tile
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Stage a 64-row x 128-col bf16 tile into LDS with LDS-DMA. `row_ptr(row)` gives the global
+// address of logical row `row` (already clamped by the caller). 16 wave-instructions of 1 KiB,
+// 4 per wave for a 256-thread block.
+template <typename RowPtr>
+__device__ __forceinline__ void stage_tile64(char* lds_tile, RowPtr row_ptr) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = w * 4 + i;
+    const int row = 4 * n + (lane >> 4);
+    const int pc = lane & 15;
+    const int ch = pc ^ swz(row);
+    const char* src = (const char*)row_ptr(row) + ch * 16;
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds_tile + n * 1024), 16, 0, 0);
+  }
+}
+
+// A-operand fragment from a row-major tile: rows on lanes (row0 + (lane&31)), k = 16*ks + 8h .. +7
+__device__ __forceinline__ bf16x8 read_rows(const char* lds_tile, int row0, int ks) {
+  const int lane = threadIdx.x & 63;
+  const int row = row0 + (lane & 31);
+  const int ch = 2 * ks + (lane >> 5);
+  return *reinterpret_cast<const bf16x8*>(lds_tile + tile_off(row, ch));
+}
+
+// A-operand fragment of the TRANSPOSED tile (tile^T: rows = tile columns d, k = tile rows)
+// for k-step s (16 tile rows starting at 16*s) and column block dt (32 columns), in the permuted
+// k order that matches accumulator-derived B operands (see acc_to_b):
+//   element j of lane half h  <->  tile row 16*s + 8*(j>>2) + 4*h + (j&3)
+__device__ __forceinline__ bf16x8 read_tr(const char* lds_tile, int s, int dt) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = 16 * s + 4 * (g >> 1) + q;
+  const int ch = 4 * dt + 2 * (g & 1) + (p >> 1);
+  const char* a0 = lds_tile + tile_off(row, ch) + 8 * (p & 1);
+  const char* a1 = lds_tile + tile_off(row + 8, ch) + 8 * (p & 1);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(a0));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(a1));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// B-operand fragment for k-step (s & 1) of a 32-row accumulator tile: registers 8*(s&1) .. +7.
+template <int HALF>
+__device__ __forceinline__ bf16x8 acc_to_b(const f32x16& acc) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)acc[8 * HALF + j];
+  return r;
+}
+
+__device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+}  // namespace attn
+}  // namespace hds

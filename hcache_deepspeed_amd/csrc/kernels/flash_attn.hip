@@ -1,0 +1,558 @@
+// FlashAttention forward + backward for gfx950 (causal / sliding-window / full, GQA, varlen),
+// head_dim 128, bf16 in/out, fp32 softmax statistics (LSE) exposed for FPDT / ring merges.
+//
+// Capability parity: replaces the reference's prebuilt NVIDIA-only `libblockedflash`
+// (deepspeed/inference/v2/kernels/ragged_ops/blocked_flash), the `flash_attn`
+// python dependency of sequence/fpdt_layer.py (§2.13) and the CUTLASS memory-efficient
+// attention of csrc/deepspeed4science (K24) for the training path.
+//
+// Structure (all three kernels: 256 threads = 4 waves, v_mfma_f32_32x32x16_bf16):
+//   fwd   : workgroup = 128 query rows of one (batch, q-head); wave = 32 rows; K/V tiles of 64
+//           keys via LDS-DMA into a 2-deep LDS ring; S^T = K.Q^T puts the query on the lane so the
+//           online softmax is lane-local; O^T += V^T.P^T reuses the S accumulators as the B
+//           operand and reads V^T with ds_read_b64_tr_b16.  Heaviest causal blocks launch first.
+//   dkdv  : workgroup = 128 keys of one (batch, kv-head); wave = 32 keys (key on the lane);
+//           sweeps the GQA group's q-heads x 64-query tiles; dK and dV stay in accumulators
+//           for the whole sweep, so no cross-workgroup reduction exists for them.
+//   dq    : workgroup = 128 query rows of one (batch, q-head); sweeps key tiles; dQ in
+//           accumulators. Deterministic (no float atomics anywhere).
+// P is recomputed from the forward LSE; delta = rowsum(dO * O) comes from a tiny pre-kernel.
+#include "attn_common.h"
+
+using namespace hds;
+using namespace hds::attn;
+
+namespace {
+
+constexpr int D = 128;
+constexpr int BM = 128;  // query rows per workgroup (fwd, dq)
+constexpr int BN = 64;   // keys per LDS tile (fwd, dq) / query rows per tile (dkdv)
+constexpr int BK = 128;  // keys per workgroup (dkdv)
+constexpr float kLog2e = 1.4426950408889634f;
+
+struct AttnParams {
+  const bf16* q;
+  const bf16* k;
+  const bf16* v;
+  bf16* o;
+  float* lse;  // [Hq][total_tokens], natural-log units of (scale * q.k)
+  const bf16* dout;
+  bf16* dq;
+  bf16* dk;
+  bf16* dv;
+  float* delta;  // [Hq][total_tokens]
+  int64_t sq, sk, sv, so, sdo, sdq, sdk, sdv;  // token strides (elements)
+  const int* cu_seqlens;                       // [B+1] or null
+  int seq_len;                                 // when cu_seqlens is null
+  int total_tokens;
+  int batch, hq, hkv;
+  float scale;
+  int causal;
+  int window;  // >0: sliding window (keys in (q - window, q])
+};
+
+__device__ __forceinline__ void seq_bounds(const AttnParams& p, int b, int& start, int& len) {
+  if (p.cu_seqlens) {
+    start = p.cu_seqlens[b];
+    len = p.cu_seqlens[b + 1] - start;
+  } else {
+    start = b * p.seq_len;
+    len = p.seq_len;
+  }
+}
+
+__device__ __forceinline__ bool masked(const AttnParams& p, int qi, int kj, int len) {
+  if (kj >= len || qi >= len) return true;
+  if (p.causal && kj > qi) return true;
+  if (p.window > 0 && kj <= qi - p.window) return true;
+  return false;
+}
+
+// =====================================================================================
+// forward
+// =====================================================================================
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
+  const int b = blockIdx.z, hq = blockIdx.y;
+  int start, len;
+  seq_bounds(p, b, start, len);
+  const int nqb = (len + BM - 1) / BM;
+  const int qb = p.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;  // heaviest causal blocks first
+  if (qb >= nqb || len == 0) return;
+  const int hk = hq / (p.hq / p.hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int q0 = qb * BM;
+  const int myq = q0 + 32 * w + (lane & 31);
+  const float c = p.scale * kLog2e;
+
+  // Q fragments (B operand of S^T = K.Q^T): Q[myq][16ks + 8h .. +7]
+  bf16x8 qf[8];
+  {
+    const int qr = myq < len ? myq : len - 1;
+    const bf16* qp = p.q + (int64_t)(start + qr) * p.sq + (int64_t)hq * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+  }
+
+  // key-tile range
+  int kt_end = (len + BN - 1) / BN;
+  if (p.causal) {
+    const int last = q0 + BM - 1 < len - 1 ? q0 + BM - 1 : len - 1;
+    kt_end = last / BN + 1;
+  }
+  int kt_begin = 0;
+  if (p.window > 0) {
+    const int first = q0 - p.window + 1;
+    kt_begin = first > 0 ? first / BN : 0;
+  }
+
+  auto kptr = [&](int kt) {
+    return [=](int row) {
+      int r = kt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.k + (int64_t)(start + r) * p.sk + (int64_t)hk * D;
+    };
+  };
+  auto vptr = [&](int kt) {
+    return [=](int row) {
+      int r = kt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.v + (int64_t)(start + r) * p.sv + (int64_t)hk * D;
+    };
+  };
+
+  f32x16 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
+
+  stage_tile64(smem + 0, kptr(kt_begin));
+  stage_tile64(smem + 2 * 16384, vptr(kt_begin));
+  __syncthreads();
+
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
+    char* Kt = smem + buf * 16384;
+    char* Vt = smem + 2 * 16384 + buf * 16384;
+    if (kt + 1 < kt_end) {
+      stage_tile64(smem + (buf ^ 1) * 16384, kptr(kt + 1));
+      stage_tile64(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
+    }
+    const int k0 = kt * BN;
+    // wave-uniform skip of fully masked tiles
+    bool skip = (k0 >= len) || (wq_lo >= len);
+    if (p.causal && k0 > wq_hi) skip = true;
+    if (p.window > 0 && k0 + BN - 1 <= wq_lo - p.window) skip = true;
+    if (!skip) {
+      f32x16 s[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) s[t] = mfma(read_rows(Kt, 32 * t, ks), qf[ks], s[t]);
+      }
+      const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
+                             (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float x = s[t][r] * c;
+          if (need_mask && masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) x = -INFINITY;
+          s[t][r] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float muse = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = fast_exp2(m - muse);
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = fast_exp2(s[t][r] - muse);
+          s[t][r] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+      bf16x8 pb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int st = 0; st < 4; ++st) o[dt] = mfma(read_tr(Vt, st, dt), pb[st], o[dt]);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: O[myq][d] = o^T / l ; lse
+  if (myq < len) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* op = p.o + (int64_t)(start + myq) * p.so + (int64_t)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = (bf16)(o[dt][4 * g + j] * inv);
+        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * h) = v4;
+      }
+    if (h == 0 && p.lse) {
+      const float lse = (l > 0.f) ? (m + __log2f(l)) / kLog2e : -INFINITY;
+      p.lse[(int64_t)hq * p.total_tokens + start + myq] = lse;
+    }
+  }
+}
+
+// =====================================================================================
+// backward pre-pass: delta[hq][t] = sum_d dO * O   (16 lanes per row, 4 rows per wave)
+// =====================================================================================
+__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams p) {
+  const int64_t rows = (int64_t)p.total_tokens * p.hq;
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int sub = threadIdx.x & 15;
+  float acc = 0.f;
+  int64_t t = 0;
+  int hq = 0;
+  if (row < rows) {
+    t = row / p.hq;
+    hq = (int)(row - t * p.hq);
+    float a[8], bb[8];
+    Vec8<bf16>::load(p.o + t * p.so + (int64_t)hq * D + sub * 8, a);
+    Vec8<bf16>::load(p.dout + t * p.sdo + (int64_t)hq * D + sub * 8, bb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
+  }
+#pragma unroll
+  for (int off = 8; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 16);
+  if (row < rows && sub == 0) p.delta[(int64_t)hq * p.total_tokens + t] = acc;
+}
+
+// =====================================================================================
+// backward dK, dV
+// =====================================================================================
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
+  // LDS: Q[2] (16K each), dO[2] (16K each), lse[2][64], delta[2][64]
+  __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + 4 * 256];
+  const int b = blockIdx.z, hk = blockIdx.y;
+  int start, len;
+  seq_bounds(p, b, start, len);
+  const int nkb = (len + BK - 1) / BK;
+  const int kb = blockIdx.x;
+  if (kb >= nkb || len == 0) return;
+  const int G = p.hq / p.hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int kw0 = kb * BK + 32 * w;      // this wave's first key
+  const int myk = kw0 + (lane & 31);
+  const float c = p.scale * kLog2e;
+
+  // K and V fragments (B operands): K[myk][16ks + 8h ..]
+  bf16x8 kf[8], vf[8];
+  {
+    const int kr = myk < len ? myk : len - 1;
+    const bf16* kp = p.k + (int64_t)(start + kr) * p.sk + (int64_t)hk * D + 8 * h;
+    const bf16* vp = p.v + (int64_t)(start + kr) * p.sv + (int64_t)hk * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(kp + 16 * ks);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 16 * ks);
+    }
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x16{};
+
+  // query-tile range (same for every q-head of the group)
+  int qt_begin = 0;
+  if (p.causal) qt_begin = (kb * BK) / BN;
+  int qt_end = (len + BN - 1) / BN;
+  if (p.window > 0) {
+    const int lastq = kb * BK + BK - 1 + p.window - 1;
+    const int e = lastq / BN + 1;
+    qt_end = e < qt_end ? e : qt_end;
+  }
+  const int nqt = qt_end - qt_begin;
+  const int total = nqt * G;
+  if (total <= 0) {
+    // still write zeros below
+  }
+
+  auto stage = [&](int it, int buf) {
+    const int g = it / nqt, qt = qt_begin + it % nqt;
+    const int hq = hk * G + g;
+    char* Qt = smem + buf * 16384;
+    char* Ot = smem + 2 * 16384 + buf * 16384;
+    float* Lt = reinterpret_cast<float*>(smem + 4 * 16384 + buf * 256);
+    float* Dt = reinterpret_cast<float*>(smem + 4 * 16384 + 512 + buf * 256);
+    stage_tile64(Qt, [=](int row) {
+      int r = qt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.q + (int64_t)(start + r) * p.sq + (int64_t)hq * D;
+    });
+    stage_tile64(Ot, [=](int row) {
+      int r = qt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.dout + (int64_t)(start + r) * p.sdo + (int64_t)hq * D;
+    });
+    if (w < 2) {
+      int r = qt * BN + lane;
+      r = r < len ? r : len - 1;
+      const float* src = (w == 0 ? p.lse : p.delta) + (int64_t)hq * p.total_tokens + start + r;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(w == 0 ? Lt : Dt), 4, 0, 0);
+    }
+  };
+
+  if (total > 0) {
+    stage(0, 0);
+    __syncthreads();
+  }
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < total) stage(it + 1, buf ^ 1);
+    const int qt = qt_begin + it % nqt;
+    const char* Qt = smem + buf * 16384;
+    const char* Ot = smem + 2 * 16384 + buf * 16384;
+    const float* Lt = reinterpret_cast<const float*>(smem + 4 * 16384 + buf * 256);
+    const float* Dt = reinterpret_cast<const float*>(smem + 4 * 16384 + 512 + buf * 256);
+    const int qbase = qt * BN;
+    // wave-uniform skip: all queries of the tile before this wave's keys (causal)
+    bool skip = (kw0 >= len);
+    if (p.causal && qbase + BN - 1 < kw0) skip = true;
+    if (p.window > 0 && qbase > kw0 + 31 + p.window - 1) skip = true;
+    if (!skip) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        // S = Q.K^T (key on lane): rows = queries 32*sub + acc_row
+        f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) sacc = mfma(read_rows(Qt, 32 * sub, ks), kf[ks], sacc);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) dpacc = mfma(read_rows(Ot, 32 * sub, ks), vf[ks], dpacc);
+        // P and dS
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qr = 32 * sub + acc_row(r, h);
+          const int qi = qbase + qr;
+          float pr = fast_exp2(sacc[r] * c - Lt[qr] * kLog2e);
+          if (masked(p, qi, myk, len)) pr = 0.f;
+          sacc[r] = pr;
+          dpacc[r] = pr * (dpacc[r] - Dt[qr]);
+        }
+        const bf16x8 p0 = acc_to_b<0>(sacc), p1 = acc_to_b<1>(sacc);
+        const bf16x8 s0 = acc_to_b<0>(dpacc), s1 = acc_to_b<1>(dpacc);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[dt] = mfma(read_tr(Ot, 2 * sub, dt), p0, dv[dt]);
+          dv[dt] = mfma(read_tr(Ot, 2 * sub + 1, dt), p1, dv[dt]);
+          dk[dt] = mfma(read_tr(Qt, 2 * sub, dt), s0, dk[dt]);
+          dk[dt] = mfma(read_tr(Qt, 2 * sub + 1, dt), s1, dk[dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (myk < len) {
+    bf16* kp = p.dk + (int64_t)(start + myk) * p.sdk + (int64_t)hk * D;
+    bf16* vp = p.dv + (int64_t)(start + myk) * p.sdv + (int64_t)hk * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 a4, b4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a4[j] = (bf16)(dk[dt][4 * g + j] * p.scale);
+          b4[j] = (bf16)(dv[dt][4 * g + j]);
+        }
+        *reinterpret_cast<bf16x4*>(kp + 32 * dt + 8 * g + 4 * h) = a4;
+        *reinterpret_cast<bf16x4*>(vp + 32 * dt + 8 * g + 4 * h) = b4;
+      }
+  }
+}
+
+// =====================================================================================
+// backward dQ
+// =====================================================================================
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
+  const int b = blockIdx.z, hq = blockIdx.y;
+  int start, len;
+  seq_bounds(p, b, start, len);
+  const int nqb = (len + BM - 1) / BM;
+  const int qb = p.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  if (qb >= nqb || len == 0) return;
+  const int hk = hq / (p.hq / p.hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int q0 = qb * BM;
+  const int myq = q0 + 32 * w + (lane & 31);
+  const float c = p.scale * kLog2e;
+  const int qr = myq < len ? myq : len - 1;
+
+  bf16x8 qf[8], df[8];
+  {
+    const bf16* qp = p.q + (int64_t)(start + qr) * p.sq + (int64_t)hq * D + 8 * h;
+    const bf16* dp = p.dout + (int64_t)(start + qr) * p.sdo + (int64_t)hq * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+      df[ks] = *reinterpret_cast<const bf16x8*>(dp + 16 * ks);
+    }
+  }
+  const float lse2 = p.lse[(int64_t)hq * p.total_tokens + start + qr] * kLog2e;
+  const float dlt = p.delta[(int64_t)hq * p.total_tokens + start + qr];
+
+  int kt_end = (len + BN - 1) / BN;
+  if (p.causal) {
+    const int last = q0 + BM - 1 < len - 1 ? q0 + BM - 1 : len - 1;
+    kt_end = last / BN + 1;
+  }
+  int kt_begin = 0;
+  if (p.window > 0) {
+    const int first = q0 - p.window + 1;
+    kt_begin = first > 0 ? first / BN : 0;
+  }
+  auto kptr = [&](int kt) {
+    return [=](int row) {
+      int r = kt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.k + (int64_t)(start + r) * p.sk + (int64_t)hk * D;
+    };
+  };
+  auto vptr = [&](int kt) {
+    return [=](int row) {
+      int r = kt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.v + (int64_t)(start + r) * p.sv + (int64_t)hk * D;
+    };
+  };
+  f32x16 dq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dq[i] = f32x16{};
+  const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
+
+  stage_tile64(smem + 0, kptr(kt_begin));
+  stage_tile64(smem + 2 * 16384, vptr(kt_begin));
+  __syncthreads();
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
+    const char* Kt = smem + buf * 16384;
+    const char* Vt = smem + 2 * 16384 + buf * 16384;
+    if (kt + 1 < kt_end) {
+      stage_tile64(smem + (buf ^ 1) * 16384, kptr(kt + 1));
+      stage_tile64(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
+    }
+    const int k0 = kt * BN;
+    bool skip = (k0 >= len) || (wq_lo >= len);
+    if (p.causal && k0 > wq_hi) skip = true;
+    if (p.window > 0 && k0 + BN - 1 <= wq_lo - p.window) skip = true;
+    if (!skip) {
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = f32x16{};
+        dp[t] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) s[t] = mfma(read_rows(Kt, 32 * t, ks), qf[ks], s[t]);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) dp[t] = mfma(read_rows(Vt, 32 * t, ks), df[ks], dp[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float pr = fast_exp2(s[t][r] * c - lse2);
+          if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) pr = 0.f;
+          s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
+        }
+      const bf16x8 sb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int st = 0; st < 4; ++st) dq[dt] = mfma(read_tr(Kt, st, dt), sb[st], dq[dt]);
+    }
+    __syncthreads();
+  }
+  if (myq < len) {
+    bf16* qp = p.dq + (int64_t)(start + myq) * p.sdq + (int64_t)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = (bf16)(dq[dt][4 * g + j] * p.scale);
+        *reinterpret_cast<bf16x4*>(qp + 32 * dt + 8 * g + 4 * h) = v4;
+      }
+  }
+}
+
+AttnParams make_params(const void* q, const void* k, const void* v, void* o, float* lse, const void* dout, void* dq,
+                       void* dk, void* dv, float* delta, const int64_t* strides, const int* cu_seqlens, int batch,
+                       int seq_len, int total_tokens, int hq, int hkv, float scale, int causal, int window) {
+  AttnParams p;
+  p.q = (const bf16*)q;
+  p.k = (const bf16*)k;
+  p.v = (const bf16*)v;
+  p.o = (bf16*)o;
+  p.lse = lse;
+  p.dout = (const bf16*)dout;
+  p.dq = (bf16*)dq;
+  p.dk = (bf16*)dk;
+  p.dv = (bf16*)dv;
+  p.delta = delta;
+  p.sq = strides[0];
+  p.sk = strides[1];
+  p.sv = strides[2];
+  p.so = strides[3];
+  p.sdo = strides[4];
+  p.sdq = strides[5];
+  p.sdk = strides[6];
+  p.sdv = strides[7];
+  p.cu_seqlens = cu_seqlens;
+  p.seq_len = seq_len;
+  p.total_tokens = total_tokens;
+  p.batch = batch;
+  p.hq = hq;
+  p.hkv = hkv;
+  p.scale = scale;
+  p.causal = causal;
+  p.window = window;
+  return p;
+}
+
+}  // namespace
+
+// strides: int64[8] token strides (elements) for q, k, v, o, dout, dq, dk, dv
+// max_len: max sequence length in the batch (grid sizing)
+HDS_EXPORT int hds_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int64_t* strides,
+                            const int* cu_seqlens, int batch, int seq_len, int max_len, int total_tokens, int hq,
+                            int hkv, int head_dim, float scale, int causal, int window, hipStream_t st) {
+  if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
+  AttnParams p = make_params(q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, strides, cu_seqlens, batch,
+                             seq_len, total_tokens, hq, hkv, scale, causal, window);
+  dim3 grid((max_len + BM - 1) / BM, hq, batch), block(256);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, block, 0, st, p);
+  return hipGetLastError();
+}
+
+HDS_EXPORT int hds_attn_bwd(const void* q, const void* k, const void* v, const void* o, const float* lse,
+                            const void* dout, void* dq, void* dk, void* dv, float* delta, const int64_t* strides,
+                            const int* cu_seqlens, int batch, int seq_len, int max_len, int total_tokens, int hq,
+                            int hkv, int head_dim, float scale, int causal, int window, hipStream_t st) {
+  if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
+  AttnParams p = make_params(q, k, v, (void*)o, (float*)lse, dout, dq, dk, dv, delta, strides, cu_seqlens, batch,
+                             seq_len, total_tokens, hq, hkv, scale, causal, window);
+  const int64_t rows = (int64_t)total_tokens * hq;
+  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((max_len + BK - 1) / BK, hkv, batch), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((max_len + BM - 1) / BM, hq, batch), dim3(256), 0, st, p);
+  return hipGetLastError();
+}

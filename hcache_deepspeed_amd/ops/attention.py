@@ -1,0 +1,253 @@
+"""FlashAttention (causal / sliding window / full, GQA, varlen) with HIP forward+backward.
+
+Reference parity: replaces ``BlockedFlashAttn`` (inference/v2/kernels/ragged_ops/blocked_flash,
+a prebuilt NVIDIA-only library), the ``flash_attn`` dependency of FPDT
+(sequence/fpdt_layer.py:234-254) and the training attention that HF models run unfused.
+
+Two entry points:
+
+* :func:`flash_attn` -- q/k/v as ``[B, S, H, D]`` or varlen ``[T, H, D]`` + ``cu_seqlens``;
+  returns ``o`` (and optionally the fp32 LSE used by FPDT / ring-attention merges).
+* :func:`qkv_attention` -- the training fast path: consumes the fused QKV GEMM output
+  ``[T, Hq + 2*Hkv, D]``, applies RoPE in place, runs attention on strided views of the same
+  buffer, and in backward writes dq/dk/dv straight into one ``[T, Hq + 2*Hkv, D]`` gradient that
+  the QKV GEMM's backward consumes. No split / transpose / cat copies exist on either pass.
+"""
+import math
+
+import torch
+
+from . import native
+from .rope import rope_
+
+_HEAD_DIMS_NATIVE = (128, )
+
+
+def _strides8(*ts):
+    vals = []
+    for t in ts:
+        vals.append(0 if t is None else t.stride(0))
+    while len(vals) < 8:
+        vals.append(0)
+    return torch.tensor(vals, dtype=torch.int64)
+
+
+def _check_tok_layout(t, name):
+    assert t.dim() == 3 and t.stride(2) == 1 and t.stride(1) == t.shape[2], \
+        f"{name}: expected [T, H, D] with contiguous head blocks, got shape {tuple(t.shape)} strides {t.stride()}"
+
+
+def _cu_info(cu_seqlens, T, seq_len):
+    if cu_seqlens is None:
+        B = T // seq_len
+        return None, B, seq_len, seq_len
+    cu = cu_seqlens.to(torch.int32).contiguous()
+    lens = (cu[1:] - cu[:-1])
+    return cu, cu.numel() - 1, 0, int(lens.max().item()) if lens.numel() else 0
+
+
+def _ref_attention(q, k, v, causal, scale, cu_seqlens, seq_len, window):
+    """fp32 torch reference on [T, H, D] tensors; returns o (q.dtype) and lse [Hq, T] fp32."""
+    T, Hq, D = q.shape
+    Hkv = k.shape[1]
+    G = Hq // Hkv
+    if cu_seqlens is None:
+        bounds = [(i * seq_len, (i + 1) * seq_len) for i in range(T // seq_len)]
+    else:
+        c = cu_seqlens.tolist()
+        bounds = list(zip(c[:-1], c[1:]))
+    o = torch.empty(T, Hq, D, dtype=torch.float32, device=q.device)
+    lse = torch.empty(Hq, T, dtype=torch.float32, device=q.device)
+    for (s, e) in bounds:
+        L = e - s
+        if L == 0:
+            continue
+        qs = q[s:e].float().transpose(0, 1)  # [Hq, L, D]
+        ks = k[s:e].float().transpose(0, 1).repeat_interleave(G, 0)
+        vs = v[s:e].float().transpose(0, 1).repeat_interleave(G, 0)
+        sc = torch.matmul(qs, ks.transpose(1, 2)) * scale
+        i = torch.arange(L, device=q.device)
+        mask = torch.zeros(L, L, dtype=torch.bool, device=q.device)
+        if causal:
+            mask |= i[None, :] > i[:, None]
+        if window and window > 0:
+            mask |= i[None, :] <= i[:, None] - window
+        sc = sc.masked_fill(mask, float("-inf"))
+        lse[:, s:e] = torch.logsumexp(sc, dim=-1)
+        o[s:e] = torch.matmul(torch.softmax(sc, dim=-1), vs).transpose(0, 1)
+    return o.to(q.dtype), lse
+
+
+def _native_fwd(q, k, v, o, lse, causal, scale, cu, B, seq_len, max_len, window):
+    T, Hq, D = q.shape
+    strides = _strides8(q, k, v, o)
+    native.check(
+        native.kernels().hds_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+                                      strides.data_ptr(), native.ptr(cu), B, seq_len, max_len, T, Hq, k.shape[1], D,
+                                      float(scale), int(causal), int(window), native.stream()), "attn_fwd")
+
+
+def _native_bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, cu, B, seq_len, max_len, window):
+    T, Hq, D = q.shape
+    delta = torch.empty(Hq, T, device=q.device, dtype=torch.float32)
+    strides = _strides8(q, k, v, o, do, dq, dk, dv)
+    native.check(
+        native.kernels().hds_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
+                                      do.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), delta.data_ptr(),
+                                      strides.data_ptr(), native.ptr(cu), B, seq_len, max_len, T, Hq, k.shape[1], D,
+                                      float(scale), int(causal), int(window), native.stream()), "attn_bwd")
+
+
+def _ref_bwd(q, k, v, do, causal, scale, cu_seqlens, seq_len, window):
+    with torch.enable_grad():
+        qf = q.detach().float().requires_grad_(True)
+        kf = k.detach().float().requires_grad_(True)
+        vf = v.detach().float().requires_grad_(True)
+        o, _ = _ref_attention_f32(qf, kf, vf, causal, scale, cu_seqlens, seq_len, window)
+        dq, dk, dv = torch.autograd.grad(o, (qf, kf, vf), do.float())
+    return dq, dk, dv
+
+
+def _ref_attention_f32(q, k, v, causal, scale, cu_seqlens, seq_len, window):
+    # differentiable fp32 variant of _ref_attention
+    T, Hq, D = q.shape
+    G = Hq // k.shape[1]
+    if cu_seqlens is None:
+        bounds = [(i * seq_len, (i + 1) * seq_len) for i in range(T // seq_len)]
+    else:
+        c = cu_seqlens.tolist()
+        bounds = list(zip(c[:-1], c[1:]))
+    outs = []
+    for (s, e) in bounds:
+        L = e - s
+        qs = q[s:e].transpose(0, 1)
+        ks = k[s:e].transpose(0, 1).repeat_interleave(G, 0)
+        vs = v[s:e].transpose(0, 1).repeat_interleave(G, 0)
+        sc = torch.matmul(qs, ks.transpose(1, 2)) * scale
+        i = torch.arange(L, device=q.device)
+        mask = torch.zeros(L, L, dtype=torch.bool, device=q.device)
+        if causal:
+            mask |= i[None, :] > i[:, None]
+        if window and window > 0:
+            mask |= i[None, :] <= i[:, None] - window
+        sc = sc.masked_fill(mask, float("-inf"))
+        outs.append(torch.matmul(torch.softmax(sc, -1), vs).transpose(0, 1))
+    return torch.cat(outs, 0), None
+
+
+def native_supported(q):
+    return native.use_native(q) and q.shape[-1] in _HEAD_DIMS_NATIVE and q.dtype == torch.bfloat16
+
+
+class _FlashAttnFn(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, cu_seqlens, seq_len, window, return_lse):
+        T, Hq, D = q.shape
+        cu, B, sl, max_len = _cu_info(cu_seqlens, T, seq_len)
+        if native_supported(q):
+            o = torch.empty(T, Hq, D, device=q.device, dtype=q.dtype)
+            lse = torch.empty(Hq, T, device=q.device, dtype=torch.float32)
+            _native_fwd(q, k, v, o, lse, causal, scale, cu, B, sl, max_len, window)
+        else:
+            o, lse = _ref_attention(q, k, v, causal, scale, cu_seqlens, seq_len, window)
+        ctx.save_for_backward(q, k, v, o, lse, cu_seqlens)
+        ctx.args = (causal, scale, seq_len, window)
+        ctx.mark_non_differentiable(lse)
+        return o, lse
+
+    @staticmethod
+    def backward(ctx, do, dlse):
+        q, k, v, o, lse, cu_seqlens = ctx.saved_tensors
+        causal, scale, seq_len, window = ctx.args
+        T = q.shape[0]
+        cu, B, sl, max_len = _cu_info(cu_seqlens, T, seq_len)
+        if native_supported(q):
+            dq = torch.empty_like(q, memory_format=torch.contiguous_format)
+            dk = torch.empty(k.shape, device=k.device, dtype=k.dtype)
+            dv = torch.empty(v.shape, device=v.device, dtype=v.dtype)
+            _native_bwd(q, k, v, o, lse, do.contiguous(), dq, dk, dv, causal, scale, cu, B, sl, max_len, window)
+        else:
+            dq, dk, dv = _ref_bwd(q, k, v, do, causal, scale, cu_seqlens, seq_len, window)
+            dq, dk, dv = dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
+        return dq, dk, dv, None, None, None, None, None, None
+
+
+def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window=0, return_lse=False):
+    """q: [B, S, Hq, D] or [T, Hq, D] (+cu_seqlens); k/v: [.., Hkv, D]. Returns o like q (and lse [Hq, T])."""
+    batched = q.dim() == 4
+    if batched:
+        B, S = q.shape[:2]
+        q3, k3, v3 = (t.reshape(B * S, t.shape[2], t.shape[3]) for t in (q, k, v))
+        seq_len = S
+    else:
+        q3, k3, v3 = q, k, v
+        seq_len = q.shape[0]
+    for t, n in ((q3, "q"), (k3, "k"), (v3, "v")):
+        _check_tok_layout(t, n)
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    o, lse = _FlashAttnFn.apply(q3, k3, v3, bool(causal), float(scale), cu_seqlens, int(seq_len), int(window or 0),
+                                return_lse)
+    if batched:
+        o = o.view(q.shape)
+    return (o, lse) if return_lse else o
+
+
+class _QKVAttnFn(torch.autograd.Function):
+    """RoPE(q,k) + attention on the packed QKV GEMM output; see module docstring."""
+
+    @staticmethod
+    def forward(ctx, qkv, n_q, n_kv, cos, sin, seq_len, causal, scale, cu_seqlens, pos_ids, window):
+        T, NH, D = qkv.shape
+        if cos is not None:
+            rope_(qkv, cos, sin, n_q + n_kv, seq_len=seq_len, pos_ids=pos_ids)  # in place on the GEMM output
+        q = qkv[:, :n_q]
+        k = qkv[:, n_q:n_q + n_kv]
+        v = qkv[:, n_q + n_kv:]
+        cu, B, sl, max_len = _cu_info(cu_seqlens, T, seq_len)
+        if native_supported(qkv):
+            o = torch.empty(T, n_q, D, device=qkv.device, dtype=qkv.dtype)
+            lse = torch.empty(n_q, T, device=qkv.device, dtype=torch.float32)
+            _native_fwd(q, k, v, o, lse, causal, scale, cu, B, sl, max_len, window)
+        else:
+            o, lse = _ref_attention(q, k, v, causal, scale, cu_seqlens, seq_len, window)
+        ctx.save_for_backward(qkv, o, lse, cos, sin, cu_seqlens, pos_ids)
+        ctx.args = (n_q, n_kv, seq_len, causal, scale, window)
+        return o.view(T, n_q * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, cos, sin, cu_seqlens, pos_ids = ctx.saved_tensors
+        n_q, n_kv, seq_len, causal, scale, window = ctx.args
+        T, NH, D = qkv.shape
+        do = do.reshape(T, n_q, D).contiguous()
+        q = qkv[:, :n_q]
+        k = qkv[:, n_q:n_q + n_kv]
+        v = qkv[:, n_q + n_kv:]
+        dqkv = torch.empty_like(qkv)
+        cu, B, sl, max_len = _cu_info(cu_seqlens, T, seq_len)
+        if native_supported(qkv):
+            _native_bwd(q, k, v, o, lse, do, dqkv[:, :n_q], dqkv[:, n_q:n_q + n_kv], dqkv[:, n_q + n_kv:], causal, scale,
+                        cu, B, sl, max_len, window)
+        else:
+            dq, dk, dv = _ref_bwd(q, k, v, do, causal, scale, cu_seqlens, seq_len, window)
+            dqkv[:, :n_q] = dq.to(qkv.dtype)
+            dqkv[:, n_q:n_q + n_kv] = dk.to(qkv.dtype)
+            dqkv[:, n_q + n_kv:] = dv.to(qkv.dtype)
+        if cos is not None:
+            rope_(dqkv, cos, sin, n_q + n_kv, seq_len=seq_len, pos_ids=pos_ids, sign=-1.0)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
+
+
+def qkv_attention(qkv, n_q, n_kv, cos=None, sin=None, seq_len=None, causal=True, softmax_scale=None, cu_seqlens=None,
+                  pos_ids=None, window=0):
+    """qkv: [T, n_q + 2*n_kv, D] (fused projection output, CONSUMED: RoPE is applied in place).
+
+    Returns the attention output flattened to [T, n_q * D] (ready for the O projection).
+    """
+    T, NH, D = qkv.shape
+    assert NH == n_q + 2 * n_kv
+    qkv = qkv if qkv.is_contiguous() else qkv.contiguous()
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    return _QKVAttnFn.apply(qkv, n_q, n_kv, cos, sin, int(seq_len or T), bool(causal), float(scale), cu_seqlens,
+                            pos_ids, int(window or 0))

@@ -1,0 +1,149 @@
+"""ctypes bindings of the in-tree native libraries.
+
+Every GPU op of the framework goes through here. On a machine with a GPU the kernel library is
+REQUIRED: ``kernels()`` raises if it is missing instead of silently falling back to eager
+PyTorch, so a test that passes on the GPU has run the HIP code. CPU tensors use the pure-torch
+reference implementations inside each op module (that is what the CPU test-suite exercises).
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+from . import build as _build
+
+_lock = threading.Lock()
+_klib = None
+_hlib = None
+
+# argument spec letters: p=void*, i=int32, l=int64, f=float, s=hipStream_t
+_KERNEL_SIGS = {
+    "hds_norm_fwd": "iii" + "p" * 8 + "ii" + "f" + "s",
+    "hds_norm_bwd_nparts": "i",
+    "hds_norm_bwd": "iii" + "p" * 9 + "i" + "pp" + "iii" + "s",
+    "hds_rope": "ii" + "pppp" + "l" + "iii" + "l" + "ii" + "f" + "s",
+    "hds_glu_fwd": "iipplis",
+    "hds_glu_bwd": "iippplis",
+    "hds_bias_act_fwd": "iippplis",
+    "hds_bias_act_bwd": "iipppplis",
+    "hds_adam_flat": "ii" + "ppppp" + "l" + "f" * 7 + "i" + "f" + "pp" + "s",
+    "hds_multi_chunk_size": "",
+    "hds_adam_multi": "ii" + "pp" + "i" + "f" * 7 + "i" + "f" + "pp" + "s",
+    "hds_lion_flat": "ii" + "pppp" + "l" + "f" * 5 + "pp" + "s",
+    "hds_adagrad_flat": "ii" + "pppp" + "l" + "f" * 4 + "pp" + "s",
+    "hds_lamb_multi": "ii" + "pp" + "i" + "p" + "f" * 10 + "pp" + "s",
+    "hds_sumsq": "iplpps",
+    "hds_clip_coef": "pffpps",
+    "hds_xent": "i" + "pppp" + "l" + "i" + "l" + "i" + "f" + "i" + "f" + "s",
+    "hds_attn_fwd": "p" * 7 + "i" * 7 + "f" + "ii" + "s",
+    "hds_attn_bwd": "p" * 12 + "i" * 7 + "f" + "ii" + "s",
+}
+
+_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}
+
+
+def _bind(lib, sigs):
+    for name, spec in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = [_CT[c] for c in spec]
+        fn.restype = ctypes.c_int
+
+
+def _gpu_present():
+    try:
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def kernel_lib_path():
+    return _build.KERNEL_LIB
+
+
+def load_kernels(build_if_missing=True):
+    """Load (building first if needed) the HIP kernel library. Returns None when unavailable."""
+    global _klib
+    if _klib is not None:
+        return _klib
+    with _lock:
+        if _klib is not None:
+            return _klib
+        path = _build.KERNEL_LIB
+        if build_if_missing and os.environ.get("HDS_NO_BUILD", "0") != "1":
+            try:
+                path = _build.build_kernels()
+            except Exception:
+                if not os.path.exists(path):
+                    raise
+        if not os.path.exists(path):
+            return None
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        _bind(lib, _KERNEL_SIGS)
+        _klib = lib
+        return _klib
+
+
+def kernels():
+    lib = load_kernels()
+    if lib is None:
+        raise RuntimeError("hcache_deepspeed_amd: native kernel library libhds_kernels.so is missing; "
+                           "run `python -m hcache_deepspeed_amd.ops.build` (refusing to fall back to eager ops on GPU)")
+    return lib
+
+
+def host_lib():
+    """Host-side C++ runtime (pinned rings, CPU optimizers, async file I/O)."""
+    global _hlib
+    if _hlib is not None:
+        return _hlib
+    with _lock:
+        if _hlib is not None:
+            return _hlib
+        path = _build.HOST_LIB
+        if os.environ.get("HDS_NO_BUILD", "0") != "1":
+            try:
+                path = _build.build_host() or path
+            except Exception:
+                if not os.path.exists(path):
+                    raise
+        if not os.path.exists(path):
+            raise RuntimeError("hcache_deepspeed_amd: host library libhds_host.so is missing")
+        from . import host_sigs
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        host_sigs.bind(lib)
+        _hlib = lib
+        return _hlib
+
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def dt(t_or_dtype):
+    d = t_or_dtype if isinstance(t_or_dtype, torch.dtype) else t_or_dtype.dtype
+    if d not in _DT:
+        raise TypeError(f"unsupported dtype {d}")
+    return _DT[d]
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(err, what):
+    if err != 0:
+        raise RuntimeError(f"hcache_deepspeed_amd: {what} failed with hipError {err}")
+
+
+def use_native(*tensors):
+    """True when the tensors live on the GPU (native path mandatory there)."""
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            return True
+    return False

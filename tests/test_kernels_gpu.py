@@ -1,0 +1,286 @@
+"""Numerics of every HIP kernel against a plain fp32 PyTorch reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from hcache_deepspeed_amd.ops import native  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert native.load_kernels() is not None, "kernel library must load on the GPU box"
+    torch.manual_seed(0)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("H", [4096, 1024, 5120, 2056])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm_fwd_bwd(H, with_res):
+    from hcache_deepspeed_amd.ops.norm import rms_norm
+    T = 777
+    x = torch.randn(T, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(T, H, device="cuda", dtype=torch.bfloat16, requires_grad=True) if with_res else None
+    w = (1 + 0.1 * torch.randn(H, device="cuda", dtype=torch.bfloat16)).requires_grad_(True)
+    out = rms_norm(x, w, 1e-5, residual=r)
+    y, h = (out if with_res else (out, None))
+    # reference
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if with_res else None
+    wr = w.detach().float().requires_grad_(True)
+    hr = (xr + rr) if with_res else xr
+    yr = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    assert _rel(y, yr) < 1e-2
+    gy = torch.randn_like(y)
+    gh = torch.randn_like(y) if with_res else None
+    if with_res:
+        torch.autograd.backward([y, h], [gy, gh])
+        torch.autograd.backward([yr, hr], [gy.float(), gh.float()])
+    else:
+        y.backward(gy)
+        yr.backward(gy.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    if with_res:
+        assert _rel(r.grad, rr.grad) < 2e-2
+
+
+def test_layernorm_fwd_bwd():
+    from hcache_deepspeed_amd.ops.norm import layer_norm
+    T, H = 513, 768
+    x = torch.randn(T, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = torch.randn(H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    y = layer_norm(x, w, b, 1e-5)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (H, ), wr, br, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    for a, bb in ((x, xr), (w, wr), (b, br)):
+        assert _rel(a.grad, bb.grad) < 2e-2
+
+
+@pytest.mark.parametrize("interleaved", [False, True])
+def test_rope_inplace_and_inverse(interleaved):
+    from hcache_deepspeed_amd.ops.rope import rope_, rope_tables
+    T, nh, D = 300, 12, 128
+    S = 100
+    cos, sin = rope_tables(4096, D, 500000.0, device="cuda")
+    x = torch.randn(T, nh + 4, D, device="cuda", dtype=torch.bfloat16)
+    ref = x.clone()
+    rope_(x, cos, sin, nh, seq_len=S, interleaved=interleaved)
+    # torch reference
+    pos = torch.arange(T, device="cuda") % S
+    c, s = cos[pos][:, None], sin[pos][:, None]
+    xf = ref[:, :nh].float()
+    if not interleaved:
+        a, b = xf[..., :D // 2], xf[..., D // 2:]
+        exp = torch.cat([a * c - b * s, b * c + a * s], -1)
+    else:
+        a, b = xf[..., 0::2], xf[..., 1::2]
+        exp = torch.stack([a * c - b * s, b * c + a * s], -1).flatten(-2)
+    assert _rel(x[:, :nh], exp) < 1e-2
+    assert torch.equal(x[:, nh:], ref[:, nh:])
+    rope_(x, cos, sin, nh, seq_len=S, sign=-1.0, interleaved=interleaved)
+    assert _rel(x, ref) < 2e-2
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh", "relu"])
+def test_glu(act):
+    from hcache_deepspeed_amd.ops.activations import glu, _ref_act, act_code
+    T, I = 333, 1024
+    gu = torch.randn(T, 2 * I, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    y = glu(gu, act)
+    gr = gu.detach().float().requires_grad_(True)
+    g, u = gr.split(I, -1)
+    yr = _ref_act(g, act_code(act)) * u
+    assert _rel(y, yr) < 1e-2
+    d = torch.randn_like(y)
+    y.backward(d)
+    yr.backward(d.float())
+    assert _rel(gu.grad, gr.grad) < 2e-2
+
+
+def test_adam_flat_matches_torch():
+    from hcache_deepspeed_amd.ops.optimizers import adam_flat
+    n = 1_000_003
+    p = torch.randn(n, device="cuda")
+    g = torch.randn(n, device="cuda", dtype=torch.bfloat16)
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    lp = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        adam_flat(p, g, m, v, step, 1e-3, (0.9, 0.95), 1e-8, 0.1, adamw=True, lp_out=lp, grad_scale=0.5)
+        ref.grad = g.float() * 0.5
+        opt.step()
+    assert (p - ref.detach()).abs().max().item() < 1e-5
+    assert torch.equal(lp, p.to(torch.bfloat16))
+
+
+def test_fused_adam_multi_tensor():
+    from hcache_deepspeed_amd.ops.optimizers import FusedAdam
+    shapes = [(1000, 37), (4096, ), (3, 5, 7), (70001, )]
+    ps = [torch.randn(s, device="cuda", requires_grad=True) for s in shapes]
+    rs = [p.detach().clone().requires_grad_(True) for p in ps]
+    opt = FusedAdam(ps, lr=1e-2, weight_decay=0.01)
+    ropt = torch.optim.AdamW(rs, lr=1e-2, weight_decay=0.01)
+    for _ in range(3):
+        for p, r in zip(ps, rs):
+            g = torch.randn_like(p)
+            p.grad, r.grad = g, g.clone()
+        opt.step()
+        ropt.step()
+    for p, r in zip(ps, rs):
+        assert (p - r).abs().max().item() < 1e-5
+
+
+def test_lion_and_lamb_run():
+    from hcache_deepspeed_amd.ops.optimizers import FusedLamb, FusedLion
+    for cls in (FusedLion, FusedLamb):
+        p = torch.randn(10000, device="cuda", requires_grad=True)
+        ref = p.detach().cpu().clone().requires_grad_(True)
+        opt, ropt = cls([p], lr=1e-3), cls([ref], lr=1e-3)
+        g = torch.randn(10000)
+        p.grad, ref.grad = g.cuda(), g.clone()
+        opt.step()
+        ropt.step()
+        assert (p.detach().cpu() - ref.detach()).abs().max().item() < 1e-5
+
+
+def test_grad_norm_and_clip():
+    from hcache_deepspeed_amd.ops.optimizers import clip_coef, grad_sumsq
+    ts = [torch.randn(12345, device="cuda", dtype=torch.bfloat16), torch.randn(999, device="cuda")]
+    fi = torch.zeros(1, device="cuda", dtype=torch.int32)
+    s = grad_sumsq(ts, found_inf=fi)
+    exp = sum((t.float()**2).sum() for t in ts)
+    assert abs(s.item() - exp.item()) / exp.item() < 1e-4
+    assert fi.item() == 0
+    c = clip_coef(s, 1.0)
+    assert abs(c.item() - min(1.0, 1.0 / (math.sqrt(exp.item()) + 1e-6))) < 1e-4
+    ts[0][7] = float("inf")
+    grad_sumsq(ts, found_inf=fi)
+    assert fi.item() == 1
+
+
+@pytest.mark.parametrize("V", [128256, 50257, 1000])
+def test_cross_entropy(V):
+    from hcache_deepspeed_amd.ops.cross_entropy import cross_entropy
+    T = 257
+    logits = (3 * torch.randn(T, V, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    tgt = torch.randint(0, V, (T, ), device="cuda")
+    tgt[::7] = -100
+    loss = cross_entropy(logits, tgt)
+    lr = logits.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, tgt, ignore_index=-100)
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1, abs(ref.item()))
+    loss.backward()
+    ref.backward()
+    assert _rel(logits.grad, lr.grad) < 2e-2
+
+
+def test_fused_linear_cross_entropy():
+    from hcache_deepspeed_amd.ops.cross_entropy import fused_linear_cross_entropy
+    T, H, V = 1000, 256, 5003
+    h = (0.5 * torch.randn(T, H, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    w = (0.05 * torch.randn(V, H, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    t = torch.randint(0, V, (T, ), device="cuda")
+    t[:10] = -100
+    loss = fused_linear_cross_entropy(h, w, t, chunk_rows=384)
+    hr, wr = h.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(hr @ wr.t(), t)
+    assert abs(loss.item() - ref.item()) < 2e-3 * abs(ref.item())
+    (2 * loss).backward()
+    (2 * ref).backward()
+    assert _rel(h.grad, hr.grad) < 3e-2
+    assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def _attn_ref(q, k, v, causal, window=0, cu=None, S=None):
+    from hcache_deepspeed_amd.ops.attention import _ref_attention_f32
+    scale = 1 / math.sqrt(q.shape[-1])
+    o, _ = _ref_attention_f32(q, k, v, causal, scale, cu, S, window)
+    return o
+
+
+@pytest.mark.parametrize("S,Hq,Hkv,causal,window", [(256, 4, 2, True, 0), (1000, 8, 2, True, 0),
+                                                     (384, 4, 4, False, 0), (700, 4, 1, True, 129),
+                                                     (64, 2, 1, True, 0), (2048, 8, 8, True, 0)])
+def test_flash_attn_fwd_bwd(S, Hq, Hkv, causal, window):
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    B, D = 2, 128
+    q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn(q, k, v, causal=causal, window=window)
+    qr, kr, vr = (t.detach().float().reshape(B * S, t.shape[2], D).requires_grad_(True) for t in (q, k, v))
+    orf = _attn_ref(qr, kr, vr, causal, window, None, S)
+    assert _rel(o.reshape(B * S, Hq, D), orf) < 1e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float().reshape(B * S, Hq, D))
+    assert _rel(q.grad.reshape(B * S, Hq, D), qr.grad) < 2e-2
+    assert _rel(k.grad.reshape(B * S, Hkv, D), kr.grad) < 2e-2
+    assert _rel(v.grad.reshape(B * S, Hkv, D), vr.grad) < 2e-2
+
+
+def test_flash_attn_varlen():
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    lens = [17, 300, 1, 129, 64]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device="cuda", dtype=torch.int32)
+    T, Hq, Hkv, D = sum(lens), 4, 2, 128
+    q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(T, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(T, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn(q, k, v, causal=True, cu_seqlens=cu)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    orf = _attn_ref(qr, kr, vr, True, 0, cu.cpu(), None)
+    assert _rel(o, orf) < 1e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        assert _rel(a.grad, b.grad) < 2e-2
+
+
+def test_flash_attn_lse_spike():
+    """Force the online-softmax rescale: one key row far larger than the rest (guide §5.4 rule 26)."""
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    B, S, H, D = 1, 512, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    k[:, 300] = q[:, 400] * 4  # spike at tile 4 for query 400
+    o, lse = flash_attn(q, k, v, causal=True, return_lse=True)
+    orf = _attn_ref(*(t.float().reshape(S, H, D) for t in (q, k, v)), True, 0, None, S)
+    assert _rel(o.reshape(S, H, D), orf) < 1e-2
+
+
+def test_qkv_attention_matches_unfused():
+    from hcache_deepspeed_amd.ops.attention import qkv_attention, flash_attn
+    from hcache_deepspeed_amd.ops.rope import apply_rotary, rope_tables
+    B, S, Hq, Hkv, D = 2, 512, 8, 2, 128
+    T = B * S
+    cos, sin = rope_tables(S, D, 500000.0, device="cuda")
+    qkv = torch.randn(T, Hq + 2 * Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    x1 = qkv.detach().clone().requires_grad_(True)
+    o1 = qkv_attention(qkv.clone(), Hq, Hkv, cos, sin, seq_len=S)
+    q = apply_rotary(x1[:, :Hq], cos, sin, seq_len=S)
+    k = apply_rotary(x1[:, Hq:Hq + Hkv], cos, sin, seq_len=S)
+    v = x1[:, Hq + Hkv:].contiguous()
+    o2 = flash_attn(q.view(B, S, Hq, D), k.view(B, S, Hkv, D), v.view(B, S, Hkv, D)).reshape(T, Hq * D)
+    assert _rel(o1, o2) < 1e-2
+    g = torch.randn_like(o1)
+    o1.backward(g)
+    o2.backward(g)
+    assert _rel(qkv.grad, x1.grad) < 2e-2
