@@ -1,0 +1,145 @@
+"""Headline benchmark: Llama-3-8B ZeRO-3 bf16 training throughput (tokens/s for the whole job).
+
+BASELINE.json metric: "tokens/sec (node) Llama-3-8B ZeRO-3 at 1/2/4/8 MI355X". The reference publishes
+no number for it (``published: {}``), so ``vs_baseline`` is null.
+
+    python bench.py --gpus 1 --steps 10 --warmup 3
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus 8 --steps 10 --warmup 3
+
+Every step is a full training step of the real 8.03B-parameter architecture (32 layers, GQA 32/8,
+vocab 128256) through ``hcache_deepspeed_amd.initialize``: forward, backward (ZeRO-3 all-gather /
+reduce-scatter), fused AdamW on the fp32 master shard. Weights are random (zero.Init, per-unit
+seeded), data is synthetic uniform token ids. Weak scaling: per-GPU micro-batch fixed as N grows.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=2)
+    ap.add_argument("--gas", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--zero", type=int, default=3)
+    ap.add_argument("--layers", type=int, default=0, help="debug only: override layer count (result is marked invalid)")
+    ap.add_argument("--prefetch", type=int, default=2)
+    ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as tdist
+
+    import hcache_deepspeed_amd as hds
+    from hcache_deepspeed_amd.models import llama
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or "RANK" in os.environ:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    else:
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=os.environ.get("MASTER_PORT", "29533"))
+    hds.init_distributed(verbose=False)
+    rank = tdist.get_rank()
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+
+    overrides = {}
+    if args.layers:
+        overrides["num_hidden_layers"] = args.layers
+    cfg_model = llama.PRESETS[args.model](**overrides)
+    ds_config = {
+        "train_micro_batch_size_per_gpu": args.micro_batch,
+        "gradient_accumulation_steps": args.gas,
+        "bf16": {"enabled": True},
+        "optimizer": {"type": "AdamW", "params": {"lr": 1e-4, "betas": [0.9, 0.95], "eps": 1e-8,
+                                                   "weight_decay": 0.1}},
+        "gradient_clipping": 1.0,
+        "zero_optimization": {"stage": args.zero},
+        "mi355x": {"zero3_prefetch_depth": args.prefetch},
+        "steps_per_print": 1000000,
+    }
+    t_init = time.time()
+    with hds.zero.Init(enabled=args.zero == 3):
+        model = llama.LlamaForCausalLM(cfg_model)
+    if args.ckpt:
+        model.gradient_checkpointing_enable()
+    engine, _, _, _ = hds.initialize(model=model, config=ds_config)
+    t_init = time.time() - t_init
+    dev = engine.device
+    S, mb = args.seq, args.micro_batch
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    batches = [torch.randint(0, cfg_model.vocab_size, (mb, S), device=dev, generator=gen) for _ in range(4)]
+
+    def train_step(i):
+        loss = None
+        for g in range(args.gas):
+            x = batches[(i * args.gas + g) % len(batches)]
+            loss = engine(x, labels=x)
+            engine.backward(loss)
+            engine.step()
+        return loss
+
+    loss = None
+    for i in range(args.warmup):
+        loss = train_step(i)
+    torch.cuda.synchronize()
+    tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = train_step(args.warmup + i)
+    torch.cuda.synchronize()
+    tdist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    tdist.all_reduce(dt_t, op=tdist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    tokens = world * mb * args.gas * S * args.steps
+    value = tokens / dt
+    ms_per_step = dt / args.steps * 1e3
+    flops = cfg_model.flops_per_token(S) * tokens
+    mfu = flops / dt / (2.5e15 * world)
+    mem = torch.cuda.max_memory_allocated(dev) / 2**30
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec (node) Llama-3-8B ZeRO-3 at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random token ids), random-init weights",
+            "config": {"model": "Llama-3-8B" if args.model == "llama3-8b" and not args.layers else
+                       f"{args.model}{'-L' + str(args.layers) if args.layers else ''}",
+                       "global_batch": world * mb * args.gas, "seq_len": S,
+                       "parallelism": f"zero{args.zero}-dp{world}", "micro_batch_per_gpu": mb, "gas": args.gas,
+                       "activation_checkpointing": bool(args.ckpt)},
+            "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
+                      "final_loss": round(float(loss.item()), 4), "peak_mem_gib": round(mem, 1),
+                      "init_s": round(t_init, 1), "valid": not bool(args.layers)},
+        }
+        print(json.dumps(out), flush=True)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,88 @@
+"""hcache_deepspeed_amd -- an MI355X-native training / serving framework with the capabilities of
+zhangzuo21/Hcache_DeepSpeed (DeepSpeed 0.16.8 + the HCache host-side hidden-state cache).
+
+Drop-in usage::
+
+    import hcache_deepspeed_amd as deepspeed
+    engine, optimizer, dataloader, lr_scheduler = deepspeed.initialize(model=model, config=ds_config)
+
+Reference parity: deepspeed/__init__.py (``initialize`` :69-230, ``add_config_arguments`` :233-281,
+``init_inference`` :284-366, ``tp_model_init`` :369-398).
+"""
+import argparse
+
+from .version import __version__, __version_major__, __version_minor__, __version_patch__  # noqa: F401
+from . import comm  # noqa: F401
+from .comm import init_distributed  # noqa: F401
+from .runtime import zero  # noqa: F401
+from .runtime.config import DeepSpeedConfig  # noqa: F401
+from .runtime.engine import DeepSpeedEngine  # noqa: F401
+from .runtime.lr_schedules import VALID_LR_SCHEDULES  # noqa: F401
+from .utils.logging import logger, log_dist  # noqa: F401
+from .runtime.activation_checkpointing import checkpointing  # noqa: F401
+
+
+def initialize(args=None, model=None, optimizer=None, model_parameters=None, training_data=None, lr_scheduler=None,
+               distributed_port=29500, mpu=None, dist_init_required=None, collate_fn=None, config=None, mesh_param=None,
+               config_params=None):
+    """Returns ``(engine, engine.optimizer, engine.training_dataloader, engine.lr_scheduler)``."""
+    assert model is not None, "deepspeed.initialize requires a model"
+    if config is None:
+        config = config_params
+    if config is None and args is not None:
+        config = getattr(args, "deepspeed_config", None)
+    init_distributed(distributed_port=distributed_port, dist_init_required=dist_init_required)
+    cfg = DeepSpeedConfig(config, mpu=mpu)
+    from .runtime.pipe.module import PipelineModule
+    if isinstance(model, PipelineModule):
+        from .runtime.pipe.engine import PipelineEngine
+        engine = PipelineEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
+                                training_data=training_data, lr_scheduler=lr_scheduler, mpu=model.mpu(),
+                                dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
+                                config_class=cfg)
+    elif (cfg.hybrid_engine or {}).get("enabled", False):
+        from .runtime.hybrid_engine import DeepSpeedHybridEngine
+        engine = DeepSpeedHybridEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
+                                       training_data=training_data, lr_scheduler=lr_scheduler, mpu=mpu,
+                                       dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
+                                       config_class=cfg)
+    else:
+        engine = DeepSpeedEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
+                                 training_data=training_data, lr_scheduler=lr_scheduler, mpu=mpu,
+                                 dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
+                                 config_class=cfg)
+    return engine, engine.optimizer, engine.training_dataloader, engine.lr_scheduler
+
+
+def _add_core_arguments(parser):
+    group = parser.add_argument_group("DeepSpeed", "DeepSpeed configurations")
+    group.add_argument("--deepspeed", default=False, action="store_true",
+                       help="Enable DeepSpeed (helper flag for user code, no impact on DeepSpeed backend)")
+    group.add_argument("--deepspeed_config", default=None, type=str, help="DeepSpeed json configuration file.")
+    group.add_argument("--deepscale", default=False, action="store_true", help=argparse.SUPPRESS)
+    group.add_argument("--deepscale_config", default=None, type=str, help=argparse.SUPPRESS)
+    return parser
+
+
+def add_config_arguments(parser):
+    return _add_core_arguments(parser)
+
+
+def default_inference_config():
+    from .inference.config import DeepSpeedInferenceConfig
+    return DeepSpeedInferenceConfig().to_dict()
+
+
+def init_inference(model, config=None, **kwargs):
+    """Inference engine (kernel injection / AutoTP analogue). kwargs override config keys."""
+    from .inference.engine import InferenceEngine
+    from .inference.config import DeepSpeedInferenceConfig
+    cfg = dict(config or {})
+    cfg.update(kwargs)
+    return InferenceEngine(model, config=DeepSpeedInferenceConfig(**cfg))
+
+
+def tp_model_init(model, tp_size, dtype, config=None, **kwargs):
+    """AutoTP training entry: shard nn.Linear layers over a tensor-parallel group of ``tp_size``."""
+    from .parallel.tp import TpTrainingManager
+    return TpTrainingManager(model=model, tp_size=tp_size, dtype=dtype).module

@@ -134,6 +134,10 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(hidden_size, dtype=dtype, device=device))
         self.eps = eps
 
+    def reset_parameters(self):
+        with torch.no_grad():
+            self.weight.fill_(1.0)
+
     def forward(self, x, residual=None):
         return rms_norm(x, self.weight, self.eps, residual)
 
@@ -145,6 +149,12 @@ class LayerNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(hidden_size, dtype=dtype, device=device))
         self.bias = nn.Parameter(torch.zeros(hidden_size, dtype=dtype, device=device)) if bias else None
         self.eps = eps
+
+    def reset_parameters(self):
+        with torch.no_grad():
+            self.weight.fill_(1.0)
+            if self.bias is not None:
+                self.bias.zero_()
 
     def forward(self, x, residual=None):
         return layer_norm(x, self.weight, self.bias, self.eps, residual)

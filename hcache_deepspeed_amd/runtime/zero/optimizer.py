@@ -1,0 +1,728 @@
+"""One flat-shard ZeRO optimizer for stages 0/1/2/3.
+
+Reference parity (behaviour, not code): runtime/zero/stage_1_and_2.py ``DeepSpeedZeroOptimizer``,
+runtime/zero/stage3.py ``DeepSpeedZeroOptimizer_Stage3``, partition_parameters.py (parameter
+partitioning / gather), partitioned_param_coordinator.py (trace-driven prefetch),
+parameter_offload.py (module hooks), runtime/bf16_optimizer.py (fp32 master for bf16).
+
+What is different by design (MI355X-first):
+
+* every stage is built on :mod:`.flat` units -- rank-major flat buffers, parameters and grads are
+  views, and the ONLY collectives are ``all_gather_into_tensor`` / ``reduce_scatter_tensor`` (stage 0:
+  ``all_reduce``) of whole units. ZeRO-1/2 use a true reduce-scatter, not per-owner reduce
+  (reference stage_1_and_2.py:1029-1154);
+* ZeRO-3 gathers on one communicator and reduce-scatters on another, so a backward-prefetch
+  all-gather and the previous block's gradient reduce-scatter run concurrently on different RCCL
+  streams (different xGMI link directions);
+* the optimizer step is a few fused-kernel launches over the rank's whole flat shard: grad-norm
+  (+overflow) kernel, one scalar all-reduce, clip coefficient on device, then Adam that also writes
+  the bf16 parameter shard -- no host synchronisation on the bf16 path;
+* at data-parallel world size 1 the gather/scatter degenerate into aliasing: parameters, their
+  gradients and the optimizer shard share storage and no copy kernel runs at all.
+"""
+import math
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+
+from ... import comm as dist
+from ...ops import optimizers as fused
+from ...utils.logging import logger, log_dist
+from ..fp16.loss_scaler import CreateLossScaler
+from .flat import AVAILABLE, INFLIGHT, NOT_AVAILABLE, FlatUnit, ShardStore
+
+_EMPTY = {}
+
+
+def _empty(dtype, device):
+    key = (dtype, str(device))
+    t = _EMPTY.get(key)
+    if t is None:
+        t = torch.empty(0, dtype=dtype, device=device)
+        _EMPTY[key] = t
+    return t
+
+
+def _optimizer_kind(opt):
+    name = type(opt).__name__.lower()
+    if name in ("fusedadam", "adam", "adamw", "deepspeedcpuadam", "cpuadam", "hybridadam"):
+        adamw = True
+        if hasattr(opt, "adam_w_mode"):
+            adamw = bool(opt.adam_w_mode)
+        elif name == "adam":
+            adamw = bool(opt.defaults.get("decoupled_weight_decay", False))
+        return "adam", adamw
+    if "lion" in name:
+        return "lion", True
+    if "adagrad" in name:
+        return "adagrad", False
+    return "generic", False
+
+
+class _PreBackward(torch.autograd.Function):
+    """Identity on a unit's outputs whose backward fires right before that unit's backward."""
+
+    @staticmethod
+    def forward(ctx, zopt, unit, *tensors):
+        ctx.zopt, ctx.unit = zopt, unit
+        return tensors if len(tensors) > 1 else tensors[0]
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ctx.zopt._pre_backward(ctx.unit)
+        return (None, None) + grads
+
+
+def discover_stage3_units(module, leaf_modules=()):
+    """ZeRO-3 fetch units: each element of top-level ModuleLists (transformer blocks) and any module
+    whose class is in ``leaf_modules``; everything else -> one root unit kept gathered for the step."""
+    units, claimed = [], set()
+    leaf_modules = tuple(leaf_modules)
+    for name, m in module.named_modules():
+        if any(name == c or name.startswith(c + ".") for c in claimed):
+            continue
+        if leaf_modules and isinstance(m, leaf_modules) and m is not module:
+            units.append((name, m))
+            claimed.add(name)
+            continue
+        if isinstance(m, nn.ModuleList):
+            for i, child in enumerate(m):
+                cname = f"{name}.{i}" if name else str(i)
+                if any(True for _ in child.parameters()):
+                    units.append((cname, child))
+                claimed.add(cname)
+    return units
+
+
+class ZeroOptimizer:
+    """Flat-shard ZeRO (stage 0 = plain DP with the same flat machinery)."""
+
+    def __init__(self, init_optimizer, module, config, stage, dp_group=None, dtype=torch.bfloat16, device=None,
+                 grad_accum_steps=1, timers=None, mpu=None, leaf_modules=(), param_names=None):
+        self.optimizer = init_optimizer
+        self.module = module
+        self.config = config
+        self.zcfg = config.zero_config
+        self.stage = int(stage)
+        self.dp_group = dp_group
+        self.dp_world = dist.get_world_size(dp_group)
+        self.dp_rank = dist.get_rank(dp_group)
+        self.dtype = dtype
+        self.device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+                                 else torch.device("cpu"))
+        self.gas = int(grad_accum_steps)
+        self.timers = timers
+        self.clip_grad = float(config.gradient_clipping or 0.0)
+        self.param_groups = init_optimizer.param_groups
+        self.kind, self.adamw = _optimizer_kind(init_optimizer)
+        self.param_names = param_names or {}
+        self.mi = config.mi355x
+
+        # loss scaling
+        ls = config.loss_scale_config
+        self.loss_scaler = CreateLossScaler(dtype, ls.loss_scale if ls.loss_scale else 1.0, ls.loss_scale == 0,
+                                            {"init_scale": 2**ls.initial_scale_power,
+                                             "scale_window": ls.loss_scale_window,
+                                             "delayed_shift": ls.hysteresis,
+                                             "consecutive_hysteresis": ls.consecutive_hysteresis,
+                                             "min_scale": ls.min_loss_scale})
+        self.overflow = False
+
+        # dtypes
+        acc = config.grad_accum_dtype
+        if acc is None:
+            self.grad_acc_dtype = torch.float32 if (self.gas > 1 or dtype == torch.float16) else dtype
+        else:
+            self.grad_acc_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[acc]
+        cd = config.communication_data_type
+        self.comm_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16, None: dtype}[cd]
+
+        # communicators: all-gather and reduce-scatter on separate RCCL streams for ZeRO-3
+        self.ag_group = dp_group
+        self.rs_group = dp_group
+        if self.stage == 3 and self.dp_world > 1:
+            ranks = (list(range(dist.get_world_size())) if dp_group is None else
+                     torch.distributed.get_process_group_ranks(dp_group))
+            self.ag_group = dist.new_group(ranks=ranks)
+            self.rs_group = dist.new_group(ranks=ranks)
+
+        self._build_units(leaf_modules)
+        self._build_store()
+        self._install_hooks()
+        self.micro_in_window = 0
+        self.boundary = True
+        self.in_backward = False
+        self.pending_works = []
+        self.global_norm = None
+        self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._inf_buf = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._coef_buf = torch.ones(1, dtype=torch.float32, device=self.device)
+        self._fwd_trace, self._trace_ok, self._trace_pos = [], False, 0
+        self._recording = True
+        self.prefetch_depth = max(0, int(self.mi.zero3_prefetch_depth))
+        nparams = sum(u.numel for u in self.units)
+        log_dist(f"ZeRO stage {self.stage}: {len(self.units)} flat units, {nparams / 1e6:.1f}M params, "
+                 f"dp={self.dp_world}, shard={self.store.numel / 1e6:.1f}M elems, optimizer={self.kind}", ranks=[0])
+
+    # ------------------------------------------------------------------------------------
+    # construction
+    # ------------------------------------------------------------------------------------
+    def _group_of(self):
+        g = {}
+        for gi, group in enumerate(self.param_groups):
+            for p in group["params"]:
+                g[id(p)] = gi
+        return g
+
+    def _build_units(self, leaf_modules):
+        group_of = self._group_of()
+        params_all = [p for group in self.param_groups for p in group["params"]]
+        layout_world = 1 if self.stage == 0 else self.dp_world
+        layout_rank = 0 if self.stage == 0 else self.dp_rank
+        self.layout_world, self.layout_rank = layout_world, layout_rank
+        units = []
+        if self.stage == 3:
+            cands = discover_stage3_units(self.module, leaf_modules)
+            count = {}
+            for _, m in cands:
+                for p in m.parameters():
+                    count[id(p)] = count.get(id(p), 0) + 1
+            claimed = set()
+            for name, m in cands:
+                ps = [p for p in m.parameters() if id(p) in group_of and count[id(p)] == 1 and id(p) not in claimed]
+                if not ps:
+                    continue
+                for p in ps:
+                    claimed.add(id(p))
+                u = FlatUnit(len(units), ps, [group_of[id(p)] for p in ps], layout_world, layout_rank, name)
+                u.module = m
+                units.append(u)
+            rest = [p for p in params_all if id(p) not in claimed]
+            if rest:
+                root = FlatUnit(len(units), rest, [group_of[id(p)] for p in rest], layout_world, layout_rank, "root")
+                root.module = self.module
+                root.persistent = True
+                units.append(root)
+        else:
+            if "reduce_bucket_size" in (self.config.raw.get("zero_optimization") or {}):
+                bucket = int(self.zcfg.reduce_bucket_size)
+            else:
+                bucket = int(self.mi.xgmi_bucket_mb * 2**20 // torch.tensor([], dtype=self.dtype).element_size())
+            # buckets from the end of the parameter list: they complete first in backward
+            for gi, group in enumerate(self.param_groups):
+                cur, size = [], 0
+                for p in reversed(group["params"]):
+                    cur.append(p)
+                    size += p.numel()
+                    if size >= bucket:
+                        units.append(FlatUnit(len(units), cur, [gi] * len(cur), layout_world, layout_rank,
+                                              f"bucket{len(units)}"))
+                        cur, size = [], 0
+                if cur:
+                    units.append(FlatUnit(len(units), cur, [gi] * len(cur), layout_world, layout_rank,
+                                          f"bucket{len(units)}"))
+            for u in units:
+                u.persistent = True
+        self.units = units
+        self.param_to_unit = {}
+        for u in units:
+            for i, p in enumerate(u.params):
+                self.param_to_unit[id(p)] = (u, i)
+                p.ds_shape = u.shapes[i]
+                p.ds_numel = u.numels[i]
+                p.ds_id = id(p)
+        self.root_units = [u for u in units if u.persistent]
+
+    def _build_store(self):
+        dev = self.device
+        self.store = ShardStore(self.units, self.dtype, dev, self.grad_acc_dtype)
+        self.direct_grads = (self.layout_world == 1 and self.grad_acc_dtype == self.dtype)
+        from .partition_parameters import materialize_unit
+        with torch.no_grad():
+            for u in self.units:
+                repl = materialize_unit(u, dev, self.dtype, seed=int(self.config.seed or 1234) + 7919 * u.uid)
+                if repl:
+                    self._swap_params(u, repl)
+                lp = self.store.lp_slice(u)
+                if self.layout_world == 1:
+                    full = lp  # alias: parameters live in the optimizer's lp shard
+                    u.copy_params_into(full)
+                else:
+                    full = torch.empty(u.padded, dtype=self.dtype, device=dev)
+                    u.copy_params_into(full)
+                    lp.copy_(full[u.rank * u.shard:(u.rank + 1) * u.shard])
+                u.shard_tensor = lp
+                for p in u.params:
+                    p.ds_tensor = lp
+                if u.persistent or self.layout_world == 1:
+                    u.full = full
+                    u.bind_params(full)
+                    u.status = AVAILABLE
+                else:
+                    u.full = None
+                    u.unbind_params(_empty(self.dtype, dev))
+                    u.status = NOT_AVAILABLE
+                    del full
+                if u.persistent or self.layout_world == 1:
+                    if self.direct_grads:
+                        u.grad_full = self.store.grad_slice(u)
+                    else:
+                        u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=dev)
+                    u.bind_grads(u.grad_full)
+            self.store.master = self.store.lp.float()
+            self._init_states()
+        for p in (p for u in self.units for p in u.params):
+            p.ds_status = self.param_to_unit[id(p)][0].status
+            p._hds_zero = self
+
+    def _swap_params(self, u, repl):
+        """Replace materialised meta parameters everywhere this optimizer references them."""
+        for i, p in enumerate(u.params):
+            if id(p) in repl:
+                new = repl[id(p)]
+                for attr in ("ds_shape", "ds_numel"):
+                    setattr(new, attr, getattr(p, attr))
+                new.ds_id = id(new)
+                self.param_to_unit.pop(id(p), None)
+                self.param_to_unit[id(new)] = (u, i)
+                if id(p) in self.param_names:
+                    self.param_names[id(new)] = self.param_names.pop(id(p))
+                u.params[i] = new
+        for group in self.param_groups:
+            group["params"] = [repl.get(id(p), p) for p in group["params"]]
+
+    def _init_states(self):
+        s = self.store
+        if self.kind == "adam":
+            s.states["exp_avg"] = torch.zeros_like(s.master)
+            s.states["exp_avg_sq"] = torch.zeros_like(s.master)
+        elif self.kind == "lion":
+            s.states["exp_avg"] = torch.zeros_like(s.master)
+        elif self.kind == "adagrad":
+            s.states["sum"] = torch.zeros_like(s.master)
+        else:
+            # generic torch optimizer over fp32 master segments (one nn.Parameter per segment)
+            groups = []
+            self._generic_params = []
+            for gi, group in enumerate(self.param_groups):
+                segs = [sg for sg in s.segments if sg.group == gi]
+                ps = []
+                for sg in segs:
+                    mp = nn.Parameter(s.seg(s.master, sg))
+                    ps.append(mp)
+                    self._generic_params.append((mp, sg))
+                hp = {k: v for k, v in group.items() if k != "params"}
+                groups.append(dict(params=ps, **hp))
+            self._generic_opt = type(self.optimizer)(groups, **self.optimizer.defaults)
+
+    # ------------------------------------------------------------------------------------
+    # hooks
+    # ------------------------------------------------------------------------------------
+    def _install_hooks(self):
+        self._hook_handles = []
+        for u in self.units:
+            for p in u.params:
+                if p.requires_grad:
+                    self._hook_handles.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
+        if self.stage == 3:
+            for u in self.units:
+                if u.persistent or u.module is None:
+                    continue
+                self._hook_handles.append(u.module.register_forward_pre_hook(self._make_pre_fwd(u)))
+                self._hook_handles.append(u.module.register_forward_hook(self._make_post_fwd(u)))
+
+    def _make_grad_hook(self, u):
+
+        def hook(p):
+            u.pending -= 1
+            if u.pending == 0 and not u.grads_reduced:
+                self._unit_grads_ready(u)
+
+        return hook
+
+    def _make_pre_fwd(self, u):
+
+        def pre(module, args):
+            self._record_and_prefetch(u)
+            self._gather(u, wait=True)
+
+        return pre
+
+    def _make_post_fwd(self, u):
+
+        def post(module, args, output):
+            grad_on = torch.is_grad_enabled()
+            if grad_on and not self.in_backward:
+                output = self._wrap_outputs(u, output)
+            if self.layout_world > 1 and not self.in_backward and not self._is_last_in_trace(u):
+                self._release(u)
+            return output
+
+        return post
+
+    def _wrap_outputs(self, u, output):
+        if isinstance(output, torch.Tensor):
+            if output.requires_grad:
+                return _PreBackward.apply(self, u, output)
+            return output
+        if isinstance(output, (tuple, list)):
+            idx = [i for i, t in enumerate(output) if isinstance(t, torch.Tensor) and t.requires_grad]
+            if not idx:
+                return output
+            wrapped = _PreBackward.apply(self, u, *[output[i] for i in idx])
+            if len(idx) == 1:
+                wrapped = (wrapped, )
+            out = list(output)
+            for j, i in enumerate(idx):
+                out[i] = wrapped[j]
+            return type(output)(out) if isinstance(output, tuple) else out
+        if isinstance(output, dict):
+            keys = [k for k, t in output.items() if isinstance(t, torch.Tensor) and t.requires_grad]
+            if not keys:
+                return output
+            wrapped = _PreBackward.apply(self, u, *[output[k] for k in keys])
+            if len(keys) == 1:
+                wrapped = (wrapped, )
+            out = type(output)(output)
+            for k, w in zip(keys, wrapped):
+                out[k] = w
+            return out
+        return output
+
+    # ------------------------------------------------------------------------------------
+    # gather / release (ZeRO-3)
+    # ------------------------------------------------------------------------------------
+    def _gather(self, u, wait=True):
+        if u.status == NOT_AVAILABLE:
+            full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
+            u.work = dist.all_gather_into_tensor(full, u.shard_tensor, group=self.ag_group, async_op=True)
+            u.full = full
+            u.bind_params(full)
+            u.status = INFLIGHT
+        if wait and u.status == INFLIGHT:
+            u.work.wait()
+            u.work = None
+            u.status = AVAILABLE
+        if self.in_backward and u.grad_full is None and u.requires_grad_count:
+            u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=self.device)
+            u.bind_grads(u.grad_full)
+
+    def _release(self, u):
+        if u.persistent or self.layout_world == 1 or u.status == NOT_AVAILABLE:
+            return
+        if u.status == INFLIGHT:
+            u.work.wait()
+            u.work = None
+        u.unbind_params(_empty(self.dtype, self.device))
+        u.full = None
+        u.status = NOT_AVAILABLE
+
+    def _record_and_prefetch(self, u):
+        if self.in_backward or self.layout_world == 1:
+            return
+        if self._recording:
+            self._fwd_trace.append(u.uid)
+            return
+        t = self._fwd_trace
+        if self._trace_ok and self._trace_pos < len(t) and t[self._trace_pos] == u.uid:
+            for j in range(self._trace_pos + 1, min(len(t), self._trace_pos + 1 + self.prefetch_depth)):
+                self._gather(self.units[t[j]], wait=False)
+        else:
+            self._trace_ok = False
+        self._trace_pos += 1
+
+    def _is_last_in_trace(self, u):
+        return bool(self._fwd_trace) and not self._recording and self._fwd_trace[-1] == u.uid
+
+    def _pre_backward(self, u):
+        self._gather(u, wait=True)
+        if self.layout_world > 1 and self._fwd_trace and not self._recording:
+            t = self._fwd_trace
+            try:
+                i = len(t) - 1 - t[::-1].index(u.uid)
+            except ValueError:
+                return
+            for j in range(i - 1, max(-1, i - 1 - self.prefetch_depth), -1):
+                self._gather(self.units[t[j]], wait=False)
+
+    # ------------------------------------------------------------------------------------
+    # gradient reduction
+    # ------------------------------------------------------------------------------------
+    def _unit_grads_ready(self, u):
+        u.grads_reduced = True
+        if self.stage == 0:
+            if not self.boundary:
+                return  # grads keep accumulating in the unit buffer until the boundary
+            w = dist.all_reduce(u.grad_full, group=self.dp_group, async_op=True)
+            post = None
+            if not self.direct_grads:
+                post = (lambda d=self.store.grad_slice(u), g=u.grad_full: d.copy_(g))
+            self.pending_works.append((w, post))
+            return
+        if self.stage == 1 and not self.boundary:
+            return
+        if self.direct_grads:
+            return  # grads already accumulated in place inside the optimizer shard
+        dst = self.store.grad_slice(u)
+        first = self.micro_in_window == 0 or self.stage == 1
+        src = u.grad_full if u.grad_full.dtype == self.comm_dtype else u.grad_full.to(self.comm_dtype)
+        if first and dst.dtype == self.comm_dtype:
+            w = dist.reduce_scatter_tensor(dst, src, group=self.rs_group, async_op=True)
+            post = None
+        else:
+            tmp = torch.empty(u.shard, dtype=self.comm_dtype, device=self.device)
+            w = dist.reduce_scatter_tensor(tmp, src, group=self.rs_group, async_op=True)
+            if first:
+                post = (lambda d=dst, t=tmp: d.copy_(t))
+            else:
+                post = (lambda d=dst, t=tmp: d.add_(t))
+        keep = (src, )
+        if self.stage == 3 and not u.persistent and self.layout_world > 1:
+            gf = u.grad_full
+            u.unbind_grads()
+            u.grad_full = None
+            keep = (src, gf, u.full)
+            self._release(u)
+        self.pending_works.append((w, post, keep))
+
+    def prepare_backward(self, boundary):
+        self.boundary = boundary
+        self.in_backward = True
+        for u in self.units:
+            u.pending = u.requires_grad_count
+            u.grads_reduced = False
+            if self.stage in (1, 2, 0) and not self.direct_grads and u.grad_full is not None:
+                u.bind_grads(u.grad_full)
+            elif self.direct_grads:
+                u.bind_grads(u.grad_full)
+
+    def finish_backward(self):
+        for u in self.units:
+            if not u.grads_reduced and u.requires_grad_count:
+                if u.grad_full is None and self.stage == 3:
+                    # unit never ran backward (unused): contribute zeros so collectives stay matched
+                    self._gather(u, wait=True)
+                self._unit_grads_ready(u)
+        for item in self.pending_works:
+            w, post = item[0], item[1]
+            w.wait()
+            if post is not None:
+                post()
+        self.pending_works = []
+        if self.stage in (2, 3) and not self.direct_grads:
+            # the per-micro-step reduction consumed these; persistent buffers restart from zero
+            for u in self.units:
+                if u.grad_full is not None:
+                    u.grad_full.zero_()
+        if self.stage == 3 and self.layout_world > 1:
+            for u in self.units:
+                if not u.persistent:
+                    self._release(u)
+        self.in_backward = False
+        self.micro_in_window += 1
+        if self._recording and self._fwd_trace:
+            self._recording = False
+            self._trace_ok = True
+
+    # ------------------------------------------------------------------------------------
+    # forward bracket (called by the engine around module.forward)
+    # ------------------------------------------------------------------------------------
+    def pre_forward(self):
+        self._trace_pos = 0
+        self._trace_ok = bool(self._fwd_trace) and not self._recording
+        for u in self.root_units:
+            self._gather(u, wait=True)
+
+    def post_forward(self):
+        pass
+
+    # ------------------------------------------------------------------------------------
+    # engine API
+    # ------------------------------------------------------------------------------------
+    def backward(self, loss, retain_graph=False):
+        scaled = loss * self.loss_scaler.loss_scale if self.loss_scaler.loss_scale != 1.0 else loss
+        scaled.backward(retain_graph=retain_graph)
+
+    @property
+    def loss_scale(self):
+        return self.loss_scaler.loss_scale
+
+    @property
+    def cur_scale(self):
+        return self.loss_scaler.loss_scale
+
+    def zero_grad(self, set_to_none=True):
+        self.store.grad.zero_()
+        for u in self.units:
+            if u.grad_full is not None and not self.direct_grads:
+                u.grad_full.zero_()
+        self.micro_in_window = 0
+
+    def _seg_group(self, seg):
+        return self.param_groups[seg.group]
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        s = self.store
+        inv = 1.0 / (self.layout_world_for_avg() * self.loss_scaler.loss_scale)
+        self._norm_buf.zero_()
+        self._inf_buf.zero_()
+        fused.grad_sumsq([s.grad], out=self._norm_buf, found_inf=self._inf_buf)
+        if self.dp_world > 1 and self.stage > 0:
+            dist.all_reduce(self._norm_buf, group=self.dp_group)
+            if self.loss_scaler.dynamic:
+                dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.dp_group)
+        coef = fused.clip_coef(self._norm_buf, self.clip_grad, inv, coef=self._coef_buf)
+        self.global_norm = self._norm_buf  # sqrt applied lazily in get_global_norm
+        self._norm_scale = inv
+        if self.loss_scaler.dynamic:
+            self.overflow = bool(self._inf_buf.item())
+            self.loss_scaler.update_scale(self.overflow)
+            if self.overflow:
+                log_dist(f"overflow: skipping step, loss scale -> {self.loss_scaler.loss_scale}", ranks=[0])
+                self.zero_grad()
+                return False
+        found_inf = self._inf_buf if self.loss_scaler.dynamic else None
+        for gi, group in enumerate(self.param_groups):
+            group["step"] = group.get("step", 0) + 1
+        if self.kind == "generic":
+            for mp, sg in self._generic_params:
+                mp.grad = s.seg(s.grad, sg).float() * coef
+            self._generic_opt.step()
+            s.lp.copy_(s.master)
+        else:
+            for sg in s.segments:
+                g = self._seg_group(sg)
+                p32, gr, lp = s.seg(s.master, sg), s.seg(s.grad, sg), s.seg(s.lp, sg)
+                if self.kind == "adam":
+                    fused.adam_flat(p32, gr, s.seg(s.states["exp_avg"], sg), s.seg(s.states["exp_avg_sq"], sg),
+                                    g["step"], g["lr"], tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
+                                    g.get("weight_decay", 0.0), self.adamw, g.get("bias_correction", True),
+                                    lp_out=lp, grad_scale=1.0, dev_scale=coef, found_inf=found_inf)
+                elif self.kind == "lion":
+                    fused.lion_flat(p32, gr, s.seg(s.states["exp_avg"], sg), g["lr"],
+                                    tuple(g.get("betas", (0.9, 0.99))), g.get("weight_decay", 0.0), lp_out=lp,
+                                    dev_scale=coef, found_inf=found_inf)
+                elif self.kind == "adagrad":
+                    fused.adagrad_flat(p32, gr, s.seg(s.states["sum"], sg), g["lr"], g.get("eps", 1e-10),
+                                       g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
+        self._post_step_gather()
+        self.zero_grad()
+        return True
+
+    def layout_world_for_avg(self):
+        return self.dp_world
+
+    def _post_step_gather(self):
+        """ZeRO-1/2: rebuild the persistent full parameters from the updated shards."""
+        if self.layout_world == 1 or self.stage == 3:
+            return
+        works = []
+        for u in self.units:
+            works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor, group=self.dp_group, async_op=True))
+        for w in works:
+            w.wait()
+
+    def get_global_norm(self):
+        if self.global_norm is None:
+            return None
+        return (self.global_norm.sqrt() * self._norm_scale).item()
+
+    # ------------------------------------------------------------------------------------
+    # state (checkpointing)
+    # ------------------------------------------------------------------------------------
+    def layout(self):
+        """Shard layout metadata written next to optimizer states (used by zero_to_fp32/universal)."""
+        units = []
+        for u in self.units:
+            units.append({
+                "name": u.name,
+                "params": [self.param_names.get(id(p), f"param_{id(p)}") for p in u.params],
+                "shapes": [list(s) for s in u.shapes],
+                "offsets": list(u.offsets),
+                "numels": list(u.numels),
+                "shard": u.shard,
+                "padded": u.padded,
+                "store_off": u.store_off,
+            })
+        return {"stage": self.stage, "world": self.layout_world, "rank": self.layout_rank, "units": units,
+                "store_numel": self.store.numel}
+
+    def state_dict(self):
+        s = self.store
+        sd = OrderedDict()
+        sd["loss_scaler"] = self.loss_scaler.state_dict()
+        sd["dynamic_loss_scale"] = self.loss_scaler.dynamic
+        sd["overflow"] = self.overflow
+        sd["clip_grad"] = self.clip_grad
+        sd["zero_stage"] = self.stage
+        sd["partition_count"] = self.layout_world
+        sd["param_groups"] = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
+        sd["optimizer_kind"] = self.kind
+        sd["fp32_flat_shard"] = s.master.detach().cpu()
+        sd["optimizer_states"] = {k: v.detach().cpu() for k, v in s.states.items()}
+        if self.kind == "generic":
+            sd["base_optimizer_state"] = self._generic_opt.state_dict()
+        sd["layout"] = self.layout()
+        sd["ds_version"] = "hds-0.1"
+        return sd
+
+    def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
+        s = self.store
+        assert sd["layout"]["store_numel"] == s.numel, "checkpoint shard layout mismatch (different world size?)"
+        self.loss_scaler.load_state_dict(sd["loss_scaler"])
+        for g, saved in zip(self.param_groups, sd["param_groups"]):
+            for k, v in saved.items():
+                g[k] = v
+        with torch.no_grad():
+            if load_from_fp32_weights:
+                s.master.copy_(sd["fp32_flat_shard"].to(s.master.device))
+                s.lp.copy_(s.master)
+            if load_optimizer_states:
+                for k, v in sd["optimizer_states"].items():
+                    if k in s.states:
+                        s.states[k].copy_(v.to(s.states[k].device))
+                if self.kind == "generic" and "base_optimizer_state" in sd:
+                    self._generic_opt.load_state_dict(sd["base_optimizer_state"])
+        self._post_step_gather()
+
+    def refresh_fp32_from_lp(self):
+        with torch.no_grad():
+            for u in self.units:
+                if u.full is not None and self.layout_world > 1 and u.status == AVAILABLE:
+                    self.store.lp_slice(u).copy_(u.full[u.rank * u.shard:(u.rank + 1) * u.shard])
+            self.store.master.copy_(self.store.lp)
+
+    # ------------------------------------------------------------------------------------
+    # full-parameter access
+    # ------------------------------------------------------------------------------------
+    def gather_all(self):
+        for u in self.units:
+            self._gather(u, wait=True)
+
+    def release_all(self):
+        for u in self.units:
+            self._release(u)
+
+    def full_fp32_state_dict(self, names):
+        """Consolidated fp32 weights {name: tensor} on every rank (all-gathers the master shards)."""
+        out = {}
+        for u in self.units:
+            m = self.store.master[u.store_off:u.store_off + u.shard]
+            full = torch.empty(u.padded, dtype=torch.float32, device=self.device)
+            if self.layout_world > 1:
+                dist.all_gather_into_tensor(full, m, group=self.dp_group)
+            else:
+                full.copy_(m)
+            for i, p in enumerate(u.params):
+                out[names.get(id(p), f"param_{id(p)}")] = u.param_view(full, i).detach().cpu().clone()
+        return out
+
+
+class DeepSpeedZeroOptimizer(ZeroOptimizer):
+    """Name-compatible alias for ZeRO-1/2 (reference runtime/zero/stage_1_and_2.py:110)."""
+
+
+class DeepSpeedZeroOptimizer_Stage3(ZeroOptimizer):
+    """Name-compatible alias for ZeRO-3 (reference runtime/zero/stage3.py:124)."""
