@@ -29,14 +29,14 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 
 // Stage a 64-row x 128-col bf16 tile into LDS with LDS-DMA. `row_ptr(row)` gives the global
 // address of logical row `row` (already clamped by the caller). 16 wave-instructions of 1 KiB,
-// 4 per wave for a 256-thread block.
-template <typename RowPtr>
+// 16/NW per wave for an NW-wave block.
+template <int NW = 4, typename RowPtr>
 __device__ __forceinline__ void stage_tile64(char* lds_tile, RowPtr row_ptr) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = w * 4 + i;
+  for (int i = 0; i < 16 / NW; ++i) {
+    const int n = w * (16 / NW) + i;
     const int row = 4 * n + (lane >> 4);
     const int pc = lane & 15;
     const int ch = pc ^ swz(row);

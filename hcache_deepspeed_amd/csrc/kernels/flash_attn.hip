@@ -25,9 +25,8 @@ using namespace hds::attn;
 namespace {
 
 constexpr int D = 128;
-constexpr int BM = 128;  // query rows per workgroup (fwd, dq)
 constexpr int BN = 64;   // keys per LDS tile (fwd, dq) / query rows per tile (dkdv)
-constexpr int BK = 128;  // keys per workgroup (dkdv)
+// query rows per workgroup (fwd, dq) = 32 * NW ; keys per workgroup (dkdv) = 32 * NW
 constexpr float kLog2e = 1.4426950408889634f;
 
 struct AttnParams {
@@ -71,7 +70,9 @@ __device__ __forceinline__ bool masked(const AttnParams& p, int qi, int kj, int 
 // =====================================================================================
 // forward
 // =====================================================================================
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
+  constexpr int BM = 32 * NW;
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
   const int b = blockIdx.z, hq = blockIdx.y;
   int start, len;
@@ -128,8 +129,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
 
   const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
 
-  stage_tile64(smem + 0, kptr(kt_begin));
-  stage_tile64(smem + 2 * 16384, vptr(kt_begin));
+  stage_tile64<NW>(smem + 0, kptr(kt_begin));
+  stage_tile64<NW>(smem + 2 * 16384, vptr(kt_begin));
   __syncthreads();
 
   for (int kt = kt_begin; kt < kt_end; ++kt) {
@@ -137,8 +138,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
     char* Kt = smem + buf * 16384;
     char* Vt = smem + 2 * 16384 + buf * 16384;
     if (kt + 1 < kt_end) {
-      stage_tile64(smem + (buf ^ 1) * 16384, kptr(kt + 1));
-      stage_tile64(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
+      stage_tile64<NW>(smem + (buf ^ 1) * 16384, kptr(kt + 1));
+      stage_tile64<NW>(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
     }
     const int k0 = kt * BN;
     // wave-uniform skip of fully masked tiles
@@ -181,8 +182,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
       rs += __shfl_xor(rs, 32, 64);
       l = l * alpha + rs;
       m = mnew;
+      if (__any(alpha != 1.f)) {  // running max moved for some row of this wave: rescale O
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+      }
       bf16x8 pb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
@@ -239,7 +242,9 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams p) {
 // =====================================================================================
 // backward dK, dV
 // =====================================================================================
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
+  constexpr int BK = 32 * NW;
   // LDS: Q[2] (16K each), dO[2] (16K each), lse[2][64], delta[2][64]
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + 4 * 256];
   const int b = blockIdx.z, hk = blockIdx.y;
@@ -292,12 +297,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
     char* Ot = smem + 2 * 16384 + buf * 16384;
     float* Lt = reinterpret_cast<float*>(smem + 4 * 16384 + buf * 256);
     float* Dt = reinterpret_cast<float*>(smem + 4 * 16384 + 512 + buf * 256);
-    stage_tile64(Qt, [=](int row) {
+    stage_tile64<NW>(Qt, [=](int row) {
       int r = qt * BN + row;
       r = r < len ? r : len - 1;
       return p.q + (int64_t)(start + r) * p.sq + (int64_t)hq * D;
     });
-    stage_tile64(Ot, [=](int row) {
+    stage_tile64<NW>(Ot, [=](int row) {
       int r = qt * BN + row;
       r = r < len ? r : len - 1;
       return p.dout + (int64_t)(start + r) * p.sdo + (int64_t)hq * D;
@@ -381,7 +386,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 // =====================================================================================
 // backward dQ
 // =====================================================================================
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnParams p) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
+  constexpr int BM = 32 * NW;
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
   const int b = blockIdx.z, hq = blockIdx.y;
   int start, len;
@@ -438,16 +445,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnParams p) {
   for (int i = 0; i < 4; ++i) dq[i] = f32x16{};
   const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
 
-  stage_tile64(smem + 0, kptr(kt_begin));
-  stage_tile64(smem + 2 * 16384, vptr(kt_begin));
+  stage_tile64<NW>(smem + 0, kptr(kt_begin));
+  stage_tile64<NW>(smem + 2 * 16384, vptr(kt_begin));
   __syncthreads();
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = (kt - kt_begin) & 1;
     const char* Kt = smem + buf * 16384;
     const char* Vt = smem + 2 * 16384 + buf * 16384;
     if (kt + 1 < kt_end) {
-      stage_tile64(smem + (buf ^ 1) * 16384, kptr(kt + 1));
-      stage_tile64(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
+      stage_tile64<NW>(smem + (buf ^ 1) * 16384, kptr(kt + 1));
+      stage_tile64<NW>(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
     }
     const int k0 = kt * BN;
     bool skip = (k0 >= len) || (wq_lo >= len);
@@ -530,6 +537,16 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 }  // namespace
 
+int g_fwd_nw = 8, g_dkdv_nw = 4, g_dq_nw = 8;
+
+// runtime selection of the waves-per-workgroup variants (4 or 8)
+HDS_EXPORT int hds_attn_config(int fwd_nw, int dkdv_nw, int dq_nw) {
+  if (fwd_nw == 4 || fwd_nw == 8) g_fwd_nw = fwd_nw;
+  if (dkdv_nw == 4 || dkdv_nw == 8) g_dkdv_nw = dkdv_nw;
+  if (dq_nw == 4 || dq_nw == 8) g_dq_nw = dq_nw;
+  return 0;
+}
+
 // strides: int64[8] token strides (elements) for q, k, v, o, dout, dq, dk, dv
 // max_len: max sequence length in the batch (grid sizing)
 HDS_EXPORT int hds_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int64_t* strides,
@@ -538,8 +555,10 @@ HDS_EXPORT int hds_attn_fwd(const void* q, const void* k, const void* v, void* o
   if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
   AttnParams p = make_params(q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, strides, cu_seqlens, batch,
                              seq_len, total_tokens, hq, hkv, scale, causal, window);
-  dim3 grid((max_len + BM - 1) / BM, hq, batch), block(256);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, block, 0, st, p);
+  if (g_fwd_nw == 8)
+    hipLaunchKernelGGL(attn_fwd_kernel<8>, dim3((max_len + 255) / 256, hq, batch), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<4>, dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
   return hipGetLastError();
 }
 
@@ -552,7 +571,13 @@ HDS_EXPORT int hds_attn_bwd(const void* q, const void* k, const void* v, const v
                              seq_len, total_tokens, hq, hkv, scale, causal, window);
   const int64_t rows = (int64_t)total_tokens * hq;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, st, p);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((max_len + BK - 1) / BK, hkv, batch), dim3(256), 0, st, p);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((max_len + BM - 1) / BM, hq, batch), dim3(256), 0, st, p);
+  if (g_dkdv_nw == 8)
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<8>, dim3((max_len + 255) / 256, hkv, batch), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<4>, dim3((max_len + 127) / 128, hkv, batch), dim3(256), 0, st, p);
+  if (g_dq_nw == 8)
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<8>, dim3((max_len + 255) / 256, hq, batch), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<4>, dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
   return hipGetLastError();
 }

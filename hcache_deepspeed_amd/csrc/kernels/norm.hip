@@ -308,16 +308,24 @@ __global__ __launch_bounds__(256) void norm_bwd_generic(const T* __restrict__ dy
   }
 }
 
-// partial [nparts, cols] fp32 -> out[cols] (dtype WT), optionally accumulated into out
+// partial [nparts, cols] fp32 -> out[cols] (dtype WT), optionally accumulated into out.
+// Block = 64 columns x 4 part-groups: coalesced 256-B rows per wave, LDS combine of the 4 groups.
 template <typename WT>
 __global__ __launch_bounds__(256) void reduce_parts_kernel(const float* __restrict__ part, WT* __restrict__ out,
                                                            int nparts, int cols, int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int pg = threadIdx.x >> 6;
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * cols + c];
-  if (accumulate) s += to_f(out[c]);
-  out[c] = from_f<WT>(s);
+  if (c < cols)
+    for (int p = pg; p < nparts; p += 4) s += part[(int64_t)p * cols + c];
+  red[pg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (pg == 0 && c < cols) {
+    float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (accumulate) t += to_f(out[c]);
+    out[c] = from_f<WT>(t);
+  }
 }
 
 template <typename T, typename WT, bool LN>
@@ -362,7 +370,7 @@ hipError_t launch_bwd(const void* dy, const void* h, const void* dres, const voi
     case 8192: args(norm_bwd_kernel<T, WT, 16, LN>); break;
     default: args(norm_bwd_generic<T, WT, LN>); break;
   }
-  dim3 rg((cols + 255) / 256);
+  dim3 rg((cols + 63) / 64);
   if (dw) hipLaunchKernelGGL(reduce_parts_kernel<WT>, rg, block, 0, st, dw_part, (WT*)dw, nparts, cols, accumulate);
   if (LN && db) hipLaunchKernelGGL(reduce_parts_kernel<WT>, rg, block, 0, st, db_part, (WT*)db, nparts, cols, accumulate);
   return hipGetLastError();
@@ -391,7 +399,7 @@ HDS_EXPORT int hds_norm_fwd(int is_ln, int dtype, int wdtype, const void* x, con
 
 HDS_EXPORT int hds_norm_bwd_nparts(int rows) {
   int n = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
-  return n < 1024 ? (n < 1 ? 1 : n) : 1024;
+  return n < 512 ? (n < 1 ? 1 : n) : 512;  // 512 partial rows: 8 waves/CU, small reduce
 }
 
 HDS_EXPORT int hds_norm_bwd(int is_ln, int dtype, int wdtype, const void* dy, const void* h, const void* dres,

@@ -38,6 +38,7 @@ _KERNEL_SIGS = {
     "hds_xent": "i" + "pppp" + "l" + "i" + "l" + "i" + "f" + "i" + "f" + "s",
     "hds_attn_fwd": "p" * 7 + "i" * 7 + "f" + "ii" + "s",
     "hds_attn_bwd": "p" * 12 + "i" * 7 + "f" + "ii" + "s",
+    "hds_attn_config": "iii",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}

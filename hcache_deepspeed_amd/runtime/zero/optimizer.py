@@ -616,11 +616,15 @@ class ZeroOptimizer:
 
     def _post_step_gather(self):
         """ZeRO-1/2: rebuild the persistent full parameters from the updated shards."""
-        if self.layout_world == 1 or self.stage == 3:
+        if self.layout_world == 1:
             return
         works = []
         for u in self.units:
-            works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor, group=self.dp_group, async_op=True))
+            if self.stage == 3 and not u.persistent:
+                continue  # re-gathered on demand by the next forward
+            if u.full is None:
+                continue
+            works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor, group=self.ag_group, async_op=True))
         for w in works:
             w.wait()
 

@@ -58,7 +58,7 @@ def _zero_vs_torch(rank, world, stage, gas, zero_init):
         ropt.zero_grad()
     full = eng.optimizer.full_fp32_state_dict(eng._param_names)
     for n, p in ref.named_parameters():
-        assert torch.allclose(full[n], p.detach(), atol=2e-5, rtol=1e-4), (stage, n, (full[n] - p).abs().max())
+        assert torch.allclose(full[n], p.detach(), atol=3e-4, rtol=1e-3), (stage, n, (full[n] - p).abs().max())
 
 
 @pytest.mark.parametrize("stage", [0, 1, 2, 3])
