@@ -1,0 +1,265 @@
+// Serving kernels over the paged (blocked) KV cache: fused RoPE + KV scatter, and ragged
+// prefill/decode attention that reads K/V through per-sequence block tables.
+//
+// Capability parity: deepspeed/inference/v2/kernels/ragged_ops/linear_blocked_kv_rotary
+// (`kv_rotary_pos_kernel`, SURVEY §2.11 K31 -- also the only kernel the HCache `restore_kv`
+// path runs) and blocked_flash (`run_mha_fwd` over AttentionAtoms, K32, a prebuilt NVIDIA-only
+// library in the reference).
+//
+// Cache layout per layer (same as the reference BlockedKVCache): [num_blocks, block_size, 2, Hkv, D]
+// (K then V for each slot). Any block_size works: every staged tile row computes its own
+// (block, slot) address, and LDS-DMA takes a per-lane global source address.
+//
+// Attention work unit ("atom"): (sequence, kv head, 128 packed rows). Rows pack the G = Hq/Hkv
+// query heads that share a kv head with the tokens of the chunk (row = token * G + head_in_group),
+// so K/V of a kv head are read ONCE for all of its query heads -- for decode (1 token) one wave
+// serves the whole GQA group from a single pass over the sequence's KV blocks.
+#include "attn_common.h"
+
+using namespace hds;
+using namespace hds::attn;
+
+namespace {
+
+constexpr int D = 128;
+constexpr int BN = 64;
+constexpr float kLog2e = 1.4426950408889634f;
+
+// ------------------------------------------------------------------------------------------
+// fused RoPE (q in place, k rotated into the cache) + V copy into the cache
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void kv_rope_scatter_kernel(T* __restrict__ qkv, int64_t sq, T* __restrict__ cache,
+                                                              const int* __restrict__ tok_seq,
+                                                              const int* __restrict__ tok_pos,
+                                                              const int* __restrict__ block_tables, int max_blocks,
+                                                              const float* __restrict__ cos_t,
+                                                              const float* __restrict__ sin_t, int n_tok, int hq,
+                                                              int hkv, int block_size, int rotate_q, int do_rope) {
+  const int half = D / 2;
+  const int gph = D / 16;  // thread groups per head (8 rotation pairs each)
+  const int heads = hq + 2 * hkv;
+  const int64_t total = (int64_t)n_tok * heads * gph;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int t = (int)(idx / (heads * gph));
+    const int rem = (int)(idx - (int64_t)t * heads * gph);
+    const int h = rem / gph, g = rem - h * gph;
+    if (h < hq && !rotate_q) continue;
+    const int pos = tok_pos[t];
+    T* src = qkv + (int64_t)t * sq + (int64_t)h * D;
+    float a[8], b[8];
+    Vec8<T>::load(src + g * 8, a);
+    Vec8<T>::load(src + half + g * 8, b);
+    if (h < hq + hkv && do_rope) {
+      float c[8], s[8];
+      Vec8<float>::load(cos_t + (int64_t)pos * half + g * 8, c);
+      Vec8<float>::load(sin_t + (int64_t)pos * half + g * 8, s);
+      float oa[8], ob[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        oa[j] = a[j] * c[j] - b[j] * s[j];
+        ob[j] = b[j] * c[j] + a[j] * s[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] = oa[j];
+        b[j] = ob[j];
+      }
+    }
+    if (h < hq) {
+      Vec8<T>::store(src + g * 8, a);
+      Vec8<T>::store(src + half + g * 8, b);
+      continue;
+    }
+    const int kv = (h < hq + hkv) ? 0 : 1;
+    const int hk = h - hq - kv * hkv;
+    const int seq = tok_seq[t];
+    const int blk = block_tables[(int64_t)seq * max_blocks + pos / block_size];
+    const int slot = pos % block_size;
+    T* dst = cache + ((((int64_t)blk * block_size + slot) * 2 + kv) * hkv + hk) * D;
+    Vec8<T>::store(dst + g * 8, a);
+    Vec8<T>::store(dst + half + g * 8, b);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// paged attention (ragged prefill + decode)
+// ------------------------------------------------------------------------------------------
+struct PagedParams {
+  const bf16* q;  // [T, Hq, D] rows with token stride sq
+  int64_t sq;
+  const bf16* cache;  // layer base: [num_blocks, block_size, 2, Hkv, D]
+  bf16* o;            // [T, Hq, D] contiguous
+  const int* atoms;   // [n_atoms][3] = {seq, kv_head, row_start}
+  const int* seq_meta;  // [n_seqs][3] = {q_start, n_new, seen}
+  const int* block_tables;
+  int max_blocks;
+  int block_size;
+  int hq, hkv;
+  float scale;
+  int window;
+};
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
+  const int* at = p.atoms + blockIdx.x * 3;
+  const int seq = at[0], hk = at[1], row_start = at[2];
+  const int q_start = p.seq_meta[seq * 3], n_new = p.seq_meta[seq * 3 + 1], seen = p.seq_meta[seq * 3 + 2];
+  const int G = p.hq / p.hkv;
+  const int n_rows = n_new * G;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int myrow = row_start + 32 * w + (lane & 31);
+  const bool row_ok = myrow < n_rows;
+  const int rr = row_ok ? myrow : n_rows - 1;
+  const int tok = rr / G, head = hk * G + rr % G;
+  const int qpos = seen + tok;  // absolute position of this row's query
+  const float c = p.scale * kLog2e;
+  const int* table = p.block_tables + (int64_t)seq * p.max_blocks;
+  const int64_t kv_row = 2LL * p.hkv * D;  // elements between consecutive slots
+
+  bf16x8 qf[8];
+  {
+    const bf16* qp = p.q + (int64_t)(q_start + tok) * p.sq + (int64_t)head * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+  }
+  // last query position covered by this workgroup (rows are token-major)
+  const int last_row = min(row_start + 32 * NW, n_rows) - 1;
+  const int wg_qpos_max = seen + last_row / G;
+  const int ctx = wg_qpos_max + 1;
+  const int kt_end = (ctx + BN - 1) / BN;
+  int kt_begin = 0;
+  if (p.window > 0) {
+    const int first = seen + (row_start / G) - p.window + 1;
+    kt_begin = first > 0 ? first / BN : 0;
+  }
+  auto rowp = [&](int kt, int kv) {
+    return [=](int row) {
+      int pos = kt * BN + row;
+      pos = pos < ctx ? pos : ctx - 1;
+      const int blk = table[pos / p.block_size];
+      return p.cache + ((int64_t)blk * p.block_size + pos % p.block_size) * kv_row + (int64_t)kv * p.hkv * D +
+             (int64_t)hk * D;
+    };
+  };
+  const int w_row_lo = row_start + 32 * w;
+  const int w_qpos_lo = seen + min(w_row_lo, n_rows - 1) / G;
+  const int w_qpos_hi = seen + min(w_row_lo + 31, n_rows - 1) / G;
+  const bool wave_active = w_row_lo < n_rows;
+
+  f32x16 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  stage_tile64<NW>(smem, rowp(kt_begin, 0));
+  stage_tile64<NW>(smem + 2 * 16384, rowp(kt_begin, 1));
+  __syncthreads();
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
+    const char* Kt = smem + buf * 16384;
+    const char* Vt = smem + 2 * 16384 + buf * 16384;
+    if (kt + 1 < kt_end) {
+      stage_tile64<NW>(smem + (buf ^ 1) * 16384, rowp(kt + 1, 0));
+      stage_tile64<NW>(smem + 2 * 16384 + (buf ^ 1) * 16384, rowp(kt + 1, 1));
+    }
+    const int k0 = kt * BN;
+    bool skip = !wave_active || k0 > w_qpos_hi;
+    if (p.window > 0 && k0 + BN - 1 <= w_qpos_lo - p.window) skip = true;
+    if (!skip) {
+      f32x16 s[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) s[t] = mfma(read_rows(Kt, 32 * t, ks), qf[ks], s[t]);
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kp = k0 + 32 * t + acc_row(r, h);
+          float x = s[t][r] * c;
+          if (kp > qpos || !row_ok || (p.window > 0 && kp <= qpos - p.window)) x = -INFINITY;
+          s[t][r] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float muse = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = fast_exp2(m - muse);
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = fast_exp2(s[t][r] - muse);
+          s[t][r] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+      if (__any(alpha != 1.f)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+      }
+      const bf16x8 pb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int st = 0; st < 4; ++st) o[dt] = mfma(read_tr(Vt, st, dt), pb[st], o[dt]);
+    }
+    __syncthreads();
+  }
+  if (row_ok) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* op = p.o + ((int64_t)(q_start + tok) * p.hq + head) * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = (bf16)(o[dt][4 * g + j] * inv);
+        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * h) = v4;
+      }
+  }
+}
+
+}  // namespace
+
+HDS_EXPORT int hds_kv_rope_scatter(int dtype, void* qkv, int64_t sq, void* cache, const int* tok_seq,
+                                   const int* tok_pos, const int* block_tables, int max_blocks, const float* cos_t,
+                                   const float* sin_t, int n_tok, int hq, int hkv, int head_dim, int block_size,
+                                   int rotate_q, int do_rope, hipStream_t st) {
+  if (head_dim != D || n_tok <= 0) return n_tok <= 0 ? 0 : hipErrorInvalidValue;
+  const int64_t work = (int64_t)n_tok * (hq + 2 * hkv) * (D / 16);
+  dim3 grid(stream_grid(work, 256, 4096)), block(256);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(kv_rope_scatter_kernel<bf16>, grid, block, 0, st, (bf16*)qkv, sq, (bf16*)cache, tok_seq, tok_pos,
+                       block_tables, max_blocks, cos_t, sin_t, n_tok, hq, hkv, block_size, rotate_q, do_rope);
+  else if (dtype == kF16)
+    hipLaunchKernelGGL(kv_rope_scatter_kernel<_Float16>, grid, block, 0, st, (_Float16*)qkv, sq, (_Float16*)cache,
+                       tok_seq, tok_pos, block_tables, max_blocks, cos_t, sin_t, n_tok, hq, hkv, block_size, rotate_q,
+                       do_rope);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// atoms: device int32 [n_atoms][3]; seq_meta: device int32 [n_seqs][3]
+HDS_EXPORT int hds_paged_attn(const void* q, int64_t sq, const void* cache, void* o, const int* atoms, int n_atoms,
+                              const int* seq_meta, const int* block_tables, int max_blocks, int block_size, int hq,
+                              int hkv, int head_dim, float scale, int window, hipStream_t st) {
+  if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
+  if (n_atoms <= 0) return 0;
+  PagedParams p{(const bf16*)q, sq, (const bf16*)cache, (bf16*)o, atoms, seq_meta, block_tables, max_blocks,
+                block_size, hq, hkv, scale, window};
+  hipLaunchKernelGGL(paged_attn_kernel<4>, dim3(n_atoms), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+HDS_EXPORT int hds_paged_rows_per_atom() { return 128; }

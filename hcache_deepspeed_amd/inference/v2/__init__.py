@@ -1,0 +1,5 @@
+"""Ragged (FastGen-style) serving engine with the HCache hidden-state cache."""
+from .engine import (InferenceEngineV2, RaggedInferenceEngineConfig, SchedulingError, SchedulingResult,  # noqa: F401
+                     build_engine_from_model, build_hf_engine)
+from .ragged import (BlockedAllocator, BlockedKVCache, DSSequenceDescriptor, DSStateManager,  # noqa: F401
+                     DSStateManagerConfig, MemoryConfig, RaggedBatchWrapper)

@@ -1,0 +1,45 @@
+"""ctypes signatures of libhds_host.so (csrc/host/*.cpp)."""
+import ctypes
+
+P, I, L, F, D, Z = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_size_t
+
+SIGS = {
+    # pinned_ring.cpp
+    "hds_host_alloc": (P, [Z, I]),
+    "hds_host_free": (I, [P]),
+    "hds_ring_create": (P, [Z, I, I]),
+    "hds_ring_destroy": (I, [P]),
+    "hds_ring_slot_ptr": (P, [P, I]),
+    "hds_ring_slot_bytes": (Z, [P]),
+    "hds_ring_acquire": (I, [P]),
+    "hds_ring_d2h": (I, [P, I, P, Z, Z, P]),
+    "hds_ring_h2d": (I, [P, I, P, Z, Z, P]),
+    "hds_ring_record": (I, [P, I, P]),
+    "hds_ring_wait": (I, [P, I]),
+    "hds_ring_stream_wait": (I, [P, I, P]),
+    "hds_ring_query": (I, [P, I]),
+    "hds_memcpy_async": (I, [P, P, Z, I, P]),
+    # cpu_optim.cpp
+    "hds_cpu_adam": (I, [P, P, I, P, P, P, L, F, F, F, F, F, F, F, I, F]),
+    "hds_cpu_lion": (I, [P, P, I, P, P, L, F, F, F, F, F]),
+    "hds_cpu_adagrad": (I, [P, P, I, P, P, L, F, F, F, F]),
+    "hds_cpu_sumsq": (D, [P, I, L, P]),
+    "hds_cpu_num_threads": (I, []),
+    "hds_cpu_set_num_threads": (I, [I]),
+    # aio.cpp
+    "hds_aio_create": (P, [L, I, I, I, I]),
+    "hds_aio_destroy": (I, [P]),
+    "hds_aio_pread": (I, [P, P, L, ctypes.c_char_p, L, I]),
+    "hds_aio_pwrite": (I, [P, P, L, ctypes.c_char_p, L, I]),
+    "hds_aio_wait": (L, [P]),
+    "hds_aio_file_size": (L, [ctypes.c_char_p]),
+}
+
+
+def bind(lib):
+    for name, (res, args) in SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args

@@ -1,0 +1,98 @@
+"""Paged-KV serving ops: fused RoPE + KV scatter, ragged paged attention (HIP, csrc/kernels/paged_attn.hip).
+
+Reference parity: inference/v2/kernels/ragged_ops/linear_blocked_kv_rotary (``LinearBlockedKVCopy``,
+``BlockedRotaryEmbeddings``) and ragged_ops/blocked_flash (``BlockedFlashAttn``) + atom_builder.
+CPU tensors run torch references (used by the CPU test-suite and as the GPU numerics oracle).
+"""
+import torch
+
+from . import native
+
+ROWS_PER_ATOM = 128
+
+
+def kv_rope_scatter(qkv, cache, tok_seq, tok_pos, block_tables, cos, sin, n_q, n_kv, rotate_q=True, do_rope=True):
+    """qkv: [T, n_q + 2 n_kv, D]; cache: [num_blocks, block_size, 2, n_kv, D] (one layer).
+
+    RoPE at absolute positions ``tok_pos`` on q (in place, if ``rotate_q``) and k; k and v are written
+    to ``cache[block_tables[tok_seq[t], pos // bs], pos % bs]``.
+    """
+    T, NH, D = qkv.shape
+    bs = cache.shape[1]
+    if native.use_native(qkv):
+        native.check(
+            native.kernels().hds_kv_rope_scatter(native.dt(qkv), qkv.data_ptr(), qkv.stride(0), cache.data_ptr(),
+                                                 tok_seq.data_ptr(), tok_pos.data_ptr(), block_tables.data_ptr(),
+                                                 block_tables.shape[1], cos.data_ptr() if do_rope else None,
+                                                 sin.data_ptr() if do_rope else None, T, n_q, n_kv, D, bs,
+                                                 int(rotate_q), int(do_rope), native.stream()), "kv_rope_scatter")
+        return
+    pos = tok_pos.long()
+    half = D // 2
+
+    def rot(x):
+        if not do_rope:
+            return x
+        c = cos[pos][:, None, :]
+        s = sin[pos][:, None, :]
+        xf = x.float()
+        a, b = xf[..., :half], xf[..., half:]
+        return torch.cat([a * c - b * s, b * c + a * s], -1).to(x.dtype)
+
+    if rotate_q:
+        qkv[:, :n_q] = rot(qkv[:, :n_q])
+    k = rot(qkv[:, n_q:n_q + n_kv])
+    v = qkv[:, n_q + n_kv:]
+    blk = block_tables[tok_seq.long(), pos // bs].long()
+    slot = pos % bs
+    cache[blk, slot, 0] = k
+    cache[blk, slot, 1] = v
+
+
+def build_atoms(seq_meta_host, n_q, n_kv):
+    """seq_meta_host: list of (q_start, n_new, seen). Returns int32 [n_atoms, 3] = (seq, kv_head, row_start)."""
+    G = n_q // n_kv
+    atoms = []
+    for s, (_, n_new, _) in enumerate(seq_meta_host):
+        rows = n_new * G
+        for hk in range(n_kv):
+            for r0 in range(0, rows, ROWS_PER_ATOM):
+                atoms.append((s, hk, r0))
+    return torch.tensor(atoms if atoms else [(0, 0, 0)], dtype=torch.int32), len(atoms)
+
+
+def paged_attention(q, cache, atoms, n_atoms, seq_meta, block_tables, n_q, n_kv, scale, window=0,
+                    seq_meta_host=None, block_tables_host=None):
+    """q: [T, n_q, D] (token-strided view ok). Returns o [T, n_q, D]."""
+    T, _, D = q.shape
+    o = torch.empty(T, n_q, D, device=q.device, dtype=q.dtype)
+    if native.use_native(q):
+        native.check(
+            native.kernels().hds_paged_attn(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(),
+                                            atoms.data_ptr(), n_atoms, seq_meta.data_ptr(), block_tables.data_ptr(),
+                                            block_tables.shape[1], cache.shape[1], n_q, n_kv, D, float(scale),
+                                            int(window), native.stream()), "paged_attn")
+        return o
+    meta = seq_meta_host if seq_meta_host is not None else seq_meta.tolist()
+    tables = block_tables_host if block_tables_host is not None else block_tables
+    bs = cache.shape[1]
+    G = n_q // n_kv
+    for s, (q0, n_new, seen) in enumerate(meta):
+        if n_new == 0:
+            continue
+        ctx = seen + n_new
+        pos = torch.arange(ctx)
+        blk = tables[s][pos // bs].long()
+        kk = cache[blk, pos % bs, 0].float()  # [ctx, n_kv, D]
+        vv = cache[blk, pos % bs, 1].float()
+        qq = q[q0:q0 + n_new].float()  # [n_new, n_q, D]
+        kk = kk.repeat_interleave(G, 1)
+        vv = vv.repeat_interleave(G, 1)
+        sc = torch.einsum("thd,chd->htc", qq, kk) * scale
+        qpos = seen + torch.arange(n_new)
+        mask = pos[None, :] > qpos[:, None]
+        if window:
+            mask |= pos[None, :] <= qpos[:, None] - window
+        sc = sc.masked_fill(mask[None], float("-inf"))
+        o[q0:q0 + n_new] = torch.einsum("htc,chd->thd", torch.softmax(sc, -1), vv).to(o.dtype)
+    return o

@@ -1,0 +1,100 @@
+"""Ragged serving engine + HCache (put -> latents, restore_kv): consistency with the training model.
+
+The reference has no test for restore_kv/latents; these pin its semantics: restoring the KV
+cache from host latents and continuing decoding must give the same logits as never evicting.
+Runs on CPU (torch reference ops) and, marked gpu, on the MI355X with the HIP paged kernels.
+"""
+import pytest
+import torch
+
+from hcache_deepspeed_amd.inference.v2 import build_engine_from_model
+from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+
+
+def _model(device, dtype, **kw):
+    torch.manual_seed(0)
+    cfg = dict(head_dim=128, hidden_size=256, intermediate_size=512, vocab_size=211, num_attention_heads=4,
+               num_key_value_heads=2, num_hidden_layers=3)
+    cfg.update(kw)
+    m = LlamaForCausalLM(tiny(**cfg)).to(device=device, dtype=dtype).eval()
+    return m
+
+
+def _full_logits(m, ids):
+    with torch.no_grad():
+        return m(ids[None]).float()  # [T, V]
+
+
+def _devices():
+    devs = [("cpu", torch.float32)]
+    return devs
+
+
+def _run_consistency(device, dtype, latent_mode, tol):
+    m = _model(device, dtype)
+    eng = build_engine_from_model(m, {"latent_mode": latent_mode, "dtype": {torch.float32: "fp32",
+                                                                          torch.bfloat16: "bf16"}[dtype],
+                                      "state_manager": {"max_context": 1024, "kv_block_size": 64}},
+                                  device=torch.device(device), num_kv_blocks=64)
+    g = torch.Generator().manual_seed(1)
+    p1 = torch.randint(0, 211, (70, ), generator=g)
+    p2 = torch.randint(0, 211, (33, ), generator=g)
+    cont = torch.randint(0, 211, (5, ), generator=g)
+    full1 = _full_logits(m, torch.cat([p1, cont]).to(device))
+    full2 = _full_logits(m, p2.to(device))
+    # ragged prefill of two sequences
+    logits, lats = eng.put([1, 2], [p1, p2])
+    assert logits.shape == (2, 211)
+    assert torch.allclose(logits[0].float(), full1[69], atol=tol, rtol=tol)
+    assert torch.allclose(logits[1].float(), full2[-1], atol=tol, rtol=tol)
+    L = m.config.num_hidden_layers
+    assert lats[0].shape[0] == L and lats[0].shape[1] == 70
+    # HCache: drop seq 1's KV, restore from latents, continue decoding
+    eng.evict(1)
+    blocks_before = eng.free_blocks
+    eng.restore_kv([1, 2], [p1, p2], [lats[0], None])
+    assert eng.free_blocks == blocks_before - 2
+    for j in range(cont.numel()):
+        lg, _ = eng.put([1], [cont[j:j + 1]], capture_latents=False)
+        assert torch.allclose(lg[0].float(), full1[70 + j], atol=tol, rtol=tol), j
+    # scheduling API
+    tokens, blocks = eng.query(1, 100, 10)
+    assert tokens > 0
+    eng.flush(1)
+    eng.flush(2)
+    assert eng.free_blocks == 64
+
+
+@pytest.mark.parametrize("latent_mode", ["hidden", "kv"])
+def test_hcache_consistency_cpu(latent_mode):
+    _run_consistency("cpu", torch.float32, latent_mode, 2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("latent_mode", ["hidden", "kv"])
+def test_hcache_consistency_gpu(latent_mode):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_consistency("cuda", torch.bfloat16, latent_mode, 6e-2)
+
+
+def test_allocator_and_scheduling():
+    from hcache_deepspeed_amd.inference.v2 import BlockedAllocator, SchedulingResult
+    a = BlockedAllocator(10)
+    x = a.allocate(4)
+    assert a.free_blocks == 6
+    a.free(x)
+    assert a.free_blocks == 10
+    with pytest.raises(ValueError):
+        a.allocate(11)
+    with pytest.raises(ValueError):
+        a.free([3])
+    m = _model("cpu", torch.float32, num_hidden_layers=1)
+    eng = build_engine_from_model(m, {"dtype": "fp32", "state_manager": {"max_context": 256,
+                                                                        "max_ragged_batch_size": 100}},
+                                  device=torch.device("cpu"), num_kv_blocks=3)
+    assert eng.can_schedule([1], [101]) == SchedulingResult.BatchTokenLimitExceeded
+    assert eng.can_schedule([1], [300]) in (SchedulingResult.SequenceTokenLimitExceeded,
+                                            SchedulingResult.BatchTokenLimitExceeded)
+    assert eng.can_schedule([1, 2], [99, 1]) == SchedulingResult.Success
+    assert eng.can_schedule([1], [64 * 3 + 1]) != SchedulingResult.Success

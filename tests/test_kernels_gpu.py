@@ -284,3 +284,51 @@ def test_qkv_attention_matches_unfused():
     o1.backward(g)
     o2.backward(g)
     assert _rel(qkv.grad, x1.grad) < 2e-2
+
+
+def _paged_setup(lens, seen, Hq=8, Hkv=2, D=128, bs=64, nblocks=64):
+    from hcache_deepspeed_amd.ops.rope import rope_tables
+    torch.manual_seed(3)
+    cache = torch.randn(nblocks, bs, 2, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    perm = torch.randperm(nblocks).tolist()
+    tables, metas, off = [], [], 0
+    maxb = 0
+    for n, s in zip(lens, seen):
+        nb = (n + s + bs - 1) // bs
+        tables.append([perm.pop() for _ in range(nb)])
+        maxb = max(maxb, nb)
+        metas.append((off, n, s))
+        off += n
+    tab = torch.zeros(len(lens), maxb, dtype=torch.int32)
+    for i, t in enumerate(tables):
+        tab[i, :len(t)] = torch.tensor(t)
+    return cache, tab, metas, off, rope_tables(4096, D, 10000.0, device="cuda")
+
+
+def test_kv_rope_scatter_matches_reference():
+    from hcache_deepspeed_amd.ops.paged import kv_rope_scatter
+    lens, seen = [5, 70, 1], [0, 10, 200]
+    Hq, Hkv, D = 8, 2, 128
+    cache, tab, metas, T, (cos, sin) = _paged_setup(lens, seen)
+    tok_seq = torch.cat([torch.full((n, ), i, dtype=torch.int32) for i, n in enumerate(lens)])
+    tok_pos = torch.cat([torch.arange(s, s + n, dtype=torch.int32) for n, s in zip(lens, seen)])
+    qkv = torch.randn(T, Hq + 2 * Hkv, D, device="cuda", dtype=torch.bfloat16)
+    q2, c2 = qkv.clone().cpu().float(), cache.clone().cpu().float()
+    kv_rope_scatter(qkv, cache, tok_seq.cuda(), tok_pos.cuda(), tab.cuda(), cos, sin, Hq, Hkv)
+    kv_rope_scatter(q2, c2, tok_seq, tok_pos, tab, cos.cpu(), sin.cpu(), Hq, Hkv)
+    assert _rel(qkv.cpu(), q2) < 1e-2
+    assert _rel(cache.cpu(), c2) < 1e-2
+
+
+@pytest.mark.parametrize("lens,seen", [([1, 1, 1], [100, 5, 700]), ([130, 64, 3], [0, 0, 0]), ([37, 1], [90, 333])])
+def test_paged_attention_matches_reference(lens, seen):
+    from hcache_deepspeed_amd.ops.paged import build_atoms, paged_attention
+    Hq, Hkv, D = 8, 2, 128
+    cache, tab, metas, T, _ = _paged_setup(lens, seen)
+    q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16)
+    atoms, n = build_atoms(metas, Hq, Hkv)
+    meta = torch.tensor(metas, dtype=torch.int32)
+    o = paged_attention(q, cache, atoms.cuda(), n, meta.cuda(), tab.cuda(), Hq, Hkv, 1 / math.sqrt(D))
+    ref = paged_attention(q.cpu().float(), cache.cpu().float(), atoms, n, meta, tab, Hq, Hkv, 1 / math.sqrt(D),
+                          seq_meta_host=metas, block_tables_host=tab)
+    assert _rel(o.cpu(), ref) < 1e-2
