@@ -144,7 +144,11 @@ HDS_EXPORT int hds_aio_destroy(void* h) {
 HDS_EXPORT int hds_aio_pread(void* h, void* buf, int64_t bytes, const char* path, int64_t file_off, int async_op) {
   Pool* p = (Pool*)h;
   int rc = do_io(false, buf, bytes, path, file_off, p);
-  if (rc == 0 && !async_op) p->wait_all();
+  if (rc == 0 && !async_op) {
+    p->wait_all();
+    std::lock_guard<std::mutex> l(p->mu);
+    p->completed_ops--;  // synchronous requests are not reported by wait()
+  }
   return rc;
 }
 
@@ -152,7 +156,11 @@ HDS_EXPORT int hds_aio_pwrite(void* h, const void* buf, int64_t bytes, const cha
                               int async_op) {
   Pool* p = (Pool*)h;
   int rc = do_io(true, (void*)buf, bytes, path, file_off, p);
-  if (rc == 0 && !async_op) p->wait_all();
+  if (rc == 0 && !async_op) {
+    p->wait_all();
+    std::lock_guard<std::mutex> l(p->mu);
+    p->completed_ops--;
+  }
   return rc;
 }
 
