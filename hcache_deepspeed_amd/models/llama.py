@@ -145,9 +145,21 @@ class LlamaAttention(nn.Module):
         self.o_proj = _Linear(self.n_q * self.d, cfg.hidden_size, std=std / math.sqrt(2 * cfg.num_hidden_layers))
         self.layer_idx = layer_idx
 
+    sp_group = None  # Ulysses sequence-parallel group (parallel/ulysses.enable_sequence_parallel)
+
     def forward(self, x, cos, sin, seq_len, cu_seqlens=None, pos_ids=None):
         T = x.shape[0]
         qkv = self.qkv_proj(x).view(T, self.n_q + 2 * self.n_kv, self.d)
+        if self.sp_group is not None:
+            from ..parallel.ulysses import ulysses_out, ulysses_qkv
+            from .. import comm as dist
+            P = dist.get_world_size(self.sp_group)
+            B = T // seq_len
+            full = ulysses_qkv(qkv, self.n_q, self.n_kv, self.sp_group, B)
+            o = qkv_attention(full, self.n_q // P, self.n_kv // P, cos, sin, seq_len=seq_len * P, causal=True,
+                              window=self.cfg.sliding_window)
+            o = ulysses_out(o.view(B * seq_len * P, self.n_q // P, self.d), self.sp_group, B).reshape(T, -1)
+            return self.o_proj(o)
         o = qkv_attention(qkv, self.n_q, self.n_kv, cos, sin, seq_len=seq_len, causal=True, cu_seqlens=cu_seqlens,
                           pos_ids=pos_ids, window=self.cfg.sliding_window)
         return self.o_proj(o)
@@ -210,7 +222,8 @@ class LlamaModel(nn.Module):
         else:
             ids, S = input_ids, input_ids.shape[0]
         h = self.embed_tokens(ids)
-        cos, sin = self.rope(h.device, S)
+        sp = getattr(self, "_hds_sp_size", 1)
+        cos, sin = self.rope(h.device, S * sp)
         residual = None
         for i, layer in enumerate(self.layers):
             if layer_hook is not None:
@@ -237,10 +250,15 @@ class LlamaForCausalLM(nn.Module):
     def gradient_checkpointing_enable(self):
         self.model.gradient_checkpointing = True
 
-    def forward(self, input_ids, labels=None, cu_seqlens=None, pos_ids=None, return_hidden=False):
+    def forward(self, input_ids, labels=None, cu_seqlens=None, pos_ids=None, return_hidden=False, targets=None):
+        """``labels``: HF convention (shifted inside). ``targets``: already next-token aligned with
+        ``input_ids`` (required with sequence parallelism, where a rank holds a slice of each sequence)."""
         h = self.model(input_ids, cu_seqlens=cu_seqlens, pos_ids=pos_ids)
         if return_hidden:
             return h
+        if targets is not None:
+            return fused_linear_cross_entropy(h, self.lm_head.weight, targets.reshape(-1),
+                                              chunk_rows=self.ce_chunk_rows)
         if labels is None:
             return F.linear(h, self.lm_head.weight)
         lab = labels.reshape(-1) if labels.dim() > 1 else labels

@@ -87,6 +87,14 @@ class DeepSpeedEngine(nn.Module):
         self.dp_group = groups._get_sequence_data_parallel_group() if sp > 1 else groups._get_data_parallel_group()
         self.dp_world_size = dist.get_world_size(self.dp_group)
         self.seq_parallel_group = groups._get_sequence_parallel_group()
+        self.mp_group = groups._get_model_parallel_group() if groups.get_model_parallel_world_size() > 1 else None
+        if self.mp_group is not None and not getattr(model, "_hds_tp_size", 0):
+            from ..parallel.tp import AutoTP
+            AutoTP(model, self.mp_group).shard()
+            model._hds_tp_size = groups.get_model_parallel_world_size()
+        if sp > 1:
+            from ..parallel.ulysses import enable_sequence_parallel
+            enable_sequence_parallel(model, self.seq_parallel_group)
 
         # timers / monitoring
         self.wall_clock_breakdown_enabled = cfg.wall_clock_breakdown
@@ -208,7 +216,8 @@ class DeepSpeedEngine(nn.Module):
         leaf = getattr(self.module, "_z3_leaf_modules", ())
         self.optimizer = cls(basic, self.module, cfg, stage, dp_group=self.dp_group, dtype=self.compute_dtype,
                              device=self.device, grad_accum_steps=cfg.gradient_accumulation_steps,
-                             timers=self.timers, mpu=self.mpu, leaf_modules=leaf, param_names=self._param_names)
+                             timers=self.timers, mpu=self.mpu, leaf_modules=leaf, param_names=self._param_names,
+                             mp_group=self.mp_group)
 
     def _configure_lr_scheduler(self, client_lr_scheduler):
         cfg = self._config

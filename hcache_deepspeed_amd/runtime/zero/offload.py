@@ -98,8 +98,8 @@ class OffloadZeroOptimizer(ZeroOptimizer):
         self._norm_buf.zero_()
         self._inf_buf.zero_()
         fused.grad_sumsq([s.grad], out=self._norm_buf, found_inf=self._inf_buf)
-        if self.dp_world > 1 and self.stage > 0:
-            dist.all_reduce(self._norm_buf, group=self.dp_group)
+        self._reduce_norm()
+        if self.dp_world > 1 and not self.loss_scaler.dynamic:
             dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.dp_group)
         coef_t = fused.clip_coef(self._norm_buf, self.clip_grad, inv, coef=self._coef_buf)
         self.global_norm, self._norm_scale = self._norm_buf, inv

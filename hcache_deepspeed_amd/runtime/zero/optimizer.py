@@ -99,8 +99,9 @@ class ZeroOptimizer:
     """Flat-shard ZeRO (stage 0 = plain DP with the same flat machinery)."""
 
     def __init__(self, init_optimizer, module, config, stage, dp_group=None, dtype=torch.bfloat16, device=None,
-                 grad_accum_steps=1, timers=None, mpu=None, leaf_modules=(), param_names=None):
+                 grad_accum_steps=1, timers=None, mpu=None, leaf_modules=(), param_names=None, mp_group=None):
         self.optimizer = init_optimizer
+        self.mp_group = mp_group if (mp_group is not None and dist.get_world_size(mp_group) > 1) else None
         self.module = module
         self.config = config
         self.zcfg = config.zero_config
@@ -158,6 +159,8 @@ class ZeroOptimizer:
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._inf_buf = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._coef_buf = torch.ones(1, dtype=torch.float32, device=self.device)
+        self._rep_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._rep_ranges = self._replicated_ranges() if self.mp_group is not None else []
         self._fwd_trace, self._trace_ok, self._trace_pos = [], False, 0
         self._recording = True
         self.prefetch_depth = max(0, int(self.mi.zero3_prefetch_depth))
@@ -275,6 +278,19 @@ class ZeroOptimizer:
         for p in (p for u in self.units for p in u.params):
             p.ds_status = self.param_to_unit[id(p)][0].status
             p._hds_zero = self
+
+    def _replicated_ranges(self):
+        """Store ranges (of MY shard) holding TP-replicated parameters: counted once in the global norm."""
+        out = []
+        for u in self.units:
+            lo, hi = u.rank * u.shard, (u.rank + 1) * u.shard
+            for i, p in enumerate(u.params):
+                if getattr(p, "ds_tensor_model_parallel", False):
+                    continue
+                a, b = max(lo, u.offsets[i]), min(hi, u.offsets[i] + u.numels[i])
+                if a < b:
+                    out.append((u.store_off + a - lo, u.store_off + b - lo))
+        return out
 
     def _swap_params(self, u, repl):
         """Replace materialised meta parameters everywhere this optimizer references them."""
@@ -569,10 +585,7 @@ class ZeroOptimizer:
         self._norm_buf.zero_()
         self._inf_buf.zero_()
         fused.grad_sumsq([s.grad], out=self._norm_buf, found_inf=self._inf_buf)
-        if self.dp_world > 1 and self.stage > 0:
-            dist.all_reduce(self._norm_buf, group=self.dp_group)
-            if self.loss_scaler.dynamic:
-                dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.dp_group)
+        self._reduce_norm()
         coef = fused.clip_coef(self._norm_buf, self.clip_grad, inv, coef=self._coef_buf)
         self.global_norm = self._norm_buf  # sqrt applied lazily in get_global_norm
         self._norm_scale = inv
@@ -613,6 +626,25 @@ class ZeroOptimizer:
 
     def layout_world_for_avg(self):
         return self.dp_world
+
+    def _reduce_norm(self):
+        """Global grad sum-of-squares over DP (and TP: sharded params summed, replicated counted once)."""
+        if self.mp_group is not None:
+            self._rep_buf.zero_()
+            if self._rep_ranges:
+                fused.grad_sumsq([self.store.grad[a:b] for a, b in self._rep_ranges], out=self._rep_buf)
+        if self.dp_world > 1 and self.stage > 0:
+            dist.all_reduce(self._norm_buf, group=self.dp_group)
+            if self.mp_group is not None:
+                dist.all_reduce(self._rep_buf, group=self.dp_group)
+        if self.loss_scaler.dynamic and self.dp_world > 1:
+            dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.dp_group)
+        if self.mp_group is not None:
+            sharded = self._norm_buf - self._rep_buf
+            dist.all_reduce(sharded, group=self.mp_group)
+            self._norm_buf.copy_(sharded + self._rep_buf)
+            if self.loss_scaler.dynamic:
+                dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.mp_group)
 
     def _post_step_gather(self):
         """ZeRO-1/2: rebuild the persistent full parameters from the updated shards."""

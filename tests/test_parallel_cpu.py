@@ -1,0 +1,113 @@
+"""Tensor parallelism (AutoTP) and Ulysses sequence parallelism on gloo: must reproduce single-process training."""
+import pytest
+import torch
+
+from tests.dist_utils import run_distributed
+from tests.test_zero_cpu import TINY
+
+
+def _ref_losses(batches, steps, targets_mode=False):
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    torch.manual_seed(0)
+    ref = LlamaForCausalLM(tiny(**TINY))
+    opt = torch.optim.AdamW(ref.parameters(), lr=5e-3)
+    out = []
+    for b in batches[:steps]:
+        if targets_mode:
+            x, t = b
+            loss = ref(x, targets=t)
+        else:
+            loss = ref(b, labels=b)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        out.append(float(loss))
+    return out, ref
+
+
+def _tp(rank, world, stage):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    g = torch.Generator().manual_seed(7)
+    batches = [torch.randint(0, 97, (2, 12), generator=g) for _ in range(3)]
+    ref_losses, _ = _ref_losses(batches, 3)
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(**TINY))
+    cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
+           "zero_optimization": {"stage": stage}, "tensor_parallel": {"autotp_size": 2}}
+    eng, _, _, _ = ds.initialize(model=m, config=cfg)
+    assert m.model.layers[0].self_attn.n_q == TINY["num_attention_heads"] // 2
+    losses = []
+    for b in batches:
+        loss = eng(b, labels=b)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss))
+    assert losses == pytest.approx(ref_losses, rel=1e-4, abs=1e-4), (losses, ref_losses)
+
+
+@pytest.mark.parametrize("stage", [0, 3])
+def test_autotp_training_matches_single(stage):
+    from hcache_deepspeed_amd.utils import groups
+    run_distributed(_tp, 2, stage)
+
+
+def _sp(rank, world, stage):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    g = torch.Generator().manual_seed(9)
+    S = 16
+    batches = []
+    for _ in range(3):
+        x = torch.randint(0, 97, (2, S + 1), generator=g)
+        x, t = x[:, :-1].contiguous(), x[:, 1:].contiguous()  # every position valid: equal counts per rank
+        batches.append((x, t))
+    ref_losses, ref = _ref_losses(batches, 3, targets_mode=True)
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(**TINY))
+    cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
+           "zero_optimization": {"stage": stage}, "sequence_parallel_size": 2}
+    eng, _, _, _ = ds.initialize(model=m, config=cfg)
+    half = S // 2
+    losses = []
+    for x, t in batches:
+        xs, ts = x[:, rank * half:(rank + 1) * half], t[:, rank * half:(rank + 1) * half]
+        loss = eng(xs, targets=ts)
+        eng.backward(loss)
+        eng.step()
+        lt = loss.detach().clone()
+        ds.comm.all_reduce(lt)
+        losses.append(float(lt) / 2)
+    assert losses == pytest.approx(ref_losses, rel=1e-4, abs=1e-4), (losses, ref_losses)
+    full = eng.optimizer.full_fp32_state_dict(eng._param_names)
+    for n, p in ref.named_parameters():
+        assert torch.allclose(full[n], p.detach(), atol=2e-4), n
+
+
+@pytest.mark.parametrize("stage", [1, 3])
+def test_ulysses_sp_matches_single(stage):
+    run_distributed(_sp, 2, stage)
+
+
+def _ulysses_a2a(rank, world):
+    from hcache_deepspeed_amd.parallel.ulysses import DistributedAttention
+    from hcache_deepspeed_amd.utils import groups
+    groups.initialize(sp=2)
+    grp = groups._get_sequence_parallel_group()
+    torch.manual_seed(0)
+    B, S, H, D = 2, 8, 4, 16
+    q, k, v = (torch.randn(B, S, H, D) for _ in range(3))
+
+    def local(q_, k_, v_):
+        return torch.nn.functional.scaled_dot_product_attention(q_.transpose(1, 2), k_.transpose(1, 2),
+                                                                v_.transpose(1, 2), is_causal=True).transpose(1, 2)
+
+    full = local(q, k, v)
+    sl = slice(rank * S // 2, (rank + 1) * S // 2)
+    da = DistributedAttention(local, grp)
+    out = da(q[:, sl].contiguous(), k[:, sl].contiguous(), v[:, sl].contiguous())
+    assert torch.allclose(out, full[:, sl], atol=1e-5)
+
+
+def test_distributed_attention_api():
+    run_distributed(_ulysses_a2a, 2)
