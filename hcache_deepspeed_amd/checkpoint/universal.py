@@ -11,7 +11,7 @@ import os
 
 import torch
 
-from .zero_to_fp32 import load_shards, unflatten
+from .zero_to_fp32 import expert_global_name, load_shards, unflatten
 
 
 def ds_to_universal(input_dir, output_dir, tag=None):
@@ -54,9 +54,16 @@ def load_universal_into(zopt, universal_dir, load_optimizer_states=True):
                 full = torch.zeros(u.padded, dtype=torch.float32)
                 for i, p in enumerate(u.params):
                     name = zopt.param_names.get(id(p))
+                    j, nl = 0, int(getattr(p, "_hds_num_local", 1))
+                    if u.expert_key is not None:
+                        j = zopt._ep_rank(u.expert_key)
+                        if not getattr(p, "_hds_expert_stacked", False):
+                            name = expert_global_name(name, j, nl)
                     f = os.path.join(zdir, name, f"{st}.pt")
                     if os.path.exists(f):
                         t = torch.load(f, map_location="cpu", weights_only=True)["param"]
+                        if u.expert_key is not None and getattr(p, "_hds_expert_stacked", False):
+                            t = t[j * nl:(j + 1) * nl]  # this EP rank's experts of the global stack
                         full[u.offsets[i]:u.offsets[i] + u.numels[i]] = t.reshape(-1).float()
                 dst[u.store_off:u.store_off + u.shard].copy_(full[lo:hi].to(dst.device))
         s.lp.copy_(s.master)

@@ -52,17 +52,47 @@ def load_shards(ckpt_dir, states=("fp32", )):
     return layout, out
 
 
+_EXPERT_IDX = re.compile(r"(deepspeed_experts\.)(\d+)(\.)")
+
+
+def expert_global_name(name, ep_rank, num_local):
+    """Local expert parameter name on EP rank ``ep_rank`` -> name with the global expert index."""
+    return _EXPERT_IDX.sub(lambda m: f"{m.group(1)}{int(m.group(2)) + ep_rank * num_local}{m.group(3)}", name,
+                           count=1)
+
+
 def unflatten(layout, flats):
-    """flats: per-rank flat tensors (one per data-parallel rank) -> {param_name: full tensor}."""
+    """flats: per-rank flat tensors (one per data-parallel rank) -> {param_name: full tensor}.
+
+    Expert units (MoE, ``expert_group`` set) are sharded over their expert-data-parallel group: EP rank
+    j's copy lives on data-parallel ranks ``j + ep_size * i``. Stacked expert weights ([E_local, ...]) are
+    concatenated over EP ranks; per-expert modules get their global expert index in the name.
+    """
     world = layout["world"]
-    if len(flats) < world:
-        raise ValueError(f"checkpoint was written by {world} ranks, found {len(flats)} shard files")
     res = {}
     for u in layout["units"]:
         sh = u["shard"]
-        full = torch.cat([flats[r][u["store_off"]:u["store_off"] + sh] for r in range(world)])
-        for name, shape, off, n in zip(u["params"], u["shapes"], u["offsets"], u["numels"]):
-            res[name] = full[off:off + n].view(shape).clone()
+        if u.get("expert_group") is None:
+            need = world
+        else:
+            need = u["ep_size"] * u["world"]
+        if len(flats) < need:
+            raise ValueError(f"checkpoint unit {u['name']} needs {need} shard files, found {len(flats)}")
+        if u.get("expert_group") is None:
+            full = torch.cat([flats[r][u["store_off"]:u["store_off"] + sh] for r in range(world)])
+            for name, shape, off, n in zip(u["params"], u["shapes"], u["offsets"], u["numels"]):
+                res[name] = full[off:off + n].view(shape).clone()
+            continue
+        P, W = u["ep_size"], u["world"]
+        per_j = [torch.cat([flats[j + P * i][u["store_off"]:u["store_off"] + sh] for i in range(W)])
+                 for j in range(P)]
+        for k, (name, shape, off, n) in enumerate(zip(u["params"], u["shapes"], u["offsets"], u["numels"])):
+            parts = [per_j[j][off:off + n].view(shape).clone() for j in range(P)]
+            if u["expert_stacked"][k]:
+                res[name] = torch.cat(parts, 0)
+            else:
+                for j in range(P):
+                    res[expert_global_name(name, j, u["num_local"][k])] = parts[j]
     return res
 
 

@@ -1,0 +1,150 @@
+"""MoE routing ops: top-k gating with capacity slots, dispatch / combine (HIP fwd+bwd, csrc/kernels/moe.hip).
+
+Reference parity: moe/sharded_moe.py ``top1gating``/``top2gating``/``topkgating`` (:183-447; capacity factor,
+token dropping, random token selection) and inference/v2 ragged ops ``top_k_gating``/``moe_scatter``/
+``moe_gather`` (K34-K36).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+
+def capacity(n_tokens, n_experts, k, capacity_factor, min_capacity):
+    return max(int(math.ceil(n_tokens * k / n_experts * capacity_factor)), int(min_capacity))
+
+
+def topk_route(logits, k, capacity_factor=1.0, min_capacity=4, drop_tokens=True, use_rts=False, normalize=True,
+               noisy_gate_policy=None, training=True):
+    """Returns (expert [T,k] int32, pos [T,k] int32, weights [T,k] fp32, C, l_aux, exp_counts).
+
+    pos = rank of the (token, choice) among all assignments to its expert (k-major priority like
+    GShard: every token's first choice beats any token's second choice). pos >= C means dropped.
+    """
+    T, E = logits.shape
+    if noisy_gate_policy == "RSample" and training:
+        logits = logits + torch.randn_like(logits) * (1.0 / E)
+    probs = torch.softmax(logits.float(), dim=-1)
+    topw, topi = torch.topk(probs, k, dim=-1)
+    if normalize and k > 1:
+        topw = topw / topw.sum(-1, keepdim=True)
+    # load-balancing aux loss (GShard): E * sum_e mean(prob_e) * frac_tokens_e (first choice)
+    me = probs.mean(0)
+    ce = F.one_hot(topi[:, 0], E).float().mean(0)
+    l_aux = (me * ce).sum() * E
+    mask = F.one_hot(topi.t().reshape(-1), E)  # [k*T, E], k-major
+    if use_rts and training:
+        # random token selection: random priority inside each choice level
+        noise = torch.rand(k, T, device=logits.device)
+        order = torch.argsort(noise, dim=1) + torch.arange(k, device=logits.device)[:, None] * T
+        inv = torch.empty_like(order.reshape(-1))
+        inv[order.reshape(-1)] = torch.arange(k * T, device=logits.device)
+        mask_perm = mask[order.reshape(-1)]
+        pos_perm = torch.cumsum(mask_perm, 0) - 1
+        pos_all = pos_perm[inv]
+    else:
+        pos_all = torch.cumsum(mask, 0) - 1
+    pos = (pos_all * mask).sum(-1).view(k, T).t().contiguous()
+    exp_counts = mask.sum(0)
+    if drop_tokens:
+        C = capacity(T, E, k, capacity_factor, min_capacity)
+    else:
+        C = int(exp_counts.max().item())
+    return topi.to(torch.int32).contiguous(), pos.to(torch.int32), topw.contiguous(), C, l_aux, exp_counts
+
+
+def _ref_dispatch(x, expert, pos, E, C):
+    T, H = x.shape
+    out = x.new_zeros(E * C, H)
+    keep = pos < C
+    slots = (expert.long() * C + pos.long())[keep]
+    tok = torch.arange(T, device=x.device)[:, None].expand_as(expert)[keep]
+    out[slots] = x[tok]
+    return out
+
+
+def _ref_combine(y, expert, pos, w, C):
+    T, k = expert.shape
+    keep = (pos < C).float()
+    slots = (expert.long() * C + pos.long().clamp(max=C - 1)).clamp(min=0)
+    g = y[slots.reshape(-1)].view(T, k, -1).float()
+    return (g * (w * keep)[..., None]).sum(1).to(y.dtype)
+
+
+class _Dispatch(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, expert, pos, E, C):
+        ctx.save_for_backward(expert, pos)
+        ctx.C, ctx.T = C, x.shape[0]
+        if native.use_native(x):
+            out = torch.zeros(E * C, x.shape[1], device=x.device, dtype=x.dtype)
+            native.check(native.kernels().hds_moe_dispatch(native.dt(x), x.contiguous().data_ptr(), expert.data_ptr(),
+                                                           pos.data_ptr(), out.data_ptr(), x.shape[0], expert.shape[1],
+                                                           x.shape[1], C, native.stream()), "moe_dispatch")
+            return out
+        return _ref_dispatch(x, expert, pos, E, C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        expert, pos = ctx.saved_tensors
+        C, T = ctx.C, ctx.T
+        H = dout.shape[1]
+        if native.use_native(dout):
+            dx = torch.empty(T, H, device=dout.device, dtype=dout.dtype)
+            native.check(native.kernels().hds_moe_dispatch_bwd(native.dt(dout), dout.contiguous().data_ptr(),
+                                                               expert.data_ptr(), pos.data_ptr(), dx.data_ptr(), T,
+                                                               expert.shape[1], H, C, native.stream()), "moe_disp_bwd")
+            return dx, None, None, None, None
+        w = torch.ones(expert.shape, device=dout.device)
+        return _ref_combine(dout, expert, pos, w, C), None, None, None, None
+
+
+class _Combine(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, y, expert, pos, w, C):
+        ctx.save_for_backward(y, expert, pos, w)
+        ctx.C = C
+        T = expert.shape[0]
+        if native.use_native(y):
+            out = torch.empty(T, y.shape[1], device=y.device, dtype=y.dtype)
+            native.check(native.kernels().hds_moe_combine(native.dt(y), y.contiguous().data_ptr(), expert.data_ptr(),
+                                                          pos.data_ptr(), w.float().contiguous().data_ptr(),
+                                                          out.data_ptr(), T, expert.shape[1], y.shape[1], C,
+                                                          native.stream()), "moe_combine")
+            return out
+        return _ref_combine(y, expert, pos, w.float(), C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, expert, pos, w = ctx.saved_tensors
+        C = ctx.C
+        T, k = expert.shape
+        if native.use_native(y):
+            dy = torch.zeros_like(y)
+            dw = torch.empty(T, k, device=y.device, dtype=torch.float32)
+            native.check(native.kernels().hds_moe_combine_bwd(native.dt(y), dout.contiguous().data_ptr(),
+                                                              y.contiguous().data_ptr(), expert.data_ptr(),
+                                                              pos.data_ptr(), w.float().contiguous().data_ptr(),
+                                                              dy.data_ptr(), dw.data_ptr(), T, k, y.shape[1], C,
+                                                              native.stream()), "moe_combine_bwd")
+            return dy, None, None, dw.to(w.dtype), None
+        keep = pos < C
+        slots = (expert.long() * C + pos.long().clamp(max=C - 1)).clamp(min=0)
+        g = y[slots.reshape(-1)].view(T, k, -1).float()
+        dw = (g * dout.float()[:, None, :]).sum(-1) * keep
+        dy = torch.zeros_like(y, dtype=torch.float32)
+        contrib = (dout.float()[:, None, :] * (w.float() * keep)[..., None]).reshape(T * k, -1)
+        dy.index_add_(0, slots.reshape(-1)[keep.reshape(-1)], contrib[keep.reshape(-1)])
+        return dy.to(y.dtype), None, None, dw.to(w.dtype), None
+
+
+def moe_dispatch(x, expert, pos, n_experts, C):
+    return _Dispatch.apply(x, expert, pos, n_experts, C)
+
+
+def moe_combine(y, expert, pos, w, C):
+    return _Combine.apply(y, expert, pos, w, C)

@@ -42,6 +42,10 @@ _KERNEL_SIGS = {
     "hds_kv_rope_scatter": "i" + "p" + "l" + "pppp" + "i" + "pp" + "i" * 7 + "s",
     "hds_paged_attn": "p" + "l" + "ppp" + "i" + "pp" + "i" * 5 + "f" + "i" + "s",
     "hds_paged_rows_per_atom": "",
+    "hds_moe_dispatch": "i" + "pppp" + "iiii" + "s",
+    "hds_moe_dispatch_bwd": "i" + "pppp" + "iiii" + "s",
+    "hds_moe_combine": "i" + "ppppp" + "iiii" + "s",
+    "hds_moe_combine_bwd": "i" + "ppppppp" + "iiii" + "s",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}

@@ -1,0 +1,217 @@
+"""Mixture of Experts with expert parallelism (EP all-to-all over xGMI).
+
+Reference parity: moe/layer.py (``MoE`` :17-132), moe/sharded_moe.py (``TopKGate`` :183-447, ``MOELayer``
+:449-677, ``_AllToAll``), moe/experts.py (``Experts`` :13), moe/utils.py (``split_params_into_different_moe_groups_for_optimizer`` :155, ``is_moe_param``), utils/groups.py expert groups (E+D layout :236-428).
+
+Dispatch is capacity based: tokens are permuted into an expert-major [E, C, H] tensor by the HIP dispatch
+kernel, ONE ``all_to_all_single`` with equal splits moves each expert's slots to its owner (on the full
+xGMI mesh this uses every link of every GPU at once), the local experts run as batched GEMMs
+(``torch.bmm`` -> hipBLASLt) over [E_local, ep*C, H], one all-to-all returns the results and the
+combine kernel un-permutes with the gate weights. No dense [T, E, C] dispatch masks are ever built.
+"""
+import copy
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import comm as dist
+from ..ops.activations import glu
+from ..ops.moe import moe_combine, moe_dispatch, topk_route
+from ..utils import groups
+
+
+class _AllToAll(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        if dist.get_world_size(group) == 1:
+            return x
+        out = torch.empty_like(x)
+        dist.all_to_all_single(out, x.contiguous(), group=group)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return _AllToAll.apply(g, ctx.group), None
+
+
+class TopKGate(nn.Module):
+
+    def __init__(self, model_dim, num_experts, k=1, capacity_factor=1.0, eval_capacity_factor=1.0, min_capacity=8,
+                 noisy_gate_policy=None, drop_tokens=True, use_rts=True, ep_group=None,
+                 top2_2nd_expert_sampling=True):
+        super().__init__()
+        self.wg = nn.Linear(model_dim, num_experts, bias=False)
+        self.k = k
+        self.capacity_factor, self.eval_capacity_factor = capacity_factor, eval_capacity_factor
+        self.min_capacity = min_capacity
+        self.noisy_gate_policy = noisy_gate_policy
+        self.drop_tokens = drop_tokens
+        self.use_rts = use_rts
+        self.ep_group = ep_group
+        self.num_experts = num_experts
+
+    def forward(self, x):
+        logits = F.linear(x.float(), self.wg.weight.float())
+        cf = self.capacity_factor if self.training else self.eval_capacity_factor
+        expert, pos, w, C, l_aux, counts = topk_route(logits, self.k, cf, self.min_capacity, self.drop_tokens,
+                                                      self.use_rts, True, self.noisy_gate_policy, self.training)
+        if not self.drop_tokens and self.ep_group is not None and dist.get_world_size(self.ep_group) > 1:
+            c = torch.tensor([C], device=x.device)
+            dist.all_reduce(c, op=dist.ReduceOp.MAX, group=self.ep_group)
+            C = int(c.item())
+        return expert, pos, w, C, l_aux, counts
+
+
+class Experts(nn.Module):
+    """``num_local_experts`` copies of ``expert`` (reference moe/experts.py). Params are tagged as MoE params."""
+
+    def __init__(self, expert, num_local_experts=1, expert_group_name=None):
+        super().__init__()
+        self.deepspeed_experts = nn.ModuleList([copy.deepcopy(expert) for _ in range(num_local_experts)])
+        self.num_local_experts = num_local_experts
+        self._hds_expert_group = expert_group_name
+        for e in self.deepspeed_experts:
+            for p in e.parameters():
+                p.allreduce = False
+                p.group_name = expert_group_name
+                p._hds_expert_stacked = False
+                p._hds_num_local = num_local_experts
+
+    def forward(self, x):
+        # x: [E_local, N, H]
+        outs = [e(x[i]) for i, e in enumerate(self.deepspeed_experts)]
+        return torch.stack(outs, 0)
+
+
+class GroupedSwiGLUExperts(nn.Module):
+    """E_local SwiGLU experts stored stacked ([E, 2I, H], [E, H, I]) and run as batched GEMMs."""
+
+    def __init__(self, hidden, inter, num_local_experts, expert_group_name=None, std=0.02, act="silu"):
+        super().__init__()
+        self.w13 = nn.Parameter(torch.empty(num_local_experts, 2 * inter, hidden))
+        self.w2 = nn.Parameter(torch.empty(num_local_experts, hidden, inter))
+        self._std = std
+        self.act = act
+        self.num_local_experts = num_local_experts
+        self._hds_expert_group = expert_group_name
+        for p in (self.w13, self.w2):
+            p.allreduce = False
+            p.group_name = expert_group_name
+            p._hds_expert_stacked = True  # dim 0 = local expert index
+            p._hds_num_local = num_local_experts
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.normal_(self.w13, std=self._std)
+        nn.init.normal_(self.w2, std=self._std)
+
+    def forward(self, x):
+        h = torch.bmm(x, self.w13.transpose(1, 2))
+        return torch.bmm(glu(h, self.act), self.w2.transpose(1, 2))
+
+
+class MOELayer(nn.Module):
+
+    def __init__(self, gate, experts, ep_group_name, ep_size, num_local_experts):
+        super().__init__()
+        self.gate = gate
+        self.experts = experts
+        self.ep_group_name = ep_group_name
+        self.ep_size = ep_size
+        self.num_local_experts = num_local_experts
+        self.l_aux = None
+        self.exp_counts = None
+
+    @property
+    def ep_group(self):
+        return groups._State.expert_groups.get(self.ep_group_name) if self.ep_size > 1 else None
+
+    def forward(self, x):
+        shape = x.shape
+        H = shape[-1]
+        x2 = x.reshape(-1, H)
+        E = self.num_local_experts * self.ep_size
+        expert, pos, w, C, l_aux, counts = self.gate(x2)
+        disp = moe_dispatch(x2, expert, pos, E, C)  # [E*C, H], expert-major
+        if self.ep_size > 1:
+            disp = _AllToAll.apply(disp, self.ep_group)  # now [ep(src), E_local, C, H]
+            local = disp.view(self.ep_size, self.num_local_experts, C, H).transpose(0, 1).reshape(
+                self.num_local_experts, self.ep_size * C, H)
+        else:
+            local = disp.view(E, C, H)
+        y = self.experts(local)
+        if self.ep_size > 1:
+            y = y.view(self.num_local_experts, self.ep_size, C, H).transpose(0, 1).reshape(E * C, H)
+            y = _AllToAll.apply(y.contiguous(), self.ep_group)
+        else:
+            y = y.reshape(E * C, H)
+        out = moe_combine(y, expert, pos, w, C)
+        self.l_aux, self.exp_counts = l_aux, counts
+        return out.view(shape)
+
+
+class MoE(nn.Module):
+    """Reference-compatible MoE block: returns (output, l_aux, exp_counts)."""
+
+    def __init__(self, hidden_size, expert=None, num_experts=1, ep_size=1, k=1, capacity_factor=1.0,
+                 eval_capacity_factor=1.0, min_capacity=4, use_residual=False, noisy_gate_policy=None,
+                 drop_tokens=True, use_rts=True, use_tutel=False, enable_expert_tensor_parallelism=False,
+                 top2_2nd_expert_sampling=True, expert_intermediate_size=None):
+        super().__init__()
+        assert num_experts % ep_size == 0, f"num_experts ({num_experts}) must be divisible by ep_size ({ep_size})"
+        self.ep_size = ep_size
+        self.num_experts = num_experts
+        self.num_local_experts = num_experts // ep_size
+        self.expert_group_name = f"ep_size_{ep_size}"
+        if ep_size > 1 and self.expert_group_name not in groups._State.expert_groups:
+            if groups._State.topo is None:
+                groups.initialize()
+            groups._create_expert_and_data_parallel(ep_size)
+        if expert is None:
+            experts = GroupedSwiGLUExperts(hidden_size, expert_intermediate_size or 4 * hidden_size,
+                                           self.num_local_experts, self.expert_group_name)
+        else:
+            experts = Experts(expert, self.num_local_experts, self.expert_group_name)
+        gate = TopKGate(hidden_size, num_experts, k, capacity_factor, eval_capacity_factor, min_capacity,
+                        noisy_gate_policy, drop_tokens, use_rts, None, top2_2nd_expert_sampling)
+        self.deepspeed_moe = MOELayer(gate, experts, self.expert_group_name, ep_size, self.num_local_experts)
+        gate.ep_group = self.deepspeed_moe.ep_group
+        self.use_residual = use_residual
+        if use_residual:
+            self.mlp = copy.deepcopy(expert)
+            self.coefficient = nn.Linear(hidden_size, 2)
+
+    def forward(self, hidden_states, used_token=None):
+        out = self.deepspeed_moe(hidden_states)
+        if self.use_residual:
+            mo = self.mlp(hidden_states)
+            coef = torch.softmax(self.coefficient(hidden_states), dim=-1)
+            out = out * coef[..., 0:1] + mo * coef[..., 1:]
+        return out, self.deepspeed_moe.l_aux, self.deepspeed_moe.exp_counts
+
+
+def is_moe_param(p):
+    return hasattr(p, "allreduce") and not p.allreduce
+
+
+def split_params_into_different_moe_groups_for_optimizer(param_groups, max_group_size=178956971):
+    """Split each optimizer group into dense + one group per expert group (reference moe/utils.py:155)."""
+    if isinstance(param_groups, dict):
+        param_groups = [param_groups]
+    out = []
+    for g in param_groups:
+        dense = {k: v for k, v in g.items() if k != "params"}
+        dense["params"] = [p for p in g["params"] if not is_moe_param(p)]
+        out.append(dense)
+        by = {}
+        for p in g["params"]:
+            if is_moe_param(p):
+                by.setdefault(p.group_name, []).append(p)
+        for name, ps in by.items():
+            ng = {k: v for k, v in g.items() if k != "params"}
+            ng.update(params=ps, moe=True, name=name)
+            out.append(ng)
+    return out

@@ -45,6 +45,14 @@ def _optim_name(engine, save_dir, tag):
     return os.path.join(save_dir, str(tag), f"{prefix}zero_pp_rank_{dp}_mp_rank_{mp:02d}_optim_states.pt")
 
 
+def _max_ep(zopt):
+    return max(zopt._ep_size(u.expert_key) for u in zopt.expert_units)
+
+
+def _expert_name(save_dir, tag, ep_rank):
+    return os.path.join(save_dir, str(tag), f"expp_rank_{ep_rank}_mp_rank_{_mp_rank():02d}_model_states.pt")
+
+
 def _to_cpu(obj):
     if isinstance(obj, torch.Tensor):
         return obj.detach().cpu()
@@ -112,8 +120,13 @@ def save_checkpoint(engine, save_dir, tag=None, client_state=None, save_latest=T
         _write(state, _ckpt_name(engine, save_dir, tag), async_save)
     if zopt is not None:
         osd = {"optimizer_state_dict": zopt.state_dict(), "ds_config": engine.config, "ds_version": __version__}
-        if stage > 0 or dp_rank == 0:
+        if stage > 0 or dp_rank == 0 or (zopt.expert_units and dp_rank < _max_ep(zopt)):
             _write(osd, _optim_name(engine, save_dir, tag), async_save)
+    if stage < 3 and zopt is not None and zopt.expert_units and 0 < dp_rank < _max_ep(zopt):
+        # other EP ranks' experts (model file of stage 0-2 is written by dp rank 0 only)
+        names = {id(p): n for n, p in engine.module.named_parameters()}
+        exp = {names[id(p)]: p.detach().cpu() for u in zopt.expert_units for p in u.params}
+        _write({"module": exp}, _expert_name(save_dir, tag, dp_rank), async_save)
     if rank == 0:
         if save_latest:
             with open(os.path.join(save_dir, "latest"), "w") as f:
@@ -156,6 +169,11 @@ def load_checkpoint(engine, load_dir, tag=None, load_module_strict=True, load_op
     sd = torch.load(mpath, map_location="cpu", weights_only=True) if os.path.exists(mpath) else {}
     if sd.get("module") is not None:
         engine.module.load_state_dict(sd["module"], strict=load_module_strict)
+        if zopt is not None and zopt.expert_units and stage < 3:
+            j = dist.get_rank(engine.dp_group) % _max_ep(zopt)
+            if j > 0:
+                esd = torch.load(_expert_name(load_dir, tag, j), map_location="cpu", weights_only=True)
+                engine.module.load_state_dict(esd["module"], strict=False)
         if zopt is not None:
             zopt.refresh_fp32_from_lp()
     if not load_module_only and zopt is not None and engine._config.load_universal_checkpoint:
@@ -164,8 +182,10 @@ def load_checkpoint(engine, load_dir, tag=None, load_module_strict=True, load_op
     elif not load_module_only and zopt is not None:
         opath = _optim_name(engine, load_dir, tag)
         if not os.path.exists(opath):
+            # stage 0: dp rank 0 (plus one rank per EP position when there are experts) wrote the states
+            j = dist.get_rank(engine.dp_group) % _max_ep(zopt) if zopt.expert_units else 0
             prefix = "bf16_" if engine.bfloat16_enabled() else ""
-            opath = os.path.join(load_dir, tag, f"{prefix}zero_pp_rank_0_mp_rank_{_mp_rank():02d}_optim_states.pt")
+            opath = os.path.join(load_dir, tag, f"{prefix}zero_pp_rank_{j}_mp_rank_{_mp_rank():02d}_optim_states.pt")
         osd = torch.load(opath, map_location="cpu", weights_only=True)
         zopt.load_state_dict(osd["optimizer_state_dict"], load_optimizer_states=load_optimizer_states)
     if not load_module_only:

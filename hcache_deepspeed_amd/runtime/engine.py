@@ -163,8 +163,15 @@ class DeepSpeedEngine(nn.Module):
             src = dist.get_global_rank(self.dp_group, 0) if self.dp_group is not None else 0
             with torch.no_grad():
                 for p in model.parameters():
-                    if not p.is_meta:
-                        dist.broadcast(p.data, src, group=self.dp_group)
+                    if p.is_meta:
+                        continue
+                    eg = groups.expert_data_group_of(p)
+                    if eg is not False:
+                        # expert params: replicas live in the expert-data-parallel group only
+                        if eg is not None and dist.get_world_size(eg) > 1:
+                            dist.broadcast(p.data, dist.get_global_rank(eg, 0), group=eg)
+                        continue
+                    dist.broadcast(p.data, src, group=self.dp_group)
                 for b in model.buffers():
                     if not b.is_meta:
                         dist.broadcast(b.data, src, group=self.dp_group)

@@ -28,6 +28,7 @@ import torch.nn as nn
 
 from ... import comm as dist
 from ...ops import optimizers as fused
+from ...utils import groups
 from ...utils.logging import logger, log_dist
 from ..fp16.loss_scaler import CreateLossScaler
 from .flat import AVAILABLE, INFLIGHT, NOT_AVAILABLE, FlatUnit, ShardStore
@@ -178,6 +179,38 @@ class ZeroOptimizer:
                 g[id(p)] = gi
         return g
 
+    def _comm_key(self, p):
+        """None for dense params; the expert group name for MoE params sharded over an EP group."""
+        eg = groups.expert_data_group_of(p)
+        return None if eg is False else p.group_name
+
+    def _new_unit(self, units, params, group_ids, name, key):
+        """FlatUnit over ``params`` sharded over the dense DP group (key None) or, for expert params,
+        over that expert group's expert-data-parallel group (reference stage3/stage_1_and_2 expert
+        partitioning: ``expert_dp_process_group``)."""
+        if key is None:
+            world, rank = self.layout_world, self.layout_rank
+            dp_g, ag_g, rs_g = self.dp_group, self.ag_group, self.rs_group
+        else:
+            edp = groups._get_expert_data_parallel_group(key)
+            world = 1 if self.stage == 0 else dist.get_world_size(edp)
+            rank = 0 if self.stage == 0 else dist.get_rank(edp)
+            dp_g = ag_g = rs_g = edp
+        u = FlatUnit(len(units), params, group_ids, world, rank, name)
+        u.dp_group, u.ag_group, u.rs_group = dp_g, ag_g, rs_g
+        u.expert_key = key
+        u.direct = world == 1 and self.grad_acc_dtype == self.dtype
+        units.append(u)
+        return u
+
+    def _ep_rank(self, key):
+        ep = groups._get_expert_parallel_group(key)
+        return dist.get_rank(ep) if ep is not None else 0
+
+    def _ep_size(self, key):
+        ep = groups._get_expert_parallel_group(key)
+        return dist.get_world_size(ep) if ep is not None else 1
+
     def _build_units(self, leaf_modules):
         group_of = self._group_of()
         params_all = [p for group in self.param_groups for p in group["params"]]
@@ -186,27 +219,41 @@ class ZeroOptimizer:
         self.layout_world, self.layout_rank = layout_world, layout_rank
         units = []
         if self.stage == 3:
+            claimed = set()
+            # expert containers first: their params shard over the expert-data-parallel group
+            for name, m in self.module.named_modules():
+                if getattr(m, "_hds_expert_group", None) is None:
+                    continue
+                by = {}
+                for p in m.parameters():
+                    if id(p) in group_of and id(p) not in claimed:
+                        by.setdefault(self._comm_key(p), []).append(p)
+                for key, ps in by.items():
+                    claimed.update(id(p) for p in ps)
+                    u = self._new_unit(units, ps, [group_of[id(p)] for p in ps], name, key)
+                    u.module = m
             cands = discover_stage3_units(self.module, leaf_modules)
             count = {}
             for _, m in cands:
                 for p in m.parameters():
                     count[id(p)] = count.get(id(p), 0) + 1
-            claimed = set()
             for name, m in cands:
-                ps = [p for p in m.parameters() if id(p) in group_of and count[id(p)] == 1 and id(p) not in claimed]
+                ps = [p for p in m.parameters() if id(p) in group_of and count[id(p)] == 1 and id(p) not in claimed
+                      and self._comm_key(p) is None]
                 if not ps:
                     continue
-                for p in ps:
-                    claimed.add(id(p))
-                u = FlatUnit(len(units), ps, [group_of[id(p)] for p in ps], layout_world, layout_rank, name)
+                claimed.update(id(p) for p in ps)
+                u = self._new_unit(units, ps, [group_of[id(p)] for p in ps], name, None)
                 u.module = m
-                units.append(u)
-            rest = [p for p in params_all if id(p) not in claimed]
-            if rest:
-                root = FlatUnit(len(units), rest, [group_of[id(p)] for p in rest], layout_world, layout_rank, "root")
+            rest = {}
+            for p in params_all:
+                if id(p) not in claimed:
+                    rest.setdefault(self._comm_key(p), []).append(p)
+            for key, ps in rest.items():
+                root = self._new_unit(units, ps, [group_of[id(p)] for p in ps], "root" if key is None else
+                                      f"root.{key}", key)
                 root.module = self.module
                 root.persistent = True
-                units.append(root)
         else:
             if "reduce_bucket_size" in (self.config.raw.get("zero_optimization") or {}):
                 bucket = int(self.zcfg.reduce_bucket_size)
@@ -214,20 +261,23 @@ class ZeroOptimizer:
                 bucket = int(self.mi.xgmi_bucket_mb * 2**20 // torch.tensor([], dtype=self.dtype).element_size())
             # buckets from the end of the parameter list: they complete first in backward
             for gi, group in enumerate(self.param_groups):
-                cur, size = [], 0
+                cur = {}
                 for p in reversed(group["params"]):
-                    cur.append(p)
+                    key = self._comm_key(p)
+                    lst, size = cur.get(key, ([], 0))
+                    lst.append(p)
                     size += p.numel()
                     if size >= bucket:
-                        units.append(FlatUnit(len(units), cur, [gi] * len(cur), layout_world, layout_rank,
-                                              f"bucket{len(units)}"))
-                        cur, size = [], 0
-                if cur:
-                    units.append(FlatUnit(len(units), cur, [gi] * len(cur), layout_world, layout_rank,
-                                          f"bucket{len(units)}"))
+                        self._new_unit(units, lst, [gi] * len(lst), f"bucket{len(units)}", key)
+                        lst, size = [], 0
+                    cur[key] = (lst, size)
+                for key, (lst, _) in cur.items():
+                    if lst:
+                        self._new_unit(units, lst, [gi] * len(lst), f"bucket{len(units)}", key)
             for u in units:
                 u.persistent = True
         self.units = units
+        self.expert_units = [u for u in units if u.expert_key is not None]
         self.param_to_unit = {}
         for u in units:
             for i, p in enumerate(u.params):
@@ -240,15 +290,18 @@ class ZeroOptimizer:
     def _build_store(self):
         dev = self.device
         self.store = ShardStore(self.units, self.dtype, dev, self.grad_acc_dtype)
-        self.direct_grads = (self.layout_world == 1 and self.grad_acc_dtype == self.dtype)
+        self.direct_grads = all(u.direct for u in self.units)
         from .partition_parameters import materialize_unit
         with torch.no_grad():
             for u in self.units:
-                repl = materialize_unit(u, dev, self.dtype, seed=int(self.config.seed or 1234) + 7919 * u.uid)
+                seed = int(self.config.seed or 1234) + 7919 * u.uid
+                if u.expert_key is not None:
+                    seed += 1000003 * (1 + self._ep_rank(u.expert_key))  # distinct experts per EP rank
+                repl = materialize_unit(u, dev, self.dtype, seed=seed)
                 if repl:
                     self._swap_params(u, repl)
                 lp = self.store.lp_slice(u)
-                if self.layout_world == 1:
+                if u.world == 1:
                     full = lp  # alias: parameters live in the optimizer's lp shard
                     u.copy_params_into(full)
                 else:
@@ -258,7 +311,7 @@ class ZeroOptimizer:
                 u.shard_tensor = lp
                 for p in u.params:
                     p.ds_tensor = lp
-                if u.persistent or self.layout_world == 1:
+                if u.persistent or u.world == 1:
                     u.full = full
                     u.bind_params(full)
                     u.status = AVAILABLE
@@ -267,8 +320,8 @@ class ZeroOptimizer:
                     u.unbind_params(_empty(self.dtype, dev))
                     u.status = NOT_AVAILABLE
                     del full
-                if u.persistent or self.layout_world == 1:
-                    if self.direct_grads:
+                if u.persistent or u.world == 1:
+                    if u.direct:
                         u.grad_full = self.store.grad_slice(u)
                     else:
                         u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=dev)
@@ -371,7 +424,7 @@ class ZeroOptimizer:
             grad_on = torch.is_grad_enabled()
             if grad_on and not self.in_backward:
                 output = self._wrap_outputs(u, output)
-            if self.layout_world > 1 and not self.in_backward and not self._is_last_in_trace(u):
+            if u.world > 1 and not self.in_backward and not self._is_last_in_trace(u):
                 self._release(u)
             return output
 
@@ -412,7 +465,7 @@ class ZeroOptimizer:
     def _gather(self, u, wait=True):
         if u.status == NOT_AVAILABLE:
             full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
-            u.work = dist.all_gather_into_tensor(full, u.shard_tensor, group=self.ag_group, async_op=True)
+            u.work = dist.all_gather_into_tensor(full, u.shard_tensor, group=u.ag_group, async_op=True)
             u.full = full
             u.bind_params(full)
             u.status = INFLIGHT
@@ -425,7 +478,7 @@ class ZeroOptimizer:
             u.bind_grads(u.grad_full)
 
     def _release(self, u):
-        if u.persistent or self.layout_world == 1 or u.status == NOT_AVAILABLE:
+        if u.persistent or u.world == 1 or u.status == NOT_AVAILABLE:
             return
         if u.status == INFLIGHT:
             u.work.wait()
@@ -470,31 +523,31 @@ class ZeroOptimizer:
         if self.stage == 0:
             if not self.boundary:
                 return  # grads keep accumulating in the unit buffer until the boundary
-            w = dist.all_reduce(u.grad_full, group=self.dp_group, async_op=True)
+            w = dist.all_reduce(u.grad_full, group=u.dp_group, async_op=True)
             post = None
-            if not self.direct_grads:
+            if not u.direct:
                 post = (lambda d=self.store.grad_slice(u), g=u.grad_full: d.copy_(g))
             self.pending_works.append((w, post))
             return
         if self.stage == 1 and not self.boundary:
             return
-        if self.direct_grads:
+        if u.direct:
             return  # grads already accumulated in place inside the optimizer shard
         dst = self.store.grad_slice(u)
         first = self.micro_in_window == 0 or self.stage == 1
         src = u.grad_full if u.grad_full.dtype == self.comm_dtype else u.grad_full.to(self.comm_dtype)
         if first and dst.dtype == self.comm_dtype:
-            w = dist.reduce_scatter_tensor(dst, src, group=self.rs_group, async_op=True)
+            w = dist.reduce_scatter_tensor(dst, src, group=u.rs_group, async_op=True)
             post = None
         else:
             tmp = torch.empty(u.shard, dtype=self.comm_dtype, device=self.device)
-            w = dist.reduce_scatter_tensor(tmp, src, group=self.rs_group, async_op=True)
+            w = dist.reduce_scatter_tensor(tmp, src, group=u.rs_group, async_op=True)
             if first:
                 post = (lambda d=dst, t=tmp: d.copy_(t))
             else:
                 post = (lambda d=dst, t=tmp: d.add_(t))
         keep = (src, )
-        if self.stage == 3 and not u.persistent and self.layout_world > 1:
+        if self.stage == 3 and not u.persistent and u.world > 1:
             gf = u.grad_full
             u.unbind_grads()
             u.grad_full = None
@@ -508,9 +561,7 @@ class ZeroOptimizer:
         for u in self.units:
             u.pending = u.requires_grad_count
             u.grads_reduced = False
-            if self.stage in (1, 2, 0) and not self.direct_grads and u.grad_full is not None:
-                u.bind_grads(u.grad_full)
-            elif self.direct_grads:
+            if u.grad_full is not None and (u.direct or self.stage in (1, 2, 0)):
                 u.bind_grads(u.grad_full)
 
     def finish_backward(self):
@@ -526,12 +577,12 @@ class ZeroOptimizer:
             if post is not None:
                 post()
         self.pending_works = []
-        if self.stage in (2, 3) and not self.direct_grads:
+        if self.stage in (2, 3):
             # the per-micro-step reduction consumed these; persistent buffers restart from zero
             for u in self.units:
-                if u.grad_full is not None:
+                if u.grad_full is not None and not u.direct:
                     u.grad_full.zero_()
-        if self.stage == 3 and self.layout_world > 1:
+        if self.stage == 3:
             for u in self.units:
                 if not u.persistent:
                     self._release(u)
@@ -571,7 +622,7 @@ class ZeroOptimizer:
     def zero_grad(self, set_to_none=True):
         self.store.grad.zero_()
         for u in self.units:
-            if u.grad_full is not None and not self.direct_grads:
+            if u.grad_full is not None and not u.direct:
                 u.grad_full.zero_()
         self.micro_in_window = 0
 
@@ -639,6 +690,18 @@ class ZeroOptimizer:
                 dist.all_reduce(self._rep_buf, group=self.dp_group)
         if self.loss_scaler.dynamic and self.dp_world > 1:
             dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.dp_group)
+        if self.stage == 0 and self.expert_units:
+            # stage 0 keeps every expert unit whole on its owners: add the other EP ranks' experts
+            for key in sorted({u.expert_key for u in self.expert_units}):
+                ep = groups._get_expert_parallel_group(key)
+                if ep is None or dist.get_world_size(ep) == 1:
+                    continue
+                buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+                fused.grad_sumsq([self.store.grad_slice(u) for u in self.expert_units if u.expert_key == key],
+                                 out=buf)
+                tot = buf.clone()
+                dist.all_reduce(tot, group=ep)
+                self._norm_buf.add_(tot - buf)
         if self.mp_group is not None:
             sharded = self._norm_buf - self._rep_buf
             dist.all_reduce(sharded, group=self.mp_group)
@@ -648,15 +711,13 @@ class ZeroOptimizer:
 
     def _post_step_gather(self):
         """ZeRO-1/2: rebuild the persistent full parameters from the updated shards."""
-        if self.layout_world == 1:
-            return
         works = []
         for u in self.units:
-            if self.stage == 3 and not u.persistent:
-                continue  # re-gathered on demand by the next forward
+            if u.world == 1 or (self.stage == 3 and not u.persistent):
+                continue  # aliased / re-gathered on demand by the next forward
             if u.full is None:
                 continue
-            works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor, group=self.ag_group, async_op=True))
+            works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor, group=u.ag_group, async_op=True))
         for w in works:
             w.wait()
 
@@ -681,7 +742,14 @@ class ZeroOptimizer:
                 "shard": u.shard,
                 "padded": u.padded,
                 "store_off": u.store_off,
+                "world": u.world,
+                "rank": u.rank,
+                "expert_group": u.expert_key,
             })
+            if u.expert_key is not None:
+                units[-1].update(ep_size=self._ep_size(u.expert_key), ep_rank=self._ep_rank(u.expert_key),
+                                 expert_stacked=[bool(getattr(p, "_hds_expert_stacked", False)) for p in u.params],
+                                 num_local=[int(getattr(p, "_hds_num_local", 1)) for p in u.params])
         return {"stage": self.stage, "world": self.layout_world, "rank": self.layout_rank, "units": units,
                 "store_numel": self.store.numel}
 
@@ -726,7 +794,7 @@ class ZeroOptimizer:
     def refresh_fp32_from_lp(self):
         with torch.no_grad():
             for u in self.units:
-                if u.full is not None and self.layout_world > 1 and u.status == AVAILABLE:
+                if u.full is not None and u.world > 1 and u.status == AVAILABLE:
                     self.store.lp_slice(u).copy_(u.full[u.rank * u.shard:(u.rank + 1) * u.shard])
             self.store.master.copy_(self.store.lp)
 
@@ -742,15 +810,31 @@ class ZeroOptimizer:
             self._release(u)
 
     def full_fp32_state_dict(self, names):
-        """Consolidated fp32 weights {name: tensor} on every rank (all-gathers the master shards)."""
+        """Consolidated fp32 weights {name: tensor} on every rank (all-gathers the master shards; expert
+        params are also gathered over their EP group and named/stacked by global expert id)."""
+        from ...checkpoint.zero_to_fp32 import expert_global_name
         out = {}
         for u in self.units:
             m = self.store.master[u.store_off:u.store_off + u.shard]
             full = torch.empty(u.padded, dtype=torch.float32, device=self.device)
-            if self.layout_world > 1:
-                dist.all_gather_into_tensor(full, m, group=self.dp_group)
+            if u.world > 1:
+                dist.all_gather_into_tensor(full, m, group=u.dp_group)
             else:
                 full.copy_(m)
+            if u.expert_key is not None and self._ep_size(u.expert_key) > 1:
+                P = self._ep_size(u.expert_key)
+                allj = torch.empty(P * u.padded, dtype=torch.float32, device=self.device)
+                dist.all_gather_into_tensor(allj, full, group=groups._get_expert_parallel_group(u.expert_key))
+                per_j = allj.view(P, u.padded)
+                for i, p in enumerate(u.params):
+                    name = names.get(id(p), f"param_{id(p)}")
+                    parts = [u.param_view(per_j[j], i).detach().cpu().clone() for j in range(P)]
+                    if getattr(p, "_hds_expert_stacked", False):
+                        out[name] = torch.cat(parts, 0)
+                    else:
+                        for j in range(P):
+                            out[expert_global_name(name, j, int(getattr(p, "_hds_num_local", 1)))] = parts[j]
+                continue
             for i, p in enumerate(u.params):
                 out[names.get(id(p), f"param_{id(p)}")] = u.param_view(full, i).detach().cpu().clone()
         return out

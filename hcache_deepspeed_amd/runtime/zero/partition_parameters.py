@@ -63,13 +63,15 @@ def materialize_unit(unit, device, dtype, seed):
         return {}
     repl = {}
     mods = []
+    mine = {id(p) for p in metas}
     for m in unit.module.modules():
         touched = False
         for n, p in list(m._parameters.items()):
-            if p is not None and p.is_meta:
+            if p is not None and p.is_meta and id(p) in mine:
                 if id(p) not in repl:
                     new = nn.Parameter(torch.empty(p.shape, dtype=dtype or p.dtype, device=device),
                                        requires_grad=p.requires_grad)
+                    new.__dict__.update(p.__dict__)  # tags: allreduce/group_name/tensor-parallel flags
                     repl[id(p)] = new
                 m._parameters[n] = repl[id(p)]
                 touched = True
@@ -134,15 +136,15 @@ class GatheredParameters:
         with torch.no_grad():
             for z, u in self.units:
                 if self.modifier_rank is not None:
-                    if z.dp_world > 1:
-                        src = dist.get_global_rank(z.dp_group, self.modifier_rank) if z.dp_group is not None \
+                    if u.world > 1:
+                        src = dist.get_global_rank(u.dp_group, self.modifier_rank) if u.dp_group is not None \
                             else self.modifier_rank
-                        dist.broadcast(u.full, src, group=z.dp_group)
+                        dist.broadcast(u.full, src, group=u.dp_group)
                     lp = z.store.lp_slice(u)
                     if u.full.data_ptr() != lp.data_ptr():
                         lp.copy_(u.full[u.rank * u.shard:(u.rank + 1) * u.shard])
                     z.store.master[u.store_off:u.store_off + u.shard].copy_(lp)
-                if not u.persistent and z.layout_world > 1 and not z.in_backward:
+                if not u.persistent and u.world > 1 and not z.in_backward:
                     z._release(u)
         self.units = []
         return False

@@ -184,6 +184,16 @@ def _get_expert_data_parallel_group(group_name):
     return _State.expert_data_groups[group_name]
 
 
+def expert_data_group_of(p):
+    """Expert-data-parallel group of an MoE parameter; ``False`` for dense params (or EP not set up)."""
+    if getattr(p, "allreduce", True):
+        return False
+    name = getattr(p, "group_name", None)
+    if name is None or name not in _State.expert_data_groups:
+        return False
+    return _State.expert_data_groups[name]
+
+
 def _get_expert_parallel_group_dict():
     return dict(_State.expert_groups)
 
