@@ -156,6 +156,8 @@ class ZeroOptimizer:
         self.boundary = True
         self.in_backward = False
         self.pending_works = []
+        self.hold_reduction = False
+        self._held = []
         self.global_norm = None
         self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._inf_buf = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -520,6 +522,34 @@ class ZeroOptimizer:
     # ------------------------------------------------------------------------------------
     def _unit_grads_ready(self, u):
         u.grads_reduced = True
+        if self.hold_reduction and self.boundary:
+            if not self._held:
+                self._held_micro = self.micro_in_window
+            self._held.append(u)  # reduced later by release_held_reductions() (pipeline tied grads)
+            return
+        self._reduce_unit(u)
+
+    def release_held_reductions(self):
+        held, self._held = self._held, []
+        cur, self.micro_in_window = self.micro_in_window, getattr(self, "_held_micro", 0)
+        for u in held:
+            self._reduce_unit(u)
+        self.micro_in_window = cur
+        self._drain_pending()
+        if self.stage in (2, 3):
+            for u in held:
+                if u.grad_full is not None and not u.direct:
+                    u.grad_full.zero_()
+
+    def _drain_pending(self):
+        for item in self.pending_works:
+            w, post = item[0], item[1]
+            w.wait()
+            if post is not None:
+                post()
+        self.pending_works = []
+
+    def _reduce_unit(self, u):
         if self.stage == 0:
             if not self.boundary:
                 return  # grads keep accumulating in the unit buffer until the boundary
@@ -571,16 +601,12 @@ class ZeroOptimizer:
                     # unit never ran backward (unused): contribute zeros so collectives stay matched
                     self._gather(u, wait=True)
                 self._unit_grads_ready(u)
-        for item in self.pending_works:
-            w, post = item[0], item[1]
-            w.wait()
-            if post is not None:
-                post()
-        self.pending_works = []
+        self._drain_pending()
         if self.stage in (2, 3):
             # the per-micro-step reduction consumed these; persistent buffers restart from zero
+            held = {id(h) for h in self._held}
             for u in self.units:
-                if u.grad_full is not None and not u.direct:
+                if u.grad_full is not None and not u.direct and id(u) not in held:
                     u.grad_full.zero_()
         if self.stage == 3:
             for u in self.units:
