@@ -203,6 +203,8 @@ class DeepSpeedConfig:
         self.train_batch_size = c.get("train_batch_size")
         self.train_micro_batch_size_per_gpu = c.get("train_micro_batch_size_per_gpu")
         self.gradient_accumulation_steps = c.get("gradient_accumulation_steps")
+        if (c.get("elasticity") or {}).get("enabled", False):
+            self._apply_elasticity(c)
         self._triangulate_batch()
 
         # optimizer / scheduler
@@ -313,6 +315,23 @@ class DeepSpeedConfig:
             raise ConfigError(f"Check batch related parameters. train_batch_size is not equal to micro_batch_per_gpu "
                               f"* gradient_acc_step * world_size {tb} != {mb} * {gas} * {ws}")
         self.train_batch_size, self.train_micro_batch_size_per_gpu, self.gradient_accumulation_steps = tb, mb, gas
+
+    def _apply_elasticity(self, c):
+        """Elastic batch plan overrides the batch keys (reference runtime/config.py:758-800)."""
+        from ..elasticity import compute_elastic_config, ensure_immutable_elastic_config
+        from ..elasticity.elasticity import ElasticityConfig
+        from ..version import __version__
+        ec = ElasticityConfig(c["elasticity"])
+        ensure_immutable_elastic_config(c["elasticity"])
+        bs, gpus, mbs = compute_elastic_config(c, __version__, world_size=self.world_size)
+        if not ec.ignore_non_elastic_batch_info:
+            for k in ("train_batch_size", "train_micro_batch_size_per_gpu", "gradient_accumulation_steps"):
+                if c.get(k) is not None:
+                    raise ConfigError(f"elasticity is enabled: remove '{k}' or set ignore_non_elastic_batch_info")
+        self.train_batch_size = bs
+        self.train_micro_batch_size_per_gpu = mbs
+        self.gradient_accumulation_steps = bs // (mbs * self.world_size)
+        self.elastic_valid_gpus = gpus
 
     def print(self, name="DeepSpeedEngine configuration"):
         logger.info(f"{name}: {json.dumps(self.raw, indent=2, default=str)}")
