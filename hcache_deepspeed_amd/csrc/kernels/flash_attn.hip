@@ -60,6 +60,18 @@ __device__ __forceinline__ void seq_bounds(const AttnParams& p, int b, int& star
   }
 }
 
+// Launch grids are (blocks-per-sequence, heads, batch); reinterpret the linear workgroup id so the
+// block index within a sequence varies SLOWEST: the dispatcher then starts every (head, batch)'s
+// heaviest causal block before any lighter one (longest-processing-time-first across 256 CUs).
+__device__ __forceinline__ void lpt_ids(int& blk, int& head, int& b) {
+  const int heads = gridDim.y, nb = gridDim.z;
+  const int lid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  blk = lid / (heads * nb);
+  const int rem = lid - blk * heads * nb;
+  head = rem % heads;
+  b = rem / heads;
+}
+
 __device__ __forceinline__ bool masked(const AttnParams& p, int qi, int kj, int len) {
   if (kj >= len || qi >= len) return true;
   if (p.causal && kj > qi) return true;
@@ -74,11 +86,12 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
-  const int b = blockIdx.z, hq = blockIdx.y;
+  int blk, hq, b;
+  lpt_ids(blk, hq, b);
   int start, len;
   seq_bounds(p, b, start, len);
   const int nqb = (len + BM - 1) / BM;
-  const int qb = p.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;  // heaviest causal blocks first
+  const int qb = p.causal ? (gridDim.x - 1 - blk) : blk;  // heaviest causal blocks first
   if (qb >= nqb || len == 0) return;
   const int hk = hq / (p.hq / p.hkv);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
@@ -384,17 +397,183 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
 }
 
 // =====================================================================================
+// backward dK/dV, 8 waves, K/V resident in LDS (2 waves per SIMD)
+// =====================================================================================
+// Workgroup = 128 keys of one (batch, kv-head). Wave w owns key group kg = w & 3 (32 keys, key on
+// the lane) and query half qh = w >> 2 of every 64-row Q/dO tile, so the 8 waves split each tile's
+// work instead of each holding private K/V fragments: K and V live in LDS (64 KiB) and are read as
+// the B operand exactly like Q rows are read as the A operand. Per wave: dK/dV accumulators
+// (128 regs) + one 32x32 S/dP pair, which fits 256 registers -> 2 waves per SIMD, so one wave's
+// softmax/VALU section overlaps the other wave's MFMAs. The two query halves' partial dK/dV are
+// summed through LDS once at the end.
+__global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) {
+  constexpr int BK = 128;
+  // LDS: K (2 x 16K), V (2 x 16K), Q[2] (16K each), dO[2] (16K each), lse[2][64], delta[2][64]
+  __shared__ __attribute__((aligned(16))) char smem[8 * 16384 + 4 * 256];
+  char* const Kt = smem;
+  char* const Vt = smem + 2 * 16384;
+  char* const Qbase = smem + 4 * 16384;
+  char* const Obase = smem + 6 * 16384;
+  float* const LDbase = reinterpret_cast<float*>(smem + 8 * 16384);
+  int kb, hk, b;
+  lpt_ids(kb, hk, b);
+  int start, len;
+  seq_bounds(p, b, start, len);
+  const int nkb = (len + BK - 1) / BK;
+  if (kb >= nkb || len == 0) return;
+  const int G = p.hq / p.hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int kg = w & 3, qh = w >> 2;
+  const int kw0 = kb * BK + 32 * kg;  // this wave's first key
+  const int myk = kw0 + (lane & 31);
+  const float c = p.scale * kLog2e;
+  const char* Kw = Kt + (kg >> 1) * 16384;
+  const char* Vw = Vt + (kg >> 1) * 16384;
+  const int krow0 = 32 * (kg & 1);
+
+  // K / V tiles of the block (rows clamped to the sequence)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    stage_tile64<8>(Kt + t * 16384, [=](int row) {
+      int r = kb * BK + 64 * t + row;
+      r = r < len ? r : len - 1;
+      return p.k + (int64_t)(start + r) * p.sk + (int64_t)hk * D;
+    });
+    stage_tile64<8>(Vt + t * 16384, [=](int row) {
+      int r = kb * BK + 64 * t + row;
+      r = r < len ? r : len - 1;
+      return p.v + (int64_t)(start + r) * p.sv + (int64_t)hk * D;
+    });
+  }
+
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x16{};
+
+  int qt_begin = 0;
+  if (p.causal) qt_begin = (kb * BK) / BN;
+  int qt_end = (len + BN - 1) / BN;
+  if (p.window > 0) {
+    const int lastq = kb * BK + BK - 1 + p.window - 1;
+    const int e = lastq / BN + 1;
+    qt_end = e < qt_end ? e : qt_end;
+  }
+  const int nqt = qt_end - qt_begin;
+  const int total = nqt * G;
+
+  auto stage = [&](int it, int buf) {
+    const int g = it / nqt, qt = qt_begin + it % nqt;
+    const int hq = hk * G + g;
+    stage_tile64<8>(Qbase + buf * 16384, [=](int row) {
+      int r = qt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.q + (int64_t)(start + r) * p.sq + (int64_t)hq * D;
+    });
+    stage_tile64<8>(Obase + buf * 16384, [=](int row) {
+      int r = qt * BN + row;
+      r = r < len ? r : len - 1;
+      return p.dout + (int64_t)(start + r) * p.sdo + (int64_t)hq * D;
+    });
+    if (w < 2) {
+      int r = qt * BN + lane;
+      r = r < len ? r : len - 1;
+      const float* src = (w == 0 ? p.lse : p.delta) + (int64_t)hq * p.total_tokens + start + r;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(LDbase + buf * 64 + w * 128), 4, 0, 0);
+    }
+  };
+
+  if (total > 0) stage(0, 0);
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < total) stage(it + 1, buf ^ 1);
+    const int qt = qt_begin + it % nqt;
+    const char* Qt = Qbase + buf * 16384;
+    const char* Ot = Obase + buf * 16384;
+    const float* Lt = LDbase + buf * 64;
+    const float* Dt = LDbase + 128 + buf * 64;
+    const int q0 = qt * BN + 32 * qh;  // this wave's first query
+    bool skip = (kw0 >= len) || (q0 >= len);
+    if (p.causal && q0 + 31 < kw0) skip = true;
+    if (p.window > 0 && q0 > kw0 + 31 + p.window - 1) skip = true;
+    if (!skip) {
+      const bool need_mask = (p.causal && q0 < kw0 + 31) || p.window > 0 || q0 + 32 > len || kw0 + 32 > len;
+      f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) sacc = mfma(read_rows(Qt, 32 * qh, ks), read_rows(Kw, krow0, ks), sacc);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) dpacc = mfma(read_rows(Ot, 32 * qh, ks), read_rows(Vw, krow0, ks), dpacc);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int qr0 = 32 * qh + 8 * r4 + 4 * h;  // rows acc_row(4*r4 + j, h) = qr0 + j
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(Lt + qr0);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dt + qr0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * r4 + j;
+          float pr = fast_exp2(sacc[r] * c - l4[j] * kLog2e);
+          if (need_mask && masked(p, qt * BN + qr0 + j, myk, len)) pr = 0.f;
+          sacc[r] = pr;
+          dpacc[r] = pr * (dpacc[r] - d4[j]);
+        }
+      }
+      const bf16x8 p0 = acc_to_b<0>(sacc), p1 = acc_to_b<1>(sacc);
+      const bf16x8 s0 = acc_to_b<0>(dpacc), s1 = acc_to_b<1>(dpacc);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma(read_tr(Ot, 2 * qh, dt), p0, dv[dt]);
+        dv[dt] = mfma(read_tr(Ot, 2 * qh + 1, dt), p1, dv[dt]);
+        dk[dt] = mfma(read_tr(Qt, 2 * qh, dt), s0, dk[dt]);
+        dk[dt] = mfma(read_tr(Qt, 2 * qh + 1, dt), s1, dk[dt]);
+      }
+    }
+    __syncthreads();
+  }
+  // sum the two query halves: qh=1 waves park their partials in LDS (32 KiB per wave)
+  float* red = reinterpret_cast<float*>(smem) + kg * 8192;
+  if (qh == 1) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        red[(dt * 16 + r) * 64 + lane] = dk[dt][r];
+        red[(64 + dt * 16 + r) * 64 + lane] = dv[dt][r];
+      }
+  }
+  __syncthreads();
+  if (qh == 0 && myk < len) {
+    bf16* kp = p.dk + (int64_t)(start + myk) * p.sdk + (int64_t)hk * D;
+    bf16* vp = p.dv + (int64_t)(start + myk) * p.sdv + (int64_t)hk * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 a4, b4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          a4[j] = (bf16)((dk[dt][r] + red[(dt * 16 + r) * 64 + lane]) * p.scale);
+          b4[j] = (bf16)(dv[dt][r] + red[(64 + dt * 16 + r) * 64 + lane]);
+        }
+        *reinterpret_cast<bf16x4*>(kp + 32 * dt + 8 * g + 4 * h) = a4;
+        *reinterpret_cast<bf16x4*>(vp + 32 * dt + 8 * g + 4 * h) = b4;
+      }
+  }
+}
+
+// =====================================================================================
 // backward dQ
 // =====================================================================================
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
-  const int b = blockIdx.z, hq = blockIdx.y;
+  int blk, hq, b;
+  lpt_ids(blk, hq, b);
   int start, len;
   seq_bounds(p, b, start, len);
   const int nqb = (len + BM - 1) / BM;
-  const int qb = p.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const int qb = p.causal ? (gridDim.x - 1 - blk) : blk;
   if (qb >= nqb || len == 0) return;
   const int hk = hq / (p.hq / p.hkv);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
@@ -537,7 +716,7 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 }  // namespace
 
-int g_fwd_nw = 8, g_dkdv_nw = 4, g_dq_nw = 8;
+int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8;
 
 // runtime selection of the waves-per-workgroup variants (4 or 8)
 HDS_EXPORT int hds_attn_config(int fwd_nw, int dkdv_nw, int dq_nw) {
@@ -572,7 +751,7 @@ HDS_EXPORT int hds_attn_bwd(const void* q, const void* k, const void* v, const v
   const int64_t rows = (int64_t)total_tokens * hq;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, st, p);
   if (g_dkdv_nw == 8)
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<8>, dim3((max_len + 255) / 256, hkv, batch), dim3(512), 0, st, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel, dim3((max_len + 127) / 128, hkv, batch), dim3(512), 0, st, p);
   else
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<4>, dim3((max_len + 127) / 128, hkv, batch), dim3(256), 0, st, p);
   if (g_dq_nw == 8)

@@ -46,6 +46,11 @@ _KERNEL_SIGS = {
     "hds_moe_dispatch_bwd": "i" + "pppp" + "iiii" + "s",
     "hds_moe_combine": "i" + "ppppp" + "iiii" + "s",
     "hds_moe_combine_bwd": "i" + "ppppppp" + "iiii" + "s",
+    "hds_quant_int": "i" + "pppp" + "l" + "iii" + "s",
+    "hds_dequant_int": "i" + "pppp" + "l" + "iii" + "s",
+    "hds_quant_fp8": "i" + "ppp" + "l" + "ii" + "s",
+    "hds_dequant_fp8": "i" + "ppp" + "l" + "ii" + "s",
+    "hds_dequant_reduce": "i" + "ppp" + "i" + "l" + "iii" + "s",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}

@@ -143,11 +143,13 @@ class ZeroOptimizer:
         # communicators: all-gather and reduce-scatter on separate RCCL streams for ZeRO-3
         self.ag_group = dp_group
         self.rs_group = dp_group
-        if self.stage == 3 and self.dp_world > 1:
-            ranks = (list(range(dist.get_world_size())) if dp_group is None else
-                     torch.distributed.get_process_group_ranks(dp_group))
-            self.ag_group = dist.new_group(ranks=ranks)
-            self.rs_group = dist.new_group(ranks=ranks)
+        self.norm_group = dp_group
+        dp_ranks = (list(range(dist.get_world_size())) if dp_group is None else
+                    torch.distributed.get_process_group_ranks(dp_group)) if self.dp_world > 1 else [dist.get_rank()]
+        self._setup_zeropp(dp_ranks)
+        if self.stage == 3 and self.dp_world > 1 and not self.mics:
+            self.ag_group = dist.new_group(ranks=dp_ranks)
+            self.rs_group = dist.new_group(ranks=dp_ranks)
 
         self._build_units(leaf_modules)
         self._build_store()
@@ -181,6 +183,84 @@ class ZeroOptimizer:
                 g[id(p)] = gi
         return g
 
+    # ------------------------------------------------------------------------------------
+    # ZeRO++ (qwZ / qgZ / hpZ) and MiCS
+    # ------------------------------------------------------------------------------------
+    def _setup_zeropp(self, dp_ranks):
+        """Reference: partition_parameters.py qwZ (:770-810), coalesced_collectives.py qgZ (:31-76), hpZ secondary
+        partition (utils/groups.py:650, partition_parameters.py:1673) and runtime/zero/mics.py (shard groups +
+        replica all-reduce). Groups are built from contiguous data-parallel rank blocks (one xGMI island)."""
+        z = self.zcfg
+        self.qwz = bool(z.zero_quantized_weights) and self.stage == 3 and self.dp_world > 1
+        self.qgz = bool(z.zero_quantized_gradients) and self.stage in (2, 3) and self.dp_world > 1
+        self.qgz_bits = int(getattr(self.mi, "qgz_bits", 8) or 8)
+        self.hpz = int(z.zero_hpz_partition_size or 1) if self.stage == 3 else 1
+        self.mics = int(z.mics_shard_size) if (z.mics_shard_size or 0) > 0 and self.stage > 0 else 0
+        if self.mics >= self.dp_world:
+            self.mics = 0
+        if self.hpz >= self.dp_world:
+            self.hpz = 1
+        self.hpz_group = self.shard_group = self.replica_group = None
+        me = dist.get_rank()
+
+        def blocks(size):
+            mine = None
+            for i in range(0, len(dp_ranks), size):
+                rk = dp_ranks[i:i + size]
+                g = dist.new_group(ranks=rk)
+                if me in rk:
+                    mine = g
+            return mine
+
+        if self.hpz > 1:
+            assert self.dp_world % self.hpz == 0, "zero_hpz_partition_size must divide the data-parallel size"
+            self.hpz_group = blocks(self.hpz)
+            self.hpz_rank = self.dp_rank % self.hpz
+        if self.mics:
+            assert self.dp_world % self.mics == 0, "mics_shard_size must divide the data-parallel size"
+            self.shard_group = blocks(self.mics)
+            ag = blocks(self.mics) if self.stage == 3 else self.shard_group
+            rep = None
+            for j in range(self.mics):
+                rk = dp_ranks[j::self.mics]
+                g = dist.new_group(ranks=rk)
+                if me in rk:
+                    rep = g
+            self.replica_group = rep
+            self.ag_group, self.rs_group, self.norm_group = ag, self.shard_group, self.shard_group
+
+    @staticmethod
+    def _qgroup(n):
+        for g in (2048, 1024, 512, 256, 128, 64):
+            if n % g == 0:
+                return g
+        return 8
+
+    def _qwz_gather(self, u, full):
+        """qwZ: all-gather int8 shards + fp32 group scales in ONE collective, dequantize into ``full``."""
+        from ...ops import quantizer as Q
+        G = self._qgroup(u.shard)
+        q, sc, _ = Q.quantize(u.shard_tensor, G, 8, True)
+        ng = sc.numel()
+        nbytes = u.shard + 4 * ng
+        send = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        send[:u.shard].copy_(q.view(torch.uint8))
+        send[u.shard:].copy_(sc.view(torch.uint8))
+        recv = torch.empty(u.world * nbytes, dtype=torch.uint8, device=self.device)
+        work = dist.all_gather_into_tensor(recv, send, group=u.ag_group, async_op=True)
+
+        def post():
+            rv = recv.view(u.world, nbytes)
+            for r in range(u.world):
+                dst = full[r * u.shard:(r + 1) * u.shard]
+                if r == u.rank:
+                    dst.copy_(u.shard_tensor)  # own shard exact
+                else:
+                    Q.dequantize(rv[r, :u.shard].view(torch.int8), rv[r, u.shard:].view(torch.float32), None, G, 8,
+                                 True, self.dtype, out=dst)
+
+        return work, post
+
     def _comm_key(self, p):
         """None for dense params; the expert group name for MoE params sharded over an EP group."""
         eg = groups.expert_data_group_of(p)
@@ -192,7 +272,8 @@ class ZeroOptimizer:
         partitioning: ``expert_dp_process_group``)."""
         if key is None:
             world, rank = self.layout_world, self.layout_rank
-            dp_g, ag_g, rs_g = self.dp_group, self.ag_group, self.rs_group
+            dp_g = self.shard_group if self.mics else self.dp_group
+            ag_g, rs_g = self.ag_group, self.rs_group
         else:
             edp = groups._get_expert_data_parallel_group(key)
             world = 1 if self.stage == 0 else dist.get_world_size(edp)
@@ -216,8 +297,8 @@ class ZeroOptimizer:
     def _build_units(self, leaf_modules):
         group_of = self._group_of()
         params_all = [p for group in self.param_groups for p in group["params"]]
-        layout_world = 1 if self.stage == 0 else self.dp_world
-        layout_rank = 0 if self.stage == 0 else self.dp_rank
+        layout_world = 1 if self.stage == 0 else (self.mics or self.dp_world)
+        layout_rank = 0 if self.stage == 0 else (self.dp_rank % self.mics if self.mics else self.dp_rank)
         self.layout_world, self.layout_rank = layout_world, layout_rank
         units = []
         if self.stage == 3:
@@ -467,13 +548,23 @@ class ZeroOptimizer:
     def _gather(self, u, wait=True):
         if u.status == NOT_AVAILABLE:
             full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
-            u.work = dist.all_gather_into_tensor(full, u.shard_tensor, group=u.ag_group, async_op=True)
+            u.post_gather = None
+            if self.in_backward and getattr(u, "sec", None) is not None:
+                # hpZ: backward re-gather from the secondary (intra-group) partition
+                u.work = dist.all_gather_into_tensor(full, u.sec, group=self.hpz_group, async_op=True)
+            elif self.qwz and u.expert_key is None:
+                u.work, u.post_gather = self._qwz_gather(u, full)
+            else:
+                u.work = dist.all_gather_into_tensor(full, u.shard_tensor, group=u.ag_group, async_op=True)
             u.full = full
             u.bind_params(full)
             u.status = INFLIGHT
         if wait and u.status == INFLIGHT:
             u.work.wait()
             u.work = None
+            if getattr(u, "post_gather", None) is not None:
+                u.post_gather()
+                u.post_gather = None
             u.status = AVAILABLE
         if self.in_backward and u.grad_full is None and u.requires_grad_count:
             u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=self.device)
@@ -485,6 +576,13 @@ class ZeroOptimizer:
         if u.status == INFLIGHT:
             u.work.wait()
             u.work = None
+            u.post_gather = None
+        elif self.hpz > 1 and not self.in_backward and u.expert_key is None and u.full is not None:
+            # hpZ: keep this rank's slice of the gathered unit for the backward re-gather
+            n = u.padded // self.hpz
+            u.sec = u.full[self.hpz_rank * n:(self.hpz_rank + 1) * n].clone()
+        if self.in_backward:
+            u.sec = None
         u.unbind_params(_empty(self.dtype, self.device))
         u.full = None
         u.status = NOT_AVAILABLE
@@ -566,6 +664,22 @@ class ZeroOptimizer:
         dst = self.store.grad_slice(u)
         first = self.micro_in_window == 0 or self.stage == 1
         src = u.grad_full if u.grad_full.dtype == self.comm_dtype else u.grad_full.to(self.comm_dtype)
+        replica = self.replica_group if (self.mics and u.expert_key is None) else None
+        if self.qgz and u.world > 1 and replica is None:
+            w, post, keep = self._qgz_reduce(u, src, dst, first)
+            self._after_reduce(u, src, w, post, keep)
+            return
+        if replica is not None:
+            # MiCS: reduce-scatter inside the shard group, then all-reduce the shard across replicas
+            tmp = torch.empty(u.shard, dtype=self.comm_dtype, device=self.device)
+            w = dist.reduce_scatter_tensor(tmp, src, group=u.rs_group, async_op=True)
+
+            def post(d=dst, t=tmp, f=first):
+                dist.all_reduce(t, group=replica)
+                d.copy_(t) if f else d.add_(t)
+
+            self._after_reduce(u, src, w, post, (src, tmp))
+            return
         if first and dst.dtype == self.comm_dtype:
             w = dist.reduce_scatter_tensor(dst, src, group=u.rs_group, async_op=True)
             post = None
@@ -576,14 +690,32 @@ class ZeroOptimizer:
                 post = (lambda d=dst, t=tmp: d.copy_(t))
             else:
                 post = (lambda d=dst, t=tmp: d.add_(t))
-        keep = (src, )
+        self._after_reduce(u, src, w, post, (src, ))
+
+    def _after_reduce(self, u, src, w, post, keep):
         if self.stage == 3 and not u.persistent and u.world > 1:
             gf = u.grad_full
             u.unbind_grads()
             u.grad_full = None
-            keep = (src, gf, u.full)
+            keep = tuple(keep) + (gf, u.full)
             self._release(u)
         self.pending_works.append((w, post, keep))
+
+    def _qgz_reduce(self, u, src, dst, first):
+        """qgZ: quantize the unit gradient per destination shard, one all-to-all (int8/int4 + scales), then
+        dequantize-and-sum the ``world`` received chunks straight into the fp32/bf16 gradient shard."""
+        from ...ops import quantizer as Q
+        G = self._qgroup(u.shard)
+        q, sc, _ = Q.quantize(src, G, self.qgz_bits, True)
+        qr, sr = torch.empty_like(q), torch.empty_like(sc)
+        w = dist.all_to_all_single(qr, q, group=u.rs_group, async_op=True)
+        w2 = dist.all_to_all_single(sr, sc, group=u.rs_group, async_op=True)
+
+        def post():
+            w2.wait()
+            Q.dequant_reduce(qr, sr, u.world, u.shard, G, self.qgz_bits, out=dst, accumulate=not first)
+
+        return w, post, (src, q, sc, qr, sr)
 
     def prepare_backward(self, boundary):
         self.boundary = boundary
@@ -711,9 +843,9 @@ class ZeroOptimizer:
             if self._rep_ranges:
                 fused.grad_sumsq([self.store.grad[a:b] for a, b in self._rep_ranges], out=self._rep_buf)
         if self.dp_world > 1 and self.stage > 0:
-            dist.all_reduce(self._norm_buf, group=self.dp_group)
+            dist.all_reduce(self._norm_buf, group=self.norm_group)
             if self.mp_group is not None:
-                dist.all_reduce(self._rep_buf, group=self.dp_group)
+                dist.all_reduce(self._rep_buf, group=self.norm_group)
         if self.loss_scaler.dynamic and self.dp_world > 1:
             dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.dp_group)
         if self.stage == 0 and self.expert_units:

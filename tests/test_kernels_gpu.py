@@ -375,3 +375,47 @@ def test_mixtral_tiny_train_step_gpu():
         opt.zero_grad()
         losses.append(float(loss))
     assert all(math.isfinite(v) for v in losses) and losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("bits,sym", [(8, True), (8, False), (4, True), (4, False)])
+def test_quant_int_matches_reference(bits, sym):
+    from hcache_deepspeed_amd.ops import quantizer as Q
+    x = torch.randn(64 * 2048, device="cuda", dtype=torch.bfloat16)
+    q, s, m = Q.quantize(x, 2048, bits, sym)
+    qr, sr, mr = Q._ref_quant_int(x.cpu(), 2048, bits, sym)
+    assert torch.allclose(s.cpu(), sr, rtol=1e-6)
+    # rounding ties may differ in the last unit on a handful of elements
+    y = Q.dequantize(q, s, m, 2048, bits, sym, torch.float32)
+    yr = Q._ref_dequant_int(qr, sr, mr, 2048, bits, sym, torch.float32)
+    assert (y.cpu() - yr).abs().max() <= s.max().item() * 1.01
+    assert (y.cpu() - x.float().cpu()).abs().max() <= s.max().item() * 0.51
+
+
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
+def test_quant_fp8_matches_torch_ocp(fmt):
+    from hcache_deepspeed_amd.ops import quantizer as Q
+    x = torch.randn(32 * 512, device="cuda", dtype=torch.float32) * 3
+    q, s = Q.quantize_fp8(x, 512, fmt)
+    qr, sr = Q.quantize_fp8(x.cpu(), 512, fmt)
+    assert torch.allclose(s.cpu(), sr)
+    # gfx950 converts to the OCP formats: bit-exact with torch's float8 casts (RNE)
+    mism = (q.cpu() != qr).float().mean().item()
+    assert mism < 1e-3, mism
+    y = Q.dequantize_fp8(q, s, 512, fmt, torch.float32)
+    assert torch.allclose(y.cpu(), Q.dequantize_fp8(qr, sr, 512, fmt, torch.float32), rtol=0.07, atol=1e-6)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+def test_dequant_reduce(bits):
+    from hcache_deepspeed_amd.ops import quantizer as Q
+    W, n = 4, 8192
+    xs = [torch.randn(n, device="cuda", dtype=torch.bfloat16) for _ in range(W)]
+    qs = [Q.quantize(x, 512, bits, True) for x in xs]
+    q = torch.cat([a[0] for a in qs])
+    s = torch.cat([a[1] for a in qs])
+    out = Q.dequant_reduce(q, s, W, n, 512, bits)
+    ref = Q.dequant_reduce(q.cpu(), s.cpu(), W, n, 512, bits)
+    assert torch.allclose(out.cpu(), ref, atol=1e-5, rtol=1e-5)
+    acc = torch.ones(n, device="cuda")
+    Q.dequant_reduce(q, s, W, n, 512, bits, out=acc, accumulate=True)
+    assert torch.allclose(acc.cpu(), ref + 1, atol=1e-5, rtol=1e-5)
