@@ -173,6 +173,19 @@ class _FlashAttnFn(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None, None
 
 
+def _count_attn_flops(T, H, D, seq_len, causal, cu_seqlens):
+    """Report QK^T + PV flops to a running FlopsProfiler (the HIP kernel is invisible to aten dispatch)."""
+    from ..profiling import counters
+    if not counters.active():
+        return
+    if cu_seqlens is not None:
+        lens = (cu_seqlens[1:] - cu_seqlens[:-1]).tolist()
+    else:
+        lens = [seq_len] * (T // max(1, seq_len))
+    pairs = sum(L * (L + 1) / 2 if causal else L * L for L in lens)
+    counters.add(4 * pairs * H * D, 2 * pairs * H * D, "flash_attn")
+
+
 def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window=0, return_lse=False):
     """q: [B, S, Hq, D] or [T, Hq, D] (+cu_seqlens); k/v: [.., Hkv, D]. Returns o like q (and lse [Hq, T])."""
     batched = q.dim() == 4
@@ -186,6 +199,7 @@ def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window
     for t, n in ((q3, "q"), (k3, "k"), (v3, "v")):
         _check_tok_layout(t, n)
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    _count_attn_flops(q3.shape[0], q3.shape[1], q3.shape[2], seq_len, causal, cu_seqlens)
     o, lse = _FlashAttnFn.apply(q3, k3, v3, bool(causal), float(scale), cu_seqlens, int(seq_len), int(window or 0),
                                 return_lse)
     if batched:
@@ -249,5 +263,6 @@ def qkv_attention(qkv, n_q, n_kv, cos=None, sin=None, seq_len=None, causal=True,
     assert NH == n_q + 2 * n_kv
     qkv = qkv if qkv.is_contiguous() else qkv.contiguous()
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    _count_attn_flops(T, n_q, D, int(seq_len or T), causal, cu_seqlens)
     return _QKVAttnFn.apply(qkv, n_q, n_kv, cos, sin, int(seq_len or T), bool(causal), float(scale), cu_seqlens,
                             pos_ids, int(window or 0))

@@ -94,3 +94,61 @@ def _gathered_params(rank, world):
 
 def test_gathered_parameters_modifier():
     run_distributed(_gathered_params, 2)
+
+
+def test_offload_reload_states_roundtrip():
+    """engine.offload_states()/reload_states() (reference tests/unit/runtime/zero/test_offload_states.py):
+    training continues bit-identically after a full offload/reload cycle."""
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+
+    def run(cycle):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(**TINY))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
+               "zero_optimization": {"stage": 3}}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        g = torch.Generator().manual_seed(1)
+        out = []
+        for i in range(4):
+            x = torch.randint(0, 97, (2, 12), generator=g)
+            loss = eng(x, labels=x)
+            eng.backward(loss)
+            eng.step()
+            out.append(float(loss))
+            if cycle and i == 1:
+                eng.offload_states()
+                assert eng.optimizer.store.master.numel() == 0 and eng.optimizer.store.lp.numel() == 0
+                eng.reload_states()
+        return out
+
+    import os
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=os.environ.get("MASTER_PORT", "29611"))
+    assert run(True) == run(False)
+
+
+def test_flops_profiler_counts_gemms_and_attention():
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.profiling.flops_profiler import FlopsProfiler, get_model_profile
+    torch.manual_seed(0)
+    cfg = tiny(**TINY)
+    m = LlamaForCausalLM(cfg)
+    x = torch.randint(0, 97, (2, 12))
+    prof = FlopsProfiler(m)
+    prof.start_profile()
+    with torch.no_grad():
+        m(x)
+    flops = prof.get_total_flops()
+    prof.stop_profile()
+    T, H, L = 24, cfg.hidden_size, cfg.num_hidden_layers
+    per_layer_gemm = 2 * T * H * ((cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * cfg.head_dim +
+                                  cfg.num_attention_heads * cfg.head_dim + 3 * cfg.intermediate_size)
+    lm_head = 2 * T * H * cfg.vocab_size
+    assert flops >= L * per_layer_gemm + lm_head
+    assert m.model.layers[0].__flops__ >= per_layer_gemm
+    assert prof.get_total_params() == sum(p.numel() for p in m.parameters())
+    prof.print_model_profile(module_depth=2)
+    prof.end_profile()
+    f, macs, params = get_model_profile(m, args=[x], print_profile=False, as_string=False)
+    assert f == flops
