@@ -215,7 +215,10 @@ class DeepSpeedEngine(nn.Module):
         self.basic_optimizer = basic
         stage = cfg.zero_optimization_stage
         zc = cfg.zero_config
-        if zc.offload_optimizer.enabled or zc.offload_param.enabled:
+        from .fp16.onebit import OnebitZeroOptimizer, _OnebitBase
+        if isinstance(basic, _OnebitBase):
+            cls = OnebitZeroOptimizer
+        elif zc.offload_optimizer.enabled or zc.offload_param.enabled:
             from .zero.offload import OffloadZeroOptimizer
             cls = OffloadZeroOptimizer
         else:

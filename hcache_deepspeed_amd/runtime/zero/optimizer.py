@@ -46,6 +46,8 @@ def _empty(dtype, device):
 
 
 def _optimizer_kind(opt):
+    if getattr(opt, "kind", "") in ("onebit_adam", "zero_one_adam", "onebit_lamb"):
+        return "adam", True  # warm-up runs the fused AdamW; the compressed phase is OnebitZeroOptimizer's
     name = type(opt).__name__.lower()
     if name in ("fusedadam", "adam", "adamw", "deepspeedcpuadam", "cpuadam", "hybridadam"):
         adamw = True
