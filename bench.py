@@ -29,20 +29,26 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seq", type=int, default=4096)
-    ap.add_argument("--micro-batch", type=int, default=4)
+    ap.add_argument("--micro-batch", type=int, default=6)
     ap.add_argument("--gas", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--zero", type=int, default=3)
     ap.add_argument("--layers", type=int, default=0, help="debug only: override layer count (result is marked invalid)")
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
+    ap.add_argument("--host-act-cache", action="store_true",
+                    help="HCache host activation cache (saved activations spill to pinned host memory)")
+    ap.add_argument("--offload", choices=["none", "cpu", "nvme"], default="none",
+                    help="ZeRO-Offload/Infinity of optimizer states (+ params with --offload-param)")
+    ap.add_argument("--offload-param", action="store_true")
+    ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as tdist
 
     import hcache_deepspeed_amd as hds
-    from hcache_deepspeed_amd.models import llama
+    from hcache_deepspeed_amd.models import gpt2, llama, mixtral
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or "RANK" in os.environ:
@@ -55,9 +61,22 @@ def main():
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
 
     overrides = {}
-    if args.layers:
-        overrides["num_hidden_layers"] = args.layers
-    cfg_model = llama.PRESETS[args.model](**overrides)
+    if args.model.startswith("gpt2"):
+        if args.layers:
+            overrides["n_layer"] = args.layers
+        cfg_model = {"gpt2-small": gpt2.gpt2_small, "gpt2-medium": gpt2.gpt2_medium}[args.model](**overrides)
+        build = gpt2.GPT2LMHeadModel
+    elif args.model in ("mixtral-8x7b", "tiny-moe"):
+        if args.layers:
+            overrides["num_hidden_layers"] = args.layers
+        cfg_model = {"mixtral-8x7b": mixtral.mixtral_8x7b, "tiny-moe": mixtral.tiny_moe}[args.model](
+            ep_size=args.ep, **overrides)
+        build = mixtral.MixtralForCausalLM
+    else:
+        if args.layers:
+            overrides["num_hidden_layers"] = args.layers
+        cfg_model = llama.PRESETS[args.model](**overrides)
+        build = llama.LlamaForCausalLM
     ds_config = {
         "train_micro_batch_size_per_gpu": args.micro_batch,
         "gradient_accumulation_steps": args.gas,
@@ -66,12 +85,16 @@ def main():
                                                    "weight_decay": 0.1}},
         "gradient_clipping": 1.0,
         "zero_optimization": {"stage": args.zero},
-        "mi355x": {"zero3_prefetch_depth": args.prefetch},
+        "mi355x": {"zero3_prefetch_depth": args.prefetch, "host_act_cache": {"enabled": bool(args.host_act_cache)}},
         "steps_per_print": 1000000,
     }
+    if args.offload != "none":
+        ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True}
+        if args.offload_param:
+            ds_config["zero_optimization"]["offload_param"] = {"device": args.offload, "pin_memory": True}
     t_init = time.time()
     with hds.zero.Init(enabled=args.zero == 3):
-        model = llama.LlamaForCausalLM(cfg_model)
+        model = build(cfg_model)
     if args.ckpt:
         model.gradient_checkpointing_enable()
     engine, _, _, _ = hds.initialize(model=model, config=ds_config)
@@ -110,7 +133,8 @@ def main():
     tokens = world * mb * args.gas * S * args.steps
     value = tokens / dt
     ms_per_step = dt / args.steps * 1e3
-    flops = cfg_model.flops_per_token(S) * tokens
+    flops = (cfg_model.flops_per_token(S) if hasattr(cfg_model, "flops_per_token") else
+             6 * cfg_model.active_params() + 12 * cfg_model.num_hidden_layers * S * cfg_model.hidden_size) * tokens
     mfu = flops / dt / (2.5e15 * world)
     mem = torch.cuda.max_memory_allocated(dev) / 2**30
     if rank == 0:
@@ -129,6 +153,7 @@ def main():
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": "Llama-3-8B" if args.model == "llama3-8b" and not args.layers else
                        f"{args.model}{'-L' + str(args.layers) if args.layers else ''}",
+                       "host_act_cache": bool(args.host_act_cache), "offload": args.offload,
                        "global_batch": world * mb * args.gas, "seq_len": S,
                        "parallelism": f"zero{args.zero}-dp{world}", "micro_batch_per_gpu": mb, "gas": args.gas,
                        "activation_checkpointing": bool(args.ckpt)},

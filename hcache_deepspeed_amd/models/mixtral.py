@@ -36,6 +36,11 @@ class MixtralConfig(LlamaConfig):
             n += V * H * 2
         return n
 
+    def flops_per_token(self, seq_len):
+        """Training FLOPs/token with only the top-k experts counted (+ router)."""
+        return 6 * (self.active_params() + self.num_hidden_layers * self.hidden_size * self.num_local_experts) + \
+            6 * self.vocab_size * self.hidden_size + 12 * self.num_hidden_layers * self.hidden_size * seq_len
+
     def active_params(self):
         H, I, L = self.hidden_size, self.intermediate_size, self.num_hidden_layers
         D, Hq, Hkv, k = self.head_dim, self.num_attention_heads, self.num_key_value_heads, self.num_experts_per_tok

@@ -90,7 +90,7 @@ def save_checkpoint(engine, save_dir, tag=None, client_state=None, save_latest=T
     zopt = engine.optimizer
     stage = engine.zero_optimization_stage()
     module_sd = None
-    if stage < 3 or (zopt is not None and zopt.layout_world == 1):
+    if stage < 3 or (zopt is not None and not zopt.partitioned):
         module_sd = _to_cpu(engine.module.state_dict())
     param_shapes = {n: list(p.ds_shape if hasattr(p, "ds_shape") else p.shape)
                     for n, p in engine.module.named_parameters()}
@@ -115,7 +115,7 @@ def save_checkpoint(engine, save_dir, tag=None, client_state=None, save_latest=T
         ds_version=__version__,
     )
     state.update(client_state or {})
-    write_model = (stage == 3 and zopt is not None and zopt.layout_world > 1) or dp_rank == 0
+    write_model = (stage == 3 and zopt is not None and zopt.partitioned) or dp_rank == 0
     if write_model:
         _write(state, _ckpt_name(engine, save_dir, tag), async_save)
     if zopt is not None:

@@ -404,7 +404,7 @@ class DeepSpeedEngine(nn.Module):
         return save_16bit_model(self, save_dir, save_filename)
 
     def module_state_dict(self, destination=None, prefix="", keep_vars=False, exclude_frozen_parameters=False):
-        if self.zero_optimization_stage() == 3 and self.optimizer.layout_world > 1:
+        if self.zero_optimization_stage() == 3 and self.optimizer.partitioned:
             return None
         return self.module.state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)
 

@@ -66,7 +66,7 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
         if self._training_start_time is not None:
             self._training_latency += t0 - self._training_start_time
         zopt = self.optimizer
-        gathered = zopt is not None and getattr(zopt, "stage", 0) == 3 and getattr(zopt, "layout_world", 1) > 1
+        gathered = zopt is not None and getattr(zopt, "stage", 0) == 3 and getattr(zopt, "partitioned", False)
         was_training = self.module.training
         self.module.eval()
         self._in_generate = True

@@ -125,14 +125,19 @@ class FlatUnit:
 class ShardStore:
     """Concatenation of this rank's shards of every unit: lp (compute dtype), fp32 master, grads, states."""
 
-    def __init__(self, units, dtype, device, grad_dtype, master=True):
+    def __init__(self, units, dtype, device, grad_dtype, master=True, lp_host=False):
         total = 0
         for u in units:
             u.store_off = total
             total += u.shard
         self.numel = total
         self.device = device
-        self.lp = torch.zeros(total, dtype=dtype, device=device)
+        if lp_host:
+            # ZeRO-Infinity parameter offload: the compute-dtype shard lives in pinned host memory
+            pin = torch.cuda.is_available()
+            self.lp = torch.zeros(total, dtype=dtype, device="cpu", pin_memory=pin)
+        else:
+            self.lp = torch.zeros(total, dtype=dtype, device=device)
         self.grad = torch.zeros(total, dtype=grad_dtype, device=device)
         self.master = None
         self.states = {}

@@ -34,12 +34,21 @@ def _host_empty(numel, dtype, pin):
 
 class OffloadZeroOptimizer(ZeroOptimizer):
 
+    _STATE_KEYS = {"adam": ("exp_avg", "exp_avg_sq"), "lion": ("exp_avg", ), "adagrad": ("sum", )}
+
     def __init__(self, *args, **kwargs):
+        config = args[2] if len(args) > 2 else kwargs["config"]
+        oc0 = config.zero_config.offload_optimizer
+        # full offload: never allocate device-side optimizer states (70B-class models)
+        self._defer_states = (not oc0.enabled) or float(oc0.ratio) >= 1.0
         super().__init__(*args, **kwargs)
         if self.kind == "generic":  # host path implements Adam/Lion/Adagrad; other torch optimizers -> AdamW
             self.kind, self.adamw = "adam", True
-            self.store.states = {"exp_avg": torch.zeros_like(self.store.master),
-                                 "exp_avg_sq": torch.zeros_like(self.store.master)}
+            if not self._defer_states:
+                self.store.states = {"exp_avg": torch.zeros_like(self.store.master),
+                                     "exp_avg_sq": torch.zeros_like(self.store.master)}
+        if self._defer_states:
+            self.store.states = {k: None for k in self._STATE_KEYS[self.kind]}
         oc = self.zcfg.offload_optimizer
         self.offload_device = oc.device if oc.enabled else "cpu"
         self.ratio = float(oc.ratio if oc.enabled else 1.0)
@@ -47,10 +56,14 @@ class OffloadZeroOptimizer(ZeroOptimizer):
         s = self.store
         n = s.numel
         self.n_off = int(n * self.ratio) // 64 * 64 if self.ratio < 1.0 else n
+        self.lp_on_host = s.lp.device.type == "cpu" and self.device.type == "cuda"
+        assert not (self.lp_on_host and self.n_off < n), "offload_param requires offload_optimizer.ratio == 1"
         self.sub = max(1 << 20, min(int(self.zcfg.sub_group_size), self.n_off or 1))
         # host copies of the offloaded range
         self.h_master = _host_empty(self.n_off, torch.float32, False)
         self.h_master.copy_(s.master[:self.n_off].cpu())
+        if self.n_off == n:
+            s.master = None  # free before the host state buffers are allocated
         self.h_states = {k: torch.zeros(self.n_off, dtype=torch.float32) for k in s.states}
         # double-buffered pinned staging: grads D2H (chunk k+1) / bf16 params H2D (chunk k-1)
         self.h_grad = [_host_empty(self.sub, s.grad.dtype, self.pin) for _ in range(2)]
@@ -158,7 +171,8 @@ class OffloadZeroOptimizer(ZeroOptimizer):
             hg = self.h_grad[b][:n]
             g = self.param_groups[gi]
             p32 = self.h_master[lo:hi]
-            out = self.h_lp[b][:n]
+            # parameters offloaded too: the CPU optimizer writes bf16 straight into the pinned lp shard
+            out = s.lp[lo:hi] if self.lp_on_host else self.h_lp[b][:n]
             if self.kind in ("adam", "generic"):
                 m = self._state_chunk("exp_avg", lo, hi, cache)
                 v = self._state_chunk("exp_avg_sq", lo, hi, cache)
@@ -179,6 +193,8 @@ class OffloadZeroOptimizer(ZeroOptimizer):
                                  bf16_out=out if self.dtype == torch.bfloat16 else None, grad_scale=coef)
             if self.dtype != torch.bfloat16:
                 out.copy_(p32)
+            if self.lp_on_host:
+                continue
             if gpu:
                 with torch.cuda.stream(self.h2d_stream):
                     s.lp[lo:hi].copy_(out, non_blocking=True)

@@ -63,6 +63,23 @@ def _optimizer_kind(opt):
     return "generic", False
 
 
+class _DoneWork:
+
+    def wait(self):
+        return True
+
+
+class _EventWork:
+    """Work handle for a side-stream copy: wait() orders the current stream after it."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+
 class _PreBackward(torch.autograd.Function):
     """Identity on a unit's outputs whose backward fires right before that unit's backward."""
 
@@ -153,6 +170,12 @@ class ZeroOptimizer:
             self.ag_group = dist.new_group(ranks=dp_ranks)
             self.rs_group = dist.new_group(ranks=dp_ranks)
 
+        op = self.zcfg.offload_param
+        self.offload_param = bool(op.enabled) and self.stage == 3
+        if self.offload_param and self.device.type == "cuda":
+            self.param_h2d_stream = torch.cuda.Stream(self.device)
+        else:
+            self.param_h2d_stream = None
         self._build_units(leaf_modules)
         self._build_store()
         self._install_hooks()
@@ -374,7 +397,7 @@ class ZeroOptimizer:
 
     def _build_store(self):
         dev = self.device
-        self.store = ShardStore(self.units, self.dtype, dev, self.grad_acc_dtype)
+        self.store = ShardStore(self.units, self.dtype, dev, self.grad_acc_dtype, lp_host=self.offload_param)
         self.direct_grads = all(u.direct for u in self.units)
         from .partition_parameters import materialize_unit
         with torch.no_grad():
@@ -386,7 +409,11 @@ class ZeroOptimizer:
                 if repl:
                     self._swap_params(u, repl)
                 lp = self.store.lp_slice(u)
-                if u.world == 1:
+                if self.offload_param:
+                    full = torch.empty(u.padded, dtype=self.dtype, device=dev)
+                    u.copy_params_into(full)
+                    lp.copy_(full[u.rank * u.shard:(u.rank + 1) * u.shard])  # D2H into pinned host shard
+                elif u.world == 1:
                     full = lp  # alias: parameters live in the optimizer's lp shard
                     u.copy_params_into(full)
                 else:
@@ -396,7 +423,7 @@ class ZeroOptimizer:
                 u.shard_tensor = lp
                 for p in u.params:
                     p.ds_tensor = lp
-                if u.persistent or u.world == 1:
+                if u.persistent or (u.world == 1 and not self.offload_param):
                     u.full = full
                     u.bind_params(full)
                     u.status = AVAILABLE
@@ -410,9 +437,11 @@ class ZeroOptimizer:
                         u.grad_full = self.store.grad_slice(u)
                     else:
                         u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=dev)
-                    u.bind_grads(u.grad_full)
+                    if u.status == AVAILABLE:
+                        u.bind_grads(u.grad_full)
             self.store.master = self.store.lp.float()
-            self._init_states()
+            if not getattr(self, "_defer_states", False):
+                self._init_states()
         for p in (p for u in self.units for p in u.params):
             p.ds_status = self.param_to_unit[id(p)][0].status
             p._hds_zero = self
@@ -509,7 +538,7 @@ class ZeroOptimizer:
             grad_on = torch.is_grad_enabled()
             if grad_on and not self.in_backward:
                 output = self._wrap_outputs(u, output)
-            if u.world > 1 and not self.in_backward and not self._is_last_in_trace(u):
+            if self._partitioned(u) and not self.in_backward and not self._is_last_in_trace(u):
                 self._release(u)
             return output
 
@@ -547,11 +576,44 @@ class ZeroOptimizer:
     # ------------------------------------------------------------------------------------
     # gather / release (ZeRO-3)
     # ------------------------------------------------------------------------------------
+    def _partitioned(self, u):
+        """True when the unit's full parameters are materialised on demand (not aliased / persistent)."""
+        return u.world > 1 or self.offload_param
+
+    @property
+    def partitioned(self):
+        return self.layout_world > 1 or self.offload_param
+
+    def _h2d_gather(self, u, full):
+        """ZeRO-Infinity fetch: pinned host shard -> device (side stream), then all-gather when sharded."""
+        s = self.param_h2d_stream
+        if s is None:  # CPU runs: synchronous copies, same semantics
+            if u.world == 1:
+                full.copy_(u.shard_tensor)
+                return _DoneWork()
+            tmp = u.shard_tensor.to(self.device)
+            return dist.all_gather_into_tensor(full, tmp, group=u.ag_group, async_op=True)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            if u.world == 1:
+                full.copy_(u.shard_tensor, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s)
+                work = _EventWork(ev)
+            else:
+                tmp = torch.empty(u.shard, dtype=self.dtype, device=self.device)
+                tmp.copy_(u.shard_tensor, non_blocking=True)
+                work = dist.all_gather_into_tensor(full, tmp, group=u.ag_group, async_op=True)
+        full.record_stream(s)
+        return work
+
     def _gather(self, u, wait=True):
         if u.status == NOT_AVAILABLE:
             full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
             u.post_gather = None
-            if self.in_backward and getattr(u, "sec", None) is not None:
+            if self.offload_param:
+                u.work = self._h2d_gather(u, full)
+            elif self.in_backward and getattr(u, "sec", None) is not None:
                 # hpZ: backward re-gather from the secondary (intra-group) partition
                 u.work = dist.all_gather_into_tensor(full, u.sec, group=self.hpz_group, async_op=True)
             elif self.qwz and u.expert_key is None:
@@ -571,9 +633,11 @@ class ZeroOptimizer:
         if self.in_backward and u.grad_full is None and u.requires_grad_count:
             u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=self.device)
             u.bind_grads(u.grad_full)
+        elif self.in_backward and u.direct and self.offload_param and u.requires_grad_count:
+            u.bind_grads(u.grad_full)  # offloaded unit: grads land straight in the device grad shard
 
     def _release(self, u):
-        if u.persistent or u.world == 1 or u.status == NOT_AVAILABLE:
+        if u.persistent or not self._partitioned(u) or u.status == NOT_AVAILABLE:
             return
         if u.status == INFLIGHT:
             u.work.wait()
@@ -590,7 +654,7 @@ class ZeroOptimizer:
         u.status = NOT_AVAILABLE
 
     def _record_and_prefetch(self, u):
-        if self.in_backward or self.layout_world == 1:
+        if self.in_backward or not self.partitioned:
             return
         if self._recording:
             self._fwd_trace.append(u.uid)
@@ -608,7 +672,7 @@ class ZeroOptimizer:
 
     def _pre_backward(self, u):
         self._gather(u, wait=True)
-        if self.layout_world > 1 and self._fwd_trace and not self._recording:
+        if self.partitioned and self._fwd_trace and not self._recording:
             t = self._fwd_trace
             try:
                 i = len(t) - 1 - t[::-1].index(u.uid)
@@ -662,7 +726,12 @@ class ZeroOptimizer:
         if self.stage == 1 and not self.boundary:
             return
         if u.direct:
-            return  # grads already accumulated in place inside the optimizer shard
+            # grads already accumulated in place inside the optimizer shard; an offloaded (ZeRO-Infinity)
+            # unit's device copy is dropped as soon as its backward is complete
+            if self.stage == 3 and not u.persistent and self._partitioned(u):
+                u.unbind_grads()
+                self._release(u)
+            return
         dst = self.store.grad_slice(u)
         first = self.micro_in_window == 0 or self.stage == 1
         src = u.grad_full if u.grad_full.dtype == self.comm_dtype else u.grad_full.to(self.comm_dtype)
@@ -725,7 +794,7 @@ class ZeroOptimizer:
         for u in self.units:
             u.pending = u.requires_grad_count
             u.grads_reduced = False
-            if u.grad_full is not None and (u.direct or self.stage in (1, 2, 0)):
+            if u.grad_full is not None and (u.direct or self.stage in (1, 2, 0)) and u.status == AVAILABLE:
                 u.bind_grads(u.grad_full)
 
     def finish_backward(self):
@@ -873,6 +942,13 @@ class ZeroOptimizer:
         """ZeRO-1/2: rebuild the persistent full parameters from the updated shards."""
         works = []
         for u in self.units:
+            if self.offload_param and u.persistent and u.full is not None:
+                if u.world == 1:
+                    u.full.copy_(u.shard_tensor)
+                else:
+                    works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor.to(self.device), group=u.ag_group,
+                                                             async_op=True))
+                continue
             if u.world == 1 or (self.stage == 3 and not u.persistent):
                 continue  # aliased / re-gathered on demand by the next forward
             if u.full is None:
@@ -954,7 +1030,7 @@ class ZeroOptimizer:
     def refresh_fp32_from_lp(self):
         with torch.no_grad():
             for u in self.units:
-                if u.full is not None and u.world > 1 and u.status == AVAILABLE:
+                if u.full is not None and self._partitioned(u) and u.status == AVAILABLE:
                     self.store.lp_slice(u).copy_(u.full[u.rank * u.shard:(u.rank + 1) * u.shard])
             self.store.master.copy_(self.store.lp)
 

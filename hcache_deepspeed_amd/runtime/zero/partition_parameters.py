@@ -144,7 +144,7 @@ class GatheredParameters:
                     if u.full.data_ptr() != lp.data_ptr():
                         lp.copy_(u.full[u.rank * u.shard:(u.rank + 1) * u.shard])
                     z.store.master[u.store_off:u.store_off + u.shard].copy_(lp)
-                if not u.persistent and u.world > 1 and not z.in_backward:
+                if not u.persistent and z._partitioned(u) and not z.in_backward:
                     z._release(u)
         self.units = []
         return False

@@ -70,7 +70,7 @@ def test_aio_roundtrip(tmp_path):
     assert torch.equal(x, a) and torch.equal(y, b)
 
 
-def _offload_vs_device(rank, world, stage, device, ratio, d):
+def _offload_vs_device(rank, world, stage, device, ratio, d, param=False):
     import hcache_deepspeed_amd as ds
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
     res = {}
@@ -81,6 +81,8 @@ def _offload_vs_device(rank, world, stage, device, ratio, d):
         if mode == "offload":
             z["offload_optimizer"] = {"device": device, "nvme_path": os.path.join(d, f"nvme{rank}"), "ratio": ratio}
             z["sub_group_size"] = 20000
+            if param:
+                z["offload_param"] = {"device": "cpu", "pin_memory": True}
         cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
                "zero_optimization": z, "gradient_clipping": 1.0}
         eng, _, _, _ = ds.initialize(model=m, config=cfg)
@@ -90,6 +92,9 @@ def _offload_vs_device(rank, world, stage, device, ratio, d):
             loss = eng(x, labels=x)
             eng.backward(loss)
             eng.step()
+        if param and mode == "offload":
+            assert eng.optimizer.offload_param and eng.optimizer.store.lp.device.type == "cpu"
+            assert eng.optimizer.partitioned
         res[mode] = eng.optimizer.full_fp32_state_dict(eng._param_names)
     for k in res["device"]:
         assert torch.allclose(res["device"][k], res["offload"][k], atol=1e-5), k
@@ -99,3 +104,9 @@ def _offload_vs_device(rank, world, stage, device, ratio, d):
                                                 (2, "cpu", 0.5)])
 def test_zero_offload_matches_device(stage, device, ratio, tmp_path):
     run_distributed(_offload_vs_device, 2, stage, device, ratio, str(tmp_path))
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_zero_infinity_param_offload_matches_device(world, tmp_path):
+    """ZeRO-Infinity: offload_param + offload_optimizer (cpu) reproduce the on-device ZeRO-3 trajectory."""
+    run_distributed(_offload_vs_device, world, 3, "cpu", 1.0, str(tmp_path), True)
