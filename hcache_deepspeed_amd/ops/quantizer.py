@@ -92,7 +92,19 @@ def dequantize(q, scales, mins=None, group_size=512, bits=8, symmetric=True, dty
 
 
 def fake_quantize(x, group_size=512, bits=8, symmetric=True):
-    """Quantize-dequantize (QAT / MoQ), same dtype and shape as ``x``."""
+    """Quantize-dequantize (QAT / MoQ), same dtype and shape as ``x``. 4/8-bit use the packed HIP kernels; other
+    widths (MoQ walks 16 -> target bits one at a time) use the same group math in torch."""
+    if bits not in (4, 8):
+        g = x.float().reshape(-1, group_size)
+        if symmetric:
+            qmax = 2**(bits - 1) - 1
+            sc = (g.abs().amax(1, keepdim=True) / qmax).clamp_min(1e-12)
+            y = torch.clamp(torch.round(g / sc), -qmax - 1, qmax) * sc
+        else:
+            lo, hi = g.amin(1, keepdim=True), g.amax(1, keepdim=True)
+            sc = ((hi - lo) / (2**bits - 1)).clamp_min(1e-12)
+            y = torch.clamp(torch.round((g - lo) / sc), 0, 2**bits - 1) * sc + lo
+        return y.reshape(x.shape).to(x.dtype)
     q, s, m = quantize(x, group_size, bits, symmetric)
     return dequantize(q, s, m, group_size, bits, symmetric, x.dtype).view_as(x)
 

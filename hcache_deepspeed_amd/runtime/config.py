@@ -277,6 +277,9 @@ class DeepSpeedConfig:
         self.aio_config = c.get("aio") or {}
         self.hybrid_engine = c.get("hybrid_engine") or {}
         self.curriculum_learning = c.get("curriculum_learning") or {}
+        self.pld_config = c.get("progressive_layer_drop") or {}
+        self.eigenvalue_config = c.get("eigenvalue") or {}
+        self.quantize_training = c.get("quantize_training") or {}
         self.data_efficiency = c.get("data_efficiency") or {}
         self.compression_training = c.get("compression_training") or {}
 

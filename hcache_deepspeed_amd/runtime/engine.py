@@ -51,6 +51,22 @@ def _dtype_of(cfg):
     return torch.float32
 
 
+def _truncate_seqlen(inputs, kwargs, d):
+    """Sequence-length curriculum: cut every [B, S, ...] tensor argument to [B, d, ...]."""
+    S = None
+    for t in list(inputs) + list(kwargs.values()):
+        if isinstance(t, torch.Tensor) and t.dim() >= 2:
+            S = t.shape[1]
+            break
+    if S is None or d >= S:
+        return inputs, kwargs
+
+    def cut(t):
+        return t[:, :d].contiguous() if isinstance(t, torch.Tensor) and t.dim() >= 2 and t.shape[1] == S else t
+
+    return tuple(cut(t) for t in inputs), {k: cut(v) for k, v in kwargs.items()}
+
+
 class DeepSpeedEngine(nn.Module):
 
     def __init__(self, args=None, model=None, optimizer=None, model_parameters=None, training_data=None,
@@ -132,6 +148,18 @@ class DeepSpeedEngine(nn.Module):
             from ..profiling.flops_profiler import FlopsProfiler
             self.flops_profiler = FlopsProfiler(self.module, ds_engine=self)
 
+        # data efficiency / training-dynamics features (reference engine.py:303-330, 1985-2000)
+        self.curriculum_scheduler = None
+        cl = cfg.curriculum_learning
+        if cl.get("enabled", False):
+            from .data_pipeline.curriculum_scheduler import CurriculumScheduler
+            self.curriculum_scheduler = CurriculumScheduler(cl)
+            self.curriculum_type = cl.get("curriculum_type", "seqlen")
+        self.progressive_layer_drop = None
+        if cfg.pld_config.get("enabled", False):
+            from .progressive_layer_drop import ProgressiveLayerDrop
+            self.progressive_layer_drop = ProgressiveLayerDrop(cfg.pld_config.get("theta", 0.5),
+                                                               cfg.pld_config.get("gamma", 0.001))
         self._activation_cache = None
         if cfg.mi355x.host_act_cache.enabled:
             from ..offload.activation_cache import HostActivationCache
@@ -314,6 +342,14 @@ class DeepSpeedEngine(nn.Module):
                 "profile_step", 1):
             self.flops_profiler.start_profile()
         self.timers(FORWARD_MICRO_TIMER).start()
+        if self.curriculum_scheduler is not None and self.module.training:
+            d = self.curriculum_scheduler.update_difficulty(self.global_steps + 1)
+            if self.curriculum_type == "seqlen":
+                inputs, kwargs = _truncate_seqlen(inputs, kwargs, int(d))
+            else:
+                kwargs["curriculum_seqlen"] = d
+        if self.progressive_layer_drop is not None and self.module.training:
+            kwargs.update(self.progressive_layer_drop.get_state())
         if self.optimizer is not None:
             self.optimizer.pre_forward()
         ctx = self._activation_cache.forward_context() if (self._activation_cache is not None and
@@ -366,6 +402,8 @@ class DeepSpeedEngine(nn.Module):
                 self.lr_scheduler.step(**(lr_kwargs or {}))
             self.global_steps += 1
             self.global_samples += self.train_batch_size()
+            if self.progressive_layer_drop is not None:
+                self.progressive_layer_drop.update_state(self.global_steps)
             if self.monitor.enabled and dist.get_rank() == 0:
                 self.monitor.write_events([("Train/Samples/lr", self.get_lr()[0], self.global_samples)])
             if self.global_steps % self.steps_per_print() == 0 and self.wall_clock_breakdown():
@@ -373,6 +411,13 @@ class DeepSpeedEngine(nn.Module):
         self.micro_steps += 1
         self._force_boundary = None
         self.timers(STEP_MICRO_TIMER).stop()
+
+    def set_custom_curriculum_learning_schedule(self, schedule_func_dict):
+        if self.curriculum_scheduler is not None:
+            self.curriculum_scheduler.set_custom_get_difficulty(schedule_func_dict)
+
+    def get_pld_theta(self):
+        return self.progressive_layer_drop.get_theta() if self.progressive_layer_drop else None
 
     def zero_grad(self):
         if self.optimizer is not None:

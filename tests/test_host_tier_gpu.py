@@ -49,8 +49,11 @@ def test_host_activation_cache_matches_resident():
     loss2.backward()
     assert cache.stats()["bytes_offloaded"] > 0
     assert torch.allclose(loss, loss2)
+    # hipBLASLt may pick stream-K (atomic, order-nondeterministic) GEMMs, so compare at bf16 resolution; a wrong or
+    # stale offloaded activation shows up as O(1) relative error
     for n, p in m.named_parameters():
-        assert torch.equal(p.grad, ref[n]), n
+        rel = ((p.grad.float() - ref[n].float()).norm() / (ref[n].float().norm() + 1e-12)).item()
+        assert rel < 2e-2, (n, rel)
 
 
 def test_engine_with_host_activation_cache():
