@@ -1,0 +1,166 @@
+"""Full / local views of a parameter's high-precision state held in the flat ZeRO store.
+
+Reference parity: utils/tensor_fragment.py (``safe_get_full_fp32_param`` :132, ``safe_set_full_fp32_param``,
+``safe_get_full_optimizer_state`` :164, ``safe_set_full_optimizer_state``, ``safe_get_full_grad`` :199,
+``safe_set_full_grad``, ``safe_get_local_*`` / ``safe_set_local_*`` :243-310). Each parameter is a
+contiguous range of its unit's rank-major flat buffer; the "local" fragment is the intersection of that
+range with this rank's shard, the "full" value is ONE all-gather of the unit's shard (collective over the
+unit's data-parallel group: call on every rank).
+"""
+import torch
+
+from .. import comm as dist
+
+_GRAD = "__grad__"
+_FP32 = "__fp32__"
+
+
+def _zopt(param):
+    return getattr(param, "_hds_zero", None)
+
+
+def _buffer(z, key):
+    s = z.store
+    if key == _FP32:
+        return s.master
+    if key == _GRAD:
+        return s.grad
+    return s.states.get(key)
+
+
+def _local_range(z, u, i):
+    """(param-relative [a, b), store [lo, hi)) of this rank's fragment of param i of unit u."""
+    lo_sh, hi_sh = u.rank * u.shard, (u.rank + 1) * u.shard
+    p0, p1 = u.offsets[i], u.offsets[i] + u.numels[i]
+    a, b = max(lo_sh, p0), min(hi_sh, p1)
+    if a >= b:
+        return None
+    return (a - p0, b - p0), (u.store_off + a - lo_sh, u.store_off + b - lo_sh)
+
+
+def _full_unit(z, u, key):
+    buf = _buffer(z, key)
+    if buf is None:
+        return None
+    mine = buf[u.store_off:u.store_off + u.shard]
+    if u.world == 1:
+        return mine
+    full = torch.empty(u.padded, dtype=mine.dtype, device=mine.device)
+    dist.all_gather_into_tensor(full, mine.contiguous(), group=u.dp_group)
+    return full
+
+
+def _get_full(param, key):
+    z = _zopt(param)
+    if z is None:
+        if key == _GRAD:
+            return None if param.grad is None else param.grad.float()
+        return param.detach().float() if key == _FP32 else None
+    u, i = z.param_to_unit[id(param)]
+    full = _full_unit(z, u, key)
+    if full is None:
+        return None
+    out = u.param_view(full, i).clone().float()
+    if key == _GRAD:
+        out.mul_(1.0 / (z.layout_world_for_avg() * z.loss_scaler.loss_scale))
+    return out
+
+
+def _set_full(param, value, key):
+    z = _zopt(param)
+    if z is None:
+        if key == _FP32:
+            param.data.copy_(value)
+        elif key == _GRAD:
+            param.grad = value.to(param.dtype).clone()
+        return
+    u, i = z.param_to_unit[id(param)]
+    r = _local_range(z, u, i)
+    if r is not None:
+        (a, b), (lo, hi) = r
+        buf = _buffer(z, key)
+        src = value.reshape(-1)[a:b].to(buf.dtype)
+        if key == _GRAD:
+            src = src * (z.layout_world_for_avg() * z.loss_scaler.loss_scale)
+        buf[lo:hi].copy_(src)
+        if key == _FP32:
+            z.store.lp[lo:hi].copy_(buf[lo:hi])
+    if key == _FP32:
+        z._post_step_gather()  # collective: every rank refreshes the gathered copies
+
+
+def safe_get_full_fp32_param(param):
+    return _get_full(param, _FP32)
+
+
+def safe_set_full_fp32_param(param, value):
+    _set_full(param, value, _FP32)
+
+
+def safe_get_full_optimizer_state(param, optim_state_key):
+    return _get_full(param, optim_state_key)
+
+
+def safe_set_full_optimizer_state(param, value, optim_state_key):
+    _set_full(param, value, optim_state_key)
+
+
+def safe_get_full_grad(param):
+    """Averaged (over data parallel) fp32 gradient; valid between backward and step."""
+    return _get_full(param, _GRAD)
+
+
+def safe_set_full_grad(param, value):
+    _set_full(param, value, _GRAD)
+
+
+def _get_local(param, key):
+    z = _zopt(param)
+    if z is None:
+        return _get_full(param, key)
+    u, i = z.param_to_unit[id(param)]
+    r = _local_range(z, u, i)
+    if r is None:
+        return None
+    _, (lo, hi) = r
+    buf = _buffer(z, key)
+    return None if buf is None else buf[lo:hi].float().clone()
+
+
+def _set_local(param, value, key):
+    z = _zopt(param)
+    if z is None:
+        return _set_full(param, value, key)
+    u, i = z.param_to_unit[id(param)]
+    r = _local_range(z, u, i)
+    if r is None:
+        return
+    _, (lo, hi) = r
+    buf = _buffer(z, key)
+    buf[lo:hi].copy_(value.reshape(-1).to(buf.dtype))
+    if key == _FP32:
+        z.store.lp[lo:hi].copy_(buf[lo:hi])
+
+
+def safe_get_local_grad(param):
+    return _get_local(param, _GRAD)
+
+
+def safe_set_local_grad(param, value):
+    _set_local(param, value, _GRAD)
+
+
+def safe_get_local_fp32_param(param):
+    return _get_local(param, _FP32)
+
+
+def safe_set_local_fp32_param(param, value):
+    _set_local(param, value, _FP32)
+
+
+def safe_get_local_optimizer_state(param, optim_state_key):
+    return _get_local(param, optim_state_key)
+
+
+def safe_set_local_optimizer_state(param, value, optim_state_key):
+    _set_local(param, value, optim_state_key)

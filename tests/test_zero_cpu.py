@@ -152,3 +152,37 @@ def test_flops_profiler_counts_gemms_and_attention():
     prof.end_profile()
     f, macs, params = get_model_profile(m, args=[x], print_profile=False, as_string=False)
     assert f == flops
+
+
+def _fragments(rank, world):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.utils import (safe_get_full_fp32_param, safe_get_full_grad, safe_get_full_optimizer_state,
+                                            safe_get_local_fp32_param, safe_set_full_fp32_param)
+    m, ref = _models()
+    cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}},
+           "zero_optimization": {"stage": 3}}
+    eng, _, _, _ = ds.initialize(model=m, config=cfg)
+    x = torch.randint(0, 97, (world * 2, 12), generator=torch.Generator().manual_seed(0))
+    loss = eng(x[rank * 2:(rank + 1) * 2], labels=x[rank * 2:(rank + 1) * 2])
+    eng.backward(loss)
+    rl = ref(x, labels=x)
+    rl.backward()
+    rp = dict(ref.named_parameters())
+    for name, p in m.named_parameters():
+        g = safe_get_full_grad(p)
+        assert torch.allclose(g, rp[name].grad, atol=1e-5, rtol=1e-4), name
+        assert torch.allclose(safe_get_full_fp32_param(p), rp[name].detach(), atol=1e-6), name
+    eng.step()
+    name, p = next(iter(m.named_parameters()))
+    ea = safe_get_full_optimizer_state(p, "exp_avg")
+    assert ea.shape == p.ds_shape and ea.abs().sum() > 0
+    new = torch.full(p.ds_shape, 0.25)
+    safe_set_full_fp32_param(p, new)
+    assert torch.allclose(safe_get_full_fp32_param(p), new)
+    loc = safe_get_local_fp32_param(p)
+    assert loc is None or torch.allclose(loc, torch.full_like(loc, 0.25))
+
+
+def test_safe_get_set_tensor_fragments_world2():
+    run_distributed(_fragments, 2)
