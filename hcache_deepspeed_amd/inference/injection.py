@@ -104,7 +104,7 @@ def _hds_attention(module, query, key, value, attention_mask, scaling, dropout=0
 def register_attention():
     try:
         from transformers import AttentionInterface
-        AttentionInterface.register("hds_flash", _hds_attention)
+        AttentionInterface.register("hds_fused_attn", _hds_attention)
         return True
     except Exception:  # noqa: BLE001
         return False
@@ -132,11 +132,11 @@ def inject(model, quant=None, trainable=False, fuse_mlp=True):
     cfg = getattr(model, "config", None)
     if cfg is not None and hasattr(cfg, "_attn_implementation") and register_attention():
         try:
-            cfg._attn_implementation = "hds_flash"
+            cfg._attn_implementation = "hds_fused_attn"
             for sub in model.modules():
                 sc = getattr(sub, "config", None)
                 if sc is not None and hasattr(sc, "_attn_implementation"):
-                    sc._attn_implementation = "hds_flash"
+                    sc._attn_implementation = "hds_fused_attn"
             n += 1
         except Exception:  # noqa: BLE001
             pass

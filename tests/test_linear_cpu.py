@@ -1,0 +1,50 @@
+"""OptimizedLinear / LoRA / FP8 QuantizedLinear (reference tests/unit/linear/test_linear.py, test_quant_param.py)."""
+import pytest
+import torch
+
+from tests.dist_utils import run_distributed
+
+
+def test_lora_linear_forward_and_grads():
+    from hcache_deepspeed_amd.linear import LoRAConfig, OptimizedLinear
+    torch.manual_seed(0)
+    lin = OptimizedLinear(32, 48, lora_config=LoRAConfig(lora_r=4, lora_alpha=8), dtype=torch.float32)
+    x = torch.randn(5, 32)
+    y = lin(x)
+    assert torch.allclose(y, x @ lin.full_weight().t(), atol=1e-5)  # B = 0 at init
+    y.sum().backward()
+    assert lin.weight.grad is None and not lin.weight.requires_grad
+    assert lin.lora_weight_2.weight.grad is not None
+    with torch.no_grad():
+        lin.lora_weight_2.weight.normal_()
+    y1 = lin(x)
+    lin.fuse_lora_weight()
+    assert torch.allclose(lin(x), y1, atol=1e-4)
+    lin.unfuse_lora_weight()
+    assert torch.allclose(lin(x), y1, atol=1e-4)
+
+
+def test_plain_and_quantized_dispatch():
+    import torch.nn as nn
+    from hcache_deepspeed_amd.linear import OptimizedLinear, QuantizationConfig, QuantizedLinear
+    assert type(OptimizedLinear(8, 8, dtype=torch.float32)) is nn.Linear
+    q = OptimizedLinear(64, 64, quantization_config=QuantizationConfig(group_size=64), dtype=torch.float32)
+    assert isinstance(q, QuantizedLinear)
+    x = torch.randn(3, 64)
+    w = q.weight.dequantized()
+    assert w.shape == (64, 64) and torch.allclose(q(x), x @ w.t(), atol=1e-5)
+
+
+def _sharded(rank, world):
+    from hcache_deepspeed_amd.linear import LoRAConfig, OptimizedLinear
+    torch.manual_seed(0)  # same init on both ranks -> shards of one weight
+    lin = OptimizedLinear(30, 20, lora_config=LoRAConfig(lora_r=2, base_weight_sharding=world), dtype=torch.float32)
+    assert lin.weight.numel() == (30 * 20 + world - 1) // world
+    full = lin.full_weight()
+    torch.manual_seed(0)
+    ref = OptimizedLinear(30, 20, lora_config=LoRAConfig(lora_r=2), dtype=torch.float32)
+    assert torch.equal(full, ref.full_weight())
+
+
+def test_base_weight_sharding_world2():
+    run_distributed(_sharded, 2)
