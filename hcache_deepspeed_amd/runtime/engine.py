@@ -404,6 +404,8 @@ class DeepSpeedEngine(nn.Module):
             self.global_samples += self.train_batch_size()
             if self.progressive_layer_drop is not None:
                 self.progressive_layer_drop.update_state(self.global_steps)
+            if self._config.autotuning.get("enabled", False):
+                self._autotuning_step()
             if self.monitor.enabled and dist.get_rank() == 0:
                 self.monitor.write_events([("Train/Samples/lr", self.get_lr()[0], self.global_samples)])
             if self.global_steps % self.steps_per_print() == 0 and self.wall_clock_breakdown():
@@ -411,6 +413,33 @@ class DeepSpeedEngine(nn.Module):
         self.micro_steps += 1
         self._force_boundary = None
         self.timers(STEP_MICRO_TIMER).stop()
+
+    def _autotuning_step(self):
+        """Autotuning experiment hook (reference engine.py:2458-2480): time steps (start, end], write the
+        metric file and, when launched by the autotuner, end the process."""
+        import json
+        import sys
+        import time
+        at = self._config.autotuning
+        start, end = int(at.get("start_profile_step", 3)), int(at.get("end_profile_step", 5))
+        if self.global_steps == start:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            self._at_t0 = time.time()
+        elif self.global_steps == end and getattr(self, "_at_t0", None) is not None:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            dt = (time.time() - self._at_t0) / max(1, end - start)
+            metric = {"throughput": self.train_batch_size() / dt, "latency": dt,
+                      "train_micro_batch_size_per_gpu": self.train_micro_batch_size_per_gpu(),
+                      "zero_stage": self.zero_optimization_stage()}
+            path = at.get("metric_path")
+            if path and dist.get_rank() == 0:
+                with open(path, "w") as f:
+                    json.dump(metric, f)
+            if os.environ.get("HDS_AUTOTUNING_EXIT") == "1":
+                dist.barrier()
+                sys.exit(0)
 
     def set_custom_curriculum_learning_schedule(self, schedule_func_dict):
         if self.curriculum_scheduler is not None:
