@@ -139,7 +139,8 @@ def main():
     mem = torch.cuda.max_memory_allocated(dev) / 2**30
     if rank == 0:
         out = {
-            "metric": "tokens/sec (node) Llama-3-8B ZeRO-3 at 1/2/4/8 MI355X",
+            "metric": ("tokens/sec (node) Llama-3-8B ZeRO-3 at 1/2/4/8 MI355X" if args.model == "llama3-8b" else
+                       f"tokens/sec (node) {args.model} ZeRO-{args.zero}"),
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": world,
