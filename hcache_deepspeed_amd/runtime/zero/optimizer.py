@@ -179,6 +179,12 @@ class ZeroOptimizer:
         self._build_units(leaf_modules)
         self._build_store()
         self._install_hooks()
+        if self.stage == 3 and self.partitioned and self.zcfg.memory_efficient_linear:
+            # keep only the Parameter (not its gathered data) alive in the autograd graph
+            from .linear import wrap_memory_efficient_linears
+            for u in self.units:
+                if not u.persistent and u.module is not None:
+                    wrap_memory_efficient_linears(u.module)
         self.micro_in_window = 0
         self.boundary = True
         self.in_backward = False

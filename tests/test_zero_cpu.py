@@ -186,3 +186,37 @@ def _fragments(rank, world):
 
 def test_safe_get_set_tensor_fragments_world2():
     run_distributed(_fragments, 2)
+
+
+def _released_memory(rank, world):
+    """ZeRO-3 with memory-efficient linears: a layer's gathered weights are actually freed after its forward
+    (the autograd graph must not pin them), and training still matches the non-partitioned trajectory."""
+    import gc
+    import weakref
+    import hcache_deepspeed_amd as ds
+    m, ref = _models()
+    cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
+           "zero_optimization": {"stage": 3}}
+    eng, _, _, _ = ds.initialize(model=m, config=cfg)
+    z = eng.optimizer
+    refs = []
+    orig = z._release
+
+    def spy(u):
+        if u.full is not None and not z.in_backward:
+            refs.append(weakref.ref(u.full))
+        orig(u)
+
+    z._release = spy
+    x = torch.randint(0, 97, (2, 12), generator=torch.Generator().manual_seed(rank))
+    loss = eng(x, labels=x)
+    gc.collect()
+    assert refs, "no unit was released during forward"
+    alive = sum(r() is not None for r in refs)
+    assert alive == 0, f"{alive}/{len(refs)} released unit buffers are still referenced"
+    eng.backward(loss)
+    eng.step()
+
+
+def test_zero3_releases_gathered_weights_world2():
+    run_distributed(_released_memory, 2)
