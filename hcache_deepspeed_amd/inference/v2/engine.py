@@ -69,6 +69,10 @@ class InferenceEngineV2:
                 torch.device("cpu")
         self.device = device
         dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[self._config.dtype]
+        from .arch import ArchSpec, convert_own_llama, spec_from_llama_config
+        if not isinstance(model_config, ArchSpec):  # this framework's Llama / Mixtral training configs
+            model_config = spec_from_llama_config(model_config)
+            weights = convert_own_llama(weights, model_config)
         self._model = RaggedTransformer(model_config, weights, device, dtype, tp_group=self._base_mp_group,
                                         latent_mode=self._config.latent_mode)
         sm = self._config.state_manager
@@ -214,22 +218,28 @@ class InferenceEngineV2:
         self._state_manager.flush_sequence(uid)
 
     def serialize(self, save_path: str) -> None:
+        """Write this rank's canonical weight shards + the ArchSpec (reference engine_v2.py ``serialize`` :284)."""
+        import dataclasses
         os.makedirs(save_path, exist_ok=True)
         m = self._model
-        sd = {"model.embed_tokens.weight": m.embed, "model.norm.weight": m.norm, "lm_head.weight": m.lm_head}
-        for i, L in enumerate(m.layers):
-            p = f"model.layers.{i}."
-            sd[p + "input_layernorm.weight"] = L.ln1
-            sd[p + "post_attention_layernorm.weight"] = L.ln2
-            sd[p + "self_attn.qkv_proj.weight"] = L.qkv
-            sd[p + "self_attn.o_proj.weight"] = L.o
-            if L.gate_up is not None:
-                sd[p + "mlp.gate_up_proj.weight"] = L.gate_up
-                sd[p + "mlp.down_proj.weight"] = L.down
-        rank = m.tp_rank
-        torch.save({k: v.cpu() for k, v in sd.items()}, os.path.join(save_path, f"params_rank_{rank}.pt"))
+        sd = {"embed": m.embed, "pos_embed": m.pos_embed, "final.w": m.final_w, "final.b": m.final_b,
+              "lm_head.w": m.lm_head, "lm_head.b": m.lm_head_b,
+              "layers": [{k: v for k, v in L.w.items() if v is not None} for L in m.layers]}
+
+        def cpu(x):
+            if isinstance(x, torch.Tensor):
+                return x.cpu()
+            if isinstance(x, dict):
+                return {k: cpu(v) for k, v in x.items() if v is not None}
+            if isinstance(x, list):
+                return [cpu(v) for v in x]
+            return x
+
+        torch.save(cpu(sd), os.path.join(save_path, f"params_rank_{m.tp_rank}.pt"))
+        meta = dataclasses.asdict(m.spec)
+        meta["tp_size"] = m.tp
         with open(os.path.join(save_path, "ds_model_config.json"), "w") as f:
-            json.dump(m.cfg.to_dict(), f)
+            json.dump(meta, f, default=str)
 
     # ------------------------------------------------------------------------------------------
     def generate(self, uid, prompt, max_new_tokens=16):
@@ -253,24 +263,47 @@ def build_engine_from_model(model, engine_config=None, device=None, num_kv_block
 
 
 def build_hf_engine(path, engine_config=None, debug_level=None, device=None):
-    """Serving engine from a HuggingFace checkpoint directory (config.json + *.safetensors)."""
-    from ...models.llama import LlamaConfig, convert_hf_state_dict
+    """Serving engine from a HuggingFace checkpoint directory (config.json + *.safetensors / *.bin).
+
+    Supported ``model_type``: llama, mistral, mixtral, qwen, qwen2, qwen2_moe, phi, phi3, falcon, opt
+    (reference inference/v2/engine_factory.py:69-130)."""
+    from .arch import convert_hf, spec_from_hf
     with open(os.path.join(path, "config.json")) as f:
         hf = json.load(f)
-    mt = hf.get("model_type", "llama")
-    if mt not in ("llama", "mistral", "qwen2"):
-        raise NotImplementedError(f"model_type {mt} is not supported by the serving engine yet")
-    cfg = LlamaConfig.from_dict({**hf, "model_type": mt, "sliding_window": hf.get("sliding_window") or 0})
-    from safetensors.torch import load_file
+    spec = spec_from_hf(hf)
     sd = {}
     for fn in sorted(os.listdir(path)):
+        full = os.path.join(path, fn)
         if fn.endswith(".safetensors"):
-            sd.update(load_file(os.path.join(path, fn)))
-    sd = convert_hf_state_dict(sd, cfg)
-    for i in range(cfg.num_hidden_layers):
-        p = f"model.layers.{i}.self_attn."
-        if p + "q_proj.bias" in sd:
-            sd[p + "qkv_proj.bias"] = torch.cat([sd[p + "q_proj.bias"], sd[p + "k_proj.bias"], sd[p + "v_proj.bias"]])
+            from safetensors.torch import load_file
+            sd.update(load_file(full))
+        elif fn.endswith(".bin") and fn.startswith("pytorch_model"):
+            sd.update(torch.load(full, map_location="cpu", weights_only=True))
     if isinstance(engine_config, dict):
         engine_config = RaggedInferenceEngineConfig.from_dict(engine_config)
-    return InferenceEngineV2(cfg, sd, engine_config, device=device)
+    return InferenceEngineV2(spec, convert_hf(sd, spec), engine_config, device=device)
+
+
+def build_engine_from_hf_model(hf_model, engine_config=None, device=None, num_kv_blocks=None):
+    """Serving engine from an in-memory ``transformers`` model (any supported model_type)."""
+    from .arch import convert_hf, spec_from_hf
+    spec = spec_from_hf(hf_model.config.to_dict())
+    sd = {k: v.detach() for k, v in hf_model.state_dict().items()}
+    if isinstance(engine_config, dict):
+        engine_config = RaggedInferenceEngineConfig.from_dict(engine_config)
+    return InferenceEngineV2(spec, convert_hf(sd, spec), engine_config, device=device, num_kv_blocks=num_kv_blocks)
+
+
+def build_engine_from_ds_checkpoint(path, engine_config=None, device=None, num_kv_blocks=None):
+    """Reload a ``serialize()``d engine (same tensor-parallel size)."""
+    from .arch import ArchSpec
+    with open(os.path.join(path, "ds_model_config.json")) as f:
+        meta = json.load(f)
+    tp = meta.pop("tp_size", 1)
+    spec = ArchSpec(**{k: v for k, v in meta.items() if k in ArchSpec.__dataclass_fields__})
+    if isinstance(engine_config, dict):
+        engine_config = RaggedInferenceEngineConfig.from_dict(engine_config)
+    rank = dist.get_rank() if (tp > 1 and dist.is_initialized()) else 0
+    sd = torch.load(os.path.join(path, f"params_rank_{rank}.pt"), map_location="cpu", weights_only=True)
+    return InferenceEngineV2(spec, {"__presharded__": True, **sd}, engine_config, device=device,
+                             num_kv_blocks=num_kv_blocks)

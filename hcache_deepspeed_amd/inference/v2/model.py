@@ -1,120 +1,171 @@
-"""Ragged paged-KV transformer for serving, with the HCache contract on every model.
+"""Ragged paged-KV decoder for serving, with the HCache contract on every supported family.
 
-Reference parity: inference/v2/model_implementations/llama_v2/model.py (``Llama2InferenceModel``,
-HCache-modified forward :203-220 and ``restore_kv`` :222-244), mistral / qwen2 implementations, the
-DSTransformerModelBase contract and the TP sharding helpers (model_implementations/sharding/*).
+Reference parity: inference/v2/model_implementations/llama_v2/model.py (``Llama2InferenceModel``, HCache-modified
+forward :203-220 and ``restore_kv`` :222-244) and the mistral / mixtral / qwen / qwen_v2 / qwen_v2_moe / phi /
+phi3 / falcon / opt implementations, the DSTransformerModelBase contract and the TP sharding helpers
+(model_implementations/sharding/*). One implementation, driven by :class:`arch.ArchSpec`: RMSNorm or
+LayerNorm (+bias), gated (SwiGLU) or plain (GELU/ReLU) MLPs with optional biases, sequential or parallel
+(shared-norm / two-norm) residual blocks, RoPE (full or partial) or learned positions, sliding windows, and
+top-k MoE with optional shared expert.
 
 HCache, as implemented here (with the defects fixed):
 
-* ``forward(batch, capture_latents=True)`` returns ``(logits, latents)``: the post-RMSNorm hidden state
-  entering every layer's QKV projection, ``[L, T, H]``. Each layer's slice is copied D2H on a side HIP
-  stream into a PINNED host buffer as soon as it is produced (event-ordered), so the transfer overlaps
-  the remaining layers instead of one blocking pageable ``.cpu()`` at the end.
-* ``restore_kv(batch, latents)`` rebuilds the paged KV cache from host latents: a copy stream streams
-  layer i+1 host->device (pinned, async) while the compute stream runs layer i's QKV GEMM + fused
-  RoPE/KV-scatter. Attention, O-projection and MLP are skipped (~1/4-1/6 of the layer FLOPs).
-* ``latent_mode="kv"`` stores post-RoPE K|V per token-layer instead (2*Hkv*D elements; half of H for
-  Llama-3 GQA) and restore becomes a pure scatter.
-* every model type in this module implements the contract (the reference broke ``put`` for all
-  non-Llama models).
+* ``forward(batch, capture_latents=True)`` returns ``(logits, latents)``: the normed hidden state entering
+  every layer's QKV projection, ``[L, T, H]``. Each layer's slice is copied D2H on a side HIP stream into a
+  PINNED host buffer as soon as it is produced (event-ordered), so the transfer overlaps the remaining
+  layers instead of one blocking pageable ``.cpu()`` at the end.
+* ``restore_kv(batch, latents)`` rebuilds the paged KV cache from host latents: a copy stream streams layer
+  i+1 host->device (pinned, async) while the compute stream runs layer i's K|V GEMM + fused RoPE/KV-scatter.
+  Attention, O-projection and MLP are skipped.
+* ``latent_mode="kv"`` stores the PRE-RoPE K|V rows per token-layer instead (2*Hkv*D elements; half of H for
+  Llama-3 GQA); restore then only rotates and scatters.
+* every family above implements the contract (the reference broke ``put`` for all non-Llama models).
 """
 import math
 
 import torch
-import torch.nn as nn
 import torch.nn.functional as F
 
 from ... import comm as dist
-from ...ops.activations import glu
-from ...ops.norm import rms_norm
+from ...ops.activations import bias_act, glu
+from ...ops.moe import moe_combine, moe_dispatch, topk_route
+from ...ops.norm import layer_norm, rms_norm
 from ...ops.paged import build_atoms, kv_rope_scatter, paged_attention
 from ...ops.rope import rope_tables
 
 
-class _LayerWeights:
-    __slots__ = ("ln1", "qkv", "qkv_bias", "o", "ln2", "gate_up", "down", "moe")
+class _Layer:
+
+    def __init__(self):
+        self.w = {}
+
+    def __getitem__(self, k):
+        return self.w.get(k)
 
 
 class RaggedTransformer:
-    """Llama / Mistral / Qwen2-style decoder over a paged KV cache (optionally tensor-parallel)."""
+    """Decoder over a paged KV cache (optionally tensor-parallel), configured by an ArchSpec."""
 
-    def __init__(self, cfg, weights, device, dtype=torch.bfloat16, tp_group=None, latent_mode="hidden"):
-        self.cfg = cfg
+    def __init__(self, spec, weights, device, dtype=torch.bfloat16, tp_group=None, latent_mode="hidden"):
+        self.cfg = self.spec = spec
         self.device = device
         self.dtype = dtype
         self.tp_group = tp_group
         self.tp = dist.get_world_size(tp_group) if tp_group is not None else 1
         self.tp_rank = dist.get_rank(tp_group) if tp_group is not None else 0
         self.latent_mode = latent_mode
-        H, D = cfg.hidden_size, cfg.head_dim
-        assert cfg.num_attention_heads % self.tp == 0 and cfg.num_key_value_heads % self.tp == 0
-        self.n_q = cfg.num_attention_heads // self.tp
-        self.n_kv = cfg.num_key_value_heads // self.tp
+        D = spec.head_dim
+        assert spec.num_attention_heads % self.tp == 0 and spec.num_key_value_heads % self.tp == 0, \
+            "attention heads must divide the tensor-parallel size"
+        self.n_q = spec.num_attention_heads // self.tp
+        self.n_kv = spec.num_key_value_heads // self.tp
         self.d = D
-        self.I = cfg.intermediate_size // self.tp
+        self.rot = spec.rotary_dim if 0 < spec.rotary_dim < D else D
         self._load(weights)
-        self.cos, self.sin = rope_tables(max(cfg.max_position_embeddings, 8192), D, cfg.rope_theta, cfg.rope_scaling,
-                                         device=device)
+        if spec.pos == "rope":
+            self.cos, self.sin = rope_tables(max(spec.max_position_embeddings, 8192), self.rot, spec.rope_theta,
+                                             spec.rope_scaling, device=device)
+        else:
+            self.cos = self.sin = None
         self.scale = 1.0 / math.sqrt(D)
         self.kv_cache = None
         self.copy_stream = torch.cuda.Stream(device) if device.type == "cuda" else None
 
     # ------------------------------------------------------------------------------------------
-    # weights (TP sharding: heads for QKV, rows for O/down, columns for gate|up; LM head by vocab)
+    # weights: canonical dict (arch.convert_*) -> this rank's shards
     # ------------------------------------------------------------------------------------------
+    def _t(self, x):
+        return None if x is None else x.to(device=self.device, dtype=self.dtype).contiguous()
+
+    def _rows(self, x):
+        if x is None or self.tp == 1:
+            return x
+        n = x.shape[0] // self.tp
+        return x[self.tp_rank * n:(self.tp_rank + 1) * n]
+
+    def _cols(self, x):
+        if x is None or self.tp == 1:
+            return x
+        n = x.shape[-1] // self.tp
+        return x[..., self.tp_rank * n:(self.tp_rank + 1) * n]
+
+    def _gated_rows(self, x):
+        """[gate; up] stacked on dim -2 -> this rank's gate rows and up rows."""
+        if x is None or self.tp == 1:
+            return x
+        g, u = x.chunk(2, dim=-2)
+        n = g.shape[-2] // self.tp
+        sl = slice(self.tp_rank * n, (self.tp_rank + 1) * n)
+        return torch.cat([g[..., sl, :], u[..., sl, :]], -2)
+
     def _load(self, sd):
-        cfg, tp, r = self.cfg, self.tp, self.tp_rank
-        D, Hq, Hkv = cfg.head_dim, cfg.num_attention_heads, cfg.num_key_value_heads
-
-        def t(x):
-            return x.to(device=self.device, dtype=self.dtype).contiguous()
-
-        self.embed = t(sd["model.embed_tokens.weight"])
-        self.norm = t(sd["model.norm.weight"])
-        lm = sd.get("lm_head.weight", sd["model.embed_tokens.weight"])
+        if sd.get("__presharded__"):  # reloaded serialize() shards: already this rank's slices
+            self._rows = self._cols = self._gated_rows = lambda x: x
+            return self._load_presharded(sd)
+        spec, r = self.spec, self.tp_rank
+        D, Hq, Hkv = spec.head_dim, spec.num_attention_heads, spec.num_key_value_heads
+        nq, nkv = self.n_q, self.n_kv
+        t = self._t
+        self.embed = t(sd["embed"])
+        self.pos_embed = t(sd.get("pos_embed"))
+        self.final_w, self.final_b = t(sd.get("final.w")), t(sd.get("final.b"))
+        lm = sd.get("lm_head.w")
+        lm = sd["embed"] if lm is None else lm
         V = lm.shape[0]
-        vs = (V + tp - 1) // tp
+        vs = (V + self.tp - 1) // self.tp
         self.vocab = V
         self.lm_head = t(lm[r * vs:(r + 1) * vs])
+        lb = sd.get("lm_head.b")
+        self.lm_head_b = t(lb[r * vs:(r + 1) * vs]) if lb is not None else None
         self.layers = []
-        for i in range(cfg.num_hidden_layers):
-            p = f"model.layers.{i}."
-            L = _LayerWeights()
-            L.ln1 = t(sd[p + "input_layernorm.weight"])
-            L.ln2 = t(sd[p + "post_attention_layernorm.weight"])
-            qkv = sd[p + "self_attn.qkv_proj.weight"]
-            q, k, v = qkv.split([Hq * D, Hkv * D, Hkv * D], 0)
-            nq, nkv = Hq // tp, Hkv // tp
-            L.qkv = t(torch.cat([q[r * nq * D:(r + 1) * nq * D], k[r * nkv * D:(r + 1) * nkv * D],
-                                 v[r * nkv * D:(r + 1) * nkv * D]], 0))
-            qb = sd.get(p + "self_attn.qkv_proj.bias")
-            if qb is not None:
-                bq, bk, bv = qb.split([Hq * D, Hkv * D, Hkv * D], 0)
-                L.qkv_bias = t(torch.cat([bq[r * nq * D:(r + 1) * nq * D], bk[r * nkv * D:(r + 1) * nkv * D],
-                                          bv[r * nkv * D:(r + 1) * nkv * D]], 0))
+        for Ls in sd["layers"]:
+            L = _Layer()
+            w = L.w
+            for k in ("ln1.w", "ln1.b", "ln2.w", "ln2.b"):
+                w[k] = t(Ls.get(k))
+
+            def heads(x):
+                if x is None:
+                    return None
+                q, k_, v = x.split([Hq * D, Hkv * D, Hkv * D], 0)
+                return torch.cat([q[r * nq * D:(r + 1) * nq * D], k_[r * nkv * D:(r + 1) * nkv * D],
+                                  v[r * nkv * D:(r + 1) * nkv * D]], 0)
+
+            w["qkv.w"], w["qkv.b"] = t(heads(Ls["qkv.w"])), t(heads(Ls.get("qkv.b")))
+            w["o.w"] = t(self._cols(Ls["o.w"]))
+            w["o.b"] = t(Ls.get("o.b")) if r == 0 else None  # row-parallel bias added once
+            if "w13" in Ls:
+                w["router.w"] = t(Ls["router.w"])
+                w["w13"] = t(self._gated_rows(Ls["w13"]))
+                w["w2"] = t(self._cols(Ls["w2"]))
+                w["shared.w13"] = t(self._gated_rows(Ls.get("shared.w13")))
+                w["shared.w2"] = t(self._cols(Ls.get("shared.w2")))
+                w["shared_gate.w"] = t(Ls.get("shared_gate.w"))
             else:
-                L.qkv_bias = None
-            o = sd[p + "self_attn.o_proj.weight"]
-            L.o = t(o[:, r * nq * D:(r + 1) * nq * D])
-            gu = sd.get(p + "mlp.gate_up_proj.weight")
-            L.moe = None
-            if gu is not None:
-                I = cfg.intermediate_size
-                g, u = gu.split([I, I], 0)
-                ii = I // tp
-                L.gate_up = t(torch.cat([g[r * ii:(r + 1) * ii], u[r * ii:(r + 1) * ii]], 0))
-                L.down = t(sd[p + "mlp.down_proj.weight"][:, r * ii:(r + 1) * ii])
-            else:
-                L.gate_up = L.down = None
-                L.moe = self._load_moe(sd, p)
+                up = Ls["up.w"]
+                w["up.w"] = t(self._gated_rows(up) if self.spec.gated else self._rows(up))
+                ub = Ls.get("up.b")
+                if ub is not None:
+                    w["up.b"] = t(self._gated_rows(ub[:, None])[:, 0] if self.spec.gated else self._rows(ub))
+                w["down.w"] = t(self._cols(Ls["down.w"]))
+                w["down.b"] = t(Ls.get("down.b")) if r == 0 else None
             self.layers.append(L)
 
-    def _load_moe(self, sd, p):
-        return None
+    def _load_presharded(self, sd):
+        t = self._t
+        self.embed, self.pos_embed = t(sd["embed"]), t(sd.get("pos_embed"))
+        self.final_w, self.final_b = t(sd.get("final.w")), t(sd.get("final.b"))
+        self.lm_head, self.lm_head_b = t(sd["lm_head.w"]), t(sd.get("lm_head.b"))
+        self.vocab = self.spec.vocab_size
+        self.layers = []
+        for Ls in sd["layers"]:
+            L = _Layer()
+            L.w = {k: t(v) for k, v in Ls.items()}
+            self.layers.append(L)
 
     # ------------------------------------------------------------------------------------------
     def kv_cache_config(self):
-        return dict(num_layers=self.cfg.num_hidden_layers, n_kv_heads=self.n_kv, head_dim=self.d)
+        return dict(num_layers=self.spec.num_hidden_layers, n_kv_heads=self.n_kv, head_dim=self.d)
 
     def set_kv_cache(self, kv_cache):
         self.kv_cache = kv_cache
@@ -124,52 +175,104 @@ class RaggedTransformer:
             dist.all_reduce(x, group=self.tp_group)
         return x
 
+    def _norm(self, x, w, b, residual=None):
+        eps = self.spec.norm_eps
+        if self.spec.norm == "rms":
+            return rms_norm(x, w, eps, residual) if residual is not None else rms_norm(x, w, eps)
+        return layer_norm(x, w, b, eps, residual) if residual is not None else layer_norm(x, w, b, eps)
+
+    def _act_name(self):
+        a = self.spec.act
+        return {"gelu_new": "gelu_tanh", "gelu_pytorch_tanh": "gelu_tanh"}.get(a, a)
+
     def _mlp(self, L, x):
-        if L.moe is not None:
-            return L.moe(x)
-        return F.linear(glu(F.linear(x, L.gate_up), self.cfg.hidden_act), L.down)
+        if L["w13"] is not None:
+            return self._moe(L, x)
+        if self.spec.gated:
+            h = F.linear(x, L["up.w"], L["up.b"])
+            return F.linear(glu(h, self._act_name()), L["down.w"], L["down.b"])
+        h = bias_act(F.linear(x, L["up.w"]), L["up.b"], self._act_name())
+        return F.linear(h, L["down.w"], L["down.b"])
+
+    def _moe(self, L, x):
+        """Inference top-k MoE (no token dropping): dispatch into expert-major slots, batched expert GEMMs."""
+        m = self.spec.moe
+        T, H = x.shape
+        logits = F.linear(x.float(), L["router.w"].float())
+        E = logits.shape[-1]
+        expert, pos, w, C, _, _ = topk_route(logits, m["top_k"], 1.0, 1, drop_tokens=False, use_rts=False,
+                                             normalize=m["normalize"], training=False)
+        disp = moe_dispatch(x, expert, pos, E, C).view(E, C, H)
+        h = torch.bmm(disp, L["w13"].transpose(1, 2))
+        y = torch.bmm(glu(h.reshape(E * C, -1), self._act_name()).view(E, C, -1), L["w2"].transpose(1, 2))
+        out = moe_combine(y.reshape(E * C, H), expert, pos, w, C)
+        if L["shared.w13"] is not None:
+            s = F.linear(glu(F.linear(x, L["shared.w13"]), self._act_name()), L["shared.w2"])
+            gate = torch.sigmoid(F.linear(x.float(), L["shared_gate.w"].float())).to(s.dtype)
+            out = out + gate * s
+        return out
 
     def _prep(self, batch):
         atoms, n_atoms = build_atoms(batch.seq_meta_host, self.n_q, self.n_kv)
         batch.atoms = atoms.to(self.device, non_blocking=True)
         batch.n_atoms = n_atoms
 
+    def _embed(self, batch):
+        h = F.embedding(batch.input_ids, self.embed)
+        if self.pos_embed is not None:
+            h = h + F.embedding(batch.tok_pos.long() + self.spec.pos_offset, self.pos_embed)
+        return h
+
+    def _attn(self, i, L, x, batch, T, capture, lat, events):
+        nq, nkv, D = self.n_q, self.n_kv, self.d
+        qkv = F.linear(x, L["qkv.w"], L["qkv.b"]).view(T, nq + 2 * nkv, D)
+        if capture and self.latent_mode == "kv":
+            self._d2h(qkv[:, nq:].reshape(T, -1).clone(), lat[i], events)  # pre-RoPE K|V
+        cache = self.kv_cache.get_cache(i)
+        kv_rope_scatter(qkv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, nq, nkv,
+                        do_rope=self.cos is not None, rotary_dim=self.rot)
+        o = paged_attention(qkv[:, :nq], cache, batch.atoms, batch.n_atoms, batch.seq_meta, batch.block_tables, nq,
+                            nkv, self.scale, self.spec.sliding_window, batch.seq_meta_host, batch.tables_host)
+        return F.linear(o.reshape(T, nq * D), L["o.w"], L["o.b"])
+
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
     def forward(self, batch, capture_latents=True):
         """Returns (logits [n_seqs, V], latents host [L, T, H] or [L, T, 2*n_kv*D] or None)."""
-        cfg = self.cfg
+        spec = self.spec
         self._prep(batch)
         T = batch.current_tokens
-        h = F.embedding(batch.input_ids, self.embed)
+        h = self._embed(batch)
         residual = None
         lat = None
         events = []
         if capture_latents:
-            width = cfg.hidden_size if self.latent_mode == "hidden" else 2 * self.n_kv * self.d
-            lat = torch.empty(cfg.num_hidden_layers, T, width, dtype=self.dtype,
+            width = spec.hidden_size if self.latent_mode == "hidden" else 2 * self.n_kv * self.d
+            lat = torch.empty(spec.num_hidden_layers, T, width, dtype=self.dtype,
                               pin_memory=self.device.type == "cuda")
-        nq, nkv, D = self.n_q, self.n_kv, self.d
         for i, L in enumerate(self.layers):
             if residual is None:
-                x = rms_norm(h, L.ln1, cfg.rms_norm_eps)
+                x = self._norm(h, L["ln1.w"], L["ln1.b"])
                 residual = h
             else:
-                x, residual = rms_norm(h, L.ln1, cfg.rms_norm_eps, residual)
-            qkv = F.linear(x, L.qkv, L.qkv_bias).view(T, nq + 2 * nkv, D)
-            cache = self.kv_cache.get_cache(i)
-            kv_rope_scatter(qkv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, nq, nkv)
-            if capture_latents:
-                src = x if self.latent_mode == "hidden" else qkv[:, nq:].reshape(T, -1)
-                self._d2h(src, lat[i], events)
-            o = paged_attention(qkv[:, :nq], cache, batch.atoms, batch.n_atoms, batch.seq_meta, batch.block_tables, nq,
-                                nkv, self.scale, cfg.sliding_window, batch.seq_meta_host, batch.tables_host)
-            a = self._allreduce(F.linear(o.view(T, nq * D), L.o))
-            x, residual = rms_norm(a, L.ln2, cfg.rms_norm_eps, residual)
-            h = self._allreduce(self._mlp(L, x))
+                x, residual = self._norm(h, L["ln1.w"], L["ln1.b"], residual)
+            if capture_latents and self.latent_mode == "hidden":
+                self._d2h(x, lat[i], events)
+            a = self._attn(i, L, x, batch, T, capture_latents, lat, events)
+            if spec.parallel == "shared_ln":
+                h = self._allreduce(a + self._mlp(L, x))
+            elif spec.parallel == "two_ln":
+                xm = self._norm(residual, L["ln2.w"], L["ln2.b"])
+                h = self._allreduce(a + self._mlp(L, xm))
+            else:
+                x2, residual = self._norm(self._allreduce(a), L["ln2.w"], L["ln2.b"], residual)
+                h = self._allreduce(self._mlp(L, x2))
         idx = batch.last_token_idx
-        hl, _ = rms_norm(h[idx], self.norm, cfg.rms_norm_eps, residual[idx])
-        logits = F.linear(hl, self.lm_head)
+        if self.final_w is not None:
+            hl, _ = self._norm(h[idx], self.final_w, self.final_b, residual[idx])
+        else:
+            hl = h[idx] + residual[idx]
+        logits = F.linear(hl, self.lm_head, self.lm_head_b)
         if self.tp > 1:
             parts = [torch.empty_like(logits) for _ in range(self.tp)]
             dist.all_gather(parts, logits, group=self.tp_group)
@@ -196,10 +299,8 @@ class RaggedTransformer:
     @torch.no_grad()
     def restore_kv(self, batch, latents):
         """Rebuild the paged KV of ``batch``'s sequences from host latents [L, T, W] (pinned preferred)."""
-        cfg = self.cfg
         T = batch.current_tokens
-        nq, nkv, D = self.n_q, self.n_kv, self.d
-        L_ = cfg.num_hidden_layers
+        L_ = self.spec.num_hidden_layers
         if self.copy_stream is None:
             for i, L in enumerate(self.layers):
                 self._restore_layer(i, L, latents[i].to(self.device), batch, T)
@@ -236,14 +337,11 @@ class RaggedTransformer:
         nq, nkv, D = self.n_q, self.n_kv, self.d
         cache = self.kv_cache.get_cache(i)
         if self.latent_mode == "hidden":
-            # only K|V rows of the projection are needed: GEMM against the k/v slice of W_qkv
-            w = L.qkv[nq * D:]
-            bias = L.qkv_bias[nq * D:] if L.qkv_bias is not None else None
+            # only the K|V rows of the projection are needed: GEMM against the k/v slice of W_qkv
+            w = L["qkv.w"][nq * D:]
+            bias = L["qkv.b"][nq * D:] if L["qkv.b"] is not None else None
             kv = F.linear(x, w, bias).view(T, 2 * nkv, D)
-            kv_rope_scatter(kv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, 0, nkv,
-                            rotate_q=False)
         else:
-            # stored K is pre-RoPE (what the projection produced); rotation happens on the way in
-            kv = x.view(T, 2 * nkv, D).contiguous()
-            kv_rope_scatter(kv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, 0, nkv,
-                            rotate_q=False)
+            kv = x.view(T, 2 * nkv, D).contiguous()  # stored pre-RoPE: rotation happens on the way in
+        kv_rope_scatter(kv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, 0, nkv,
+                        rotate_q=False, do_rope=self.cos is not None, rotary_dim=self.rot)

@@ -11,15 +11,21 @@ from . import native
 ROWS_PER_ATOM = 128
 
 
-def kv_rope_scatter(qkv, cache, tok_seq, tok_pos, block_tables, cos, sin, n_q, n_kv, rotate_q=True, do_rope=True):
+KERNEL_HEAD_DIM = 128  # head size the HIP serving kernels are built for; other sizes take the torch path
+
+
+def kv_rope_scatter(qkv, cache, tok_seq, tok_pos, block_tables, cos, sin, n_q, n_kv, rotate_q=True, do_rope=True,
+                    rotary_dim=0):
     """qkv: [T, n_q + 2 n_kv, D]; cache: [num_blocks, block_size, 2, n_kv, D] (one layer).
 
-    RoPE at absolute positions ``tok_pos`` on q (in place, if ``rotate_q``) and k; k and v are written
+    RoPE at absolute positions ``tok_pos`` on q (in place, if ``rotate_q``) and k (the first ``rotary_dim``
+    dims only when 0 < rotary_dim < D: partial rotary of Phi / GPT-NeoX style models); k and v are written
     to ``cache[block_tables[tok_seq[t], pos // bs], pos % bs]``.
     """
     T, NH, D = qkv.shape
     bs = cache.shape[1]
-    if native.use_native(qkv):
+    partial = do_rope and 0 < rotary_dim < D
+    if native.use_native(qkv) and D == KERNEL_HEAD_DIM and not partial:
         native.check(
             native.kernels().hds_kv_rope_scatter(native.dt(qkv), qkv.data_ptr(), qkv.stride(0), cache.data_ptr(),
                                                  tok_seq.data_ptr(), tok_pos.data_ptr(), block_tables.data_ptr(),
@@ -28,16 +34,18 @@ def kv_rope_scatter(qkv, cache, tok_seq, tok_pos, block_tables, cos, sin, n_q, n
                                                  int(rotate_q), int(do_rope), native.stream()), "kv_rope_scatter")
         return
     pos = tok_pos.long()
-    half = D // 2
+    rd = rotary_dim if partial else D
+    half = rd // 2
 
     def rot(x):
         if not do_rope:
             return x
-        c = cos[pos][:, None, :]
-        s = sin[pos][:, None, :]
-        xf = x.float()
+        c = cos[pos][:, None, :half]
+        s = sin[pos][:, None, :half]
+        xf = x[..., :rd].float()
         a, b = xf[..., :half], xf[..., half:]
-        return torch.cat([a * c - b * s, b * c + a * s], -1).to(x.dtype)
+        r = torch.cat([a * c - b * s, b * c + a * s], -1).to(x.dtype)
+        return torch.cat([r, x[..., rd:]], -1) if rd < D else r
 
     if rotate_q:
         qkv[:, :n_q] = rot(qkv[:, :n_q])
@@ -66,7 +74,7 @@ def paged_attention(q, cache, atoms, n_atoms, seq_meta, block_tables, n_q, n_kv,
     """q: [T, n_q, D] (token-strided view ok). Returns o [T, n_q, D]."""
     T, _, D = q.shape
     o = torch.empty(T, n_q, D, device=q.device, dtype=q.dtype)
-    if native.use_native(q):
+    if native.use_native(q) and D == KERNEL_HEAD_DIM:
         native.check(
             native.kernels().hds_paged_attn(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(),
                                             atoms.data_ptr(), n_atoms, seq_meta.data_ptr(), block_tables.data_ptr(),
@@ -81,15 +89,15 @@ def paged_attention(q, cache, atoms, n_atoms, seq_meta, block_tables, n_q, n_kv,
         if n_new == 0:
             continue
         ctx = seen + n_new
-        pos = torch.arange(ctx)
-        blk = tables[s][pos // bs].long()
+        pos = torch.arange(ctx, device=q.device)
+        blk = torch.as_tensor(tables[s], device=q.device)[pos // bs].long()
         kk = cache[blk, pos % bs, 0].float()  # [ctx, n_kv, D]
         vv = cache[blk, pos % bs, 1].float()
         qq = q[q0:q0 + n_new].float()  # [n_new, n_q, D]
         kk = kk.repeat_interleave(G, 1)
         vv = vv.repeat_interleave(G, 1)
         sc = torch.einsum("thd,chd->htc", qq, kk) * scale
-        qpos = seen + torch.arange(n_new)
+        qpos = seen + torch.arange(n_new, device=q.device)
         mask = pos[None, :] > qpos[:, None]
         if window:
             mask |= pos[None, :] <= qpos[:, None] - window
