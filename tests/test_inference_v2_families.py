@@ -16,15 +16,15 @@ from hcache_deepspeed_amd.inference.v2 import build_engine_from_hf_model  # noqa
 V = 151
 
 
-def _base(**kw):
-    d = dict(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
-             num_key_value_heads=2, max_position_embeddings=256)
-    d.update(kw)
-    return d
-
-
-def _families():
+def _families(H=64):
     t = transformers
+
+    def _base(**kw):
+        d = dict(vocab_size=V, hidden_size=H, intermediate_size=2 * H, num_hidden_layers=2, num_attention_heads=4,
+                 num_key_value_heads=2, max_position_embeddings=256)
+        d.update(kw)
+        return d
+
     return {
         "llama": lambda: t.LlamaForCausalLM(t.LlamaConfig(**_base())),
         "mistral": lambda: t.MistralForCausalLM(t.MistralConfig(**_base(sliding_window=None))),
@@ -32,21 +32,21 @@ def _families():
                                                                           num_experts_per_tok=2))),
         "qwen2": lambda: t.Qwen2ForCausalLM(t.Qwen2Config(**_base())),
         "qwen2_moe": lambda: t.Qwen2MoeForCausalLM(t.Qwen2MoeConfig(**_base(
-            num_experts=4, num_experts_per_tok=2, moe_intermediate_size=48, shared_expert_intermediate_size=96,
+            num_experts=4, num_experts_per_tok=2, moe_intermediate_size=H // 4 * 3, shared_expert_intermediate_size=H * 3 // 2,
             decoder_sparse_step=1, mlp_only_layers=[]))),
         "phi3": lambda: t.Phi3ForCausalLM(t.Phi3Config(**_base(pad_token_id=0))),
         "phi": lambda: t.PhiForCausalLM(t.PhiConfig(**_base(num_key_value_heads=4, partial_rotary_factor=0.5))),
-        "falcon": lambda: t.FalconForCausalLM(t.FalconConfig(vocab_size=V, hidden_size=64, num_hidden_layers=2,
+        "falcon": lambda: t.FalconForCausalLM(t.FalconConfig(vocab_size=V, hidden_size=H, num_hidden_layers=2,
                                                              num_attention_heads=4, multi_query=True,
                                                              parallel_attn=True, bias=False, alibi=False,
                                                              new_decoder_architecture=False)),
-        "falcon_new": lambda: t.FalconForCausalLM(t.FalconConfig(vocab_size=V, hidden_size=64, num_hidden_layers=2,
+        "falcon_new": lambda: t.FalconForCausalLM(t.FalconConfig(vocab_size=V, hidden_size=H, num_hidden_layers=2,
                                                                  num_attention_heads=4, num_kv_heads=2,
                                                                  new_decoder_architecture=True, bias=False,
                                                                  alibi=False)),
-        "opt": lambda: t.OPTForCausalLM(t.OPTConfig(vocab_size=V, hidden_size=64, num_hidden_layers=2,
-                                                    num_attention_heads=4, ffn_dim=128, max_position_embeddings=256,
-                                                    word_embed_proj_dim=64)),
+        "opt": lambda: t.OPTForCausalLM(t.OPTConfig(vocab_size=V, hidden_size=H, num_hidden_layers=2,
+                                                    num_attention_heads=4, ffn_dim=2 * H, max_position_embeddings=256,
+                                                    word_embed_proj_dim=H)),
     }
 
 
@@ -109,3 +109,30 @@ def test_hf_checkpoint_dir_and_serialize_roundtrip(family, tmp_path):
     eng2 = build_engine_from_ds_checkpoint(str(tmp_path / "ds"), cfg, device=torch.device("cpu"), num_kv_blocks=32)
     lg2, _ = eng2.put([1], [ids])
     assert torch.allclose(lg2[0], lg[0], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("family", ["llama", "mixtral", "qwen2_moe", "phi3", "phi", "falcon_new", "opt"])
+def test_family_parity_gpu(family):
+    """HIP paged attention / fused RoPE+KV-scatter path (head_dim 128) on every block structure."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    m = _families(H=512)[family]()
+    torch.manual_seed(0)
+    m = _randomize(m.float().eval())
+    eng = build_engine_from_hf_model(m, {"dtype": "bf16", "latent_mode": "kv",
+                                         "state_manager": {"max_context": 256, "kv_block_size": 64}},
+                                     device=torch.device("cuda"), num_kv_blocks=32)
+    g = torch.Generator().manual_seed(1)
+    p1 = torch.randint(0, V, (70, ), generator=g)
+    cont = torch.randint(0, V, (3, ), generator=g)
+    with torch.no_grad():
+        ref = m(torch.cat([p1, cont])[None]).logits[0].float()
+    logits, lats = eng.put([1], [p1])
+    tol = 6e-2
+    assert torch.allclose(logits[0].float().cpu(), ref[69], atol=tol, rtol=tol)
+    eng.evict(1)
+    eng.restore_kv([1], [p1], [lats[0]])
+    for j in range(cont.numel()):
+        lg, _ = eng.put([1], [cont[j:j + 1]], capture_latents=False)
+        assert torch.allclose(lg[0].float().cpu(), ref[70 + j], atol=tol, rtol=tol), (family, j)
