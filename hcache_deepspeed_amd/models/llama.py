@@ -146,9 +146,20 @@ class LlamaAttention(nn.Module):
         self.layer_idx = layer_idx
 
     sp_group = None  # Ulysses sequence-parallel group (parallel/ulysses.enable_sequence_parallel)
+    fpdt = None  # FPDT settings (parallel/fpdt.enable_fpdt): chunked, optionally host-offloaded attention
 
     def forward(self, x, cos, sin, seq_len, cu_seqlens=None, pos_ids=None):
         T = x.shape[0]
+        if self.fpdt is not None:
+            from ..parallel.fpdt import fpdt_attention
+            from .. import comm as dist
+            f = self.fpdt
+            assert cu_seqlens is None and not self.cfg.sliding_window, "FPDT: dense causal batches only"
+            P = dist.get_world_size(f["group"]) if f["group"] is not None else 1
+            nc = max(1, seq_len * P // f["chunk_size"])
+            o = fpdt_attention(x, self.qkv_proj.weight, self.qkv_proj.bias, cos, sin, self.n_q, self.n_kv, self.d,
+                               f["group"], T // seq_len, nc, offload=f["offload"])
+            return self.o_proj(o)
         qkv = self.qkv_proj(x).view(T, self.n_q + 2 * self.n_kv, self.d)
         if self.sp_group is not None:
             from ..parallel.ulysses import ulysses_out, ulysses_qkv
@@ -175,7 +186,12 @@ class LlamaMLP(nn.Module):
                                  std=std / math.sqrt(2 * cfg.num_hidden_layers))
         self.act = cfg.hidden_act
 
+    fpdt_chunks = 0  # >1: sequence-chunked MLP with per-chunk recompute (parallel/fpdt.enable_fpdt)
+
     def forward(self, x):
+        if self.fpdt_chunks > 1:
+            from ..parallel.fpdt import fpdt_gated_ffn
+            return fpdt_gated_ffn(x, self.gate_up_proj.weight, self.down_proj.weight, self.fpdt_chunks, self.act)
         return self.down_proj(glu(self.gate_up_proj(x), self.act))
 
 

@@ -266,3 +266,74 @@ def qkv_attention(qkv, n_q, n_kv, cos=None, sin=None, seq_len=None, causal=True,
     _count_attn_flops(T, n_q, D, int(seq_len or T), causal, cu_seqlens)
     return _QKVAttnFn.apply(qkv, n_q, n_kv, cos, sin, int(seq_len or T), bool(causal), float(scale), cu_seqlens,
                             pos_ids, int(window or 0))
+
+
+# ---------------------------------------------------------------------------------------------
+# Block primitives for chunked / blockwise attention (FPDT, ring-style merges). No autograd: the
+# caller owns the global (o, lse) and calls the block backward once per (query-chunk, key-chunk) pair.
+def _ref_block_bwd(q, k, v, o, lse, do, causal, scale, seq_len):
+    """fp32 blockwise backward against an externally supplied (final) o / lse: P = exp(qk^T*scale - lse)."""
+    T, Hq, D = q.shape
+    Hkv = k.shape[1]
+    G = Hq // Hkv
+    B = T // seq_len
+    L = seq_len
+
+    def bh(t):  # [T, H, D] -> [B, H, L, D]
+        return t.float().view(B, L, t.shape[1], D).permute(0, 2, 1, 3)
+
+    qf, kf, vf, of, dof = bh(q), bh(k).repeat_interleave(G, 1), bh(v).repeat_interleave(G, 1), bh(o), bh(do)
+    lsef = lse.float().view(Hq, B, L).permute(1, 0, 2)[..., None]  # [B, H, L, 1]
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        i = torch.arange(L, device=q.device)
+        s = s.masked_fill(i[None, :] > i[:, None], float("-inf"))
+    p = torch.exp(s - lsef)
+    dv = torch.matmul(p.transpose(-1, -2), dof)
+    dp = torch.matmul(dof, vf.transpose(-1, -2))
+    delta = (dof * of).sum(-1, keepdim=True)
+    ds = p * (dp - delta) * scale
+    dq = torch.matmul(ds, kf)
+    dk = torch.matmul(ds.transpose(-1, -2), qf)
+
+    def tok(t, H):  # [B, H, L, D] -> [T, H, D]
+        return t.permute(0, 2, 1, 3).reshape(T, H, D)
+
+    dk = dk.view(B, Hkv, G, L, D).sum(2)
+    dv = dv.view(B, Hkv, G, L, D).sum(2)
+    return tok(dq, Hq), tok(dk, Hkv), tok(dv, Hkv)
+
+
+def attn_block_fwd(q, k, v, causal, scale, seq_len):
+    """One (query block, key block) FlashAttention forward on [T, H, D] tensors holding T/seq_len equal-length
+    sequences; returns (o [T, Hq, D] in q.dtype, lse [Hq, T] fp32)."""
+    T, Hq, D = q.shape
+    if native_supported(q):
+        o = torch.empty(T, Hq, D, device=q.device, dtype=q.dtype)
+        lse = torch.empty(Hq, T, device=q.device, dtype=torch.float32)
+        _native_fwd(q, k, v, o, lse, causal, scale, None, T // seq_len, seq_len, seq_len, 0)
+        return o, lse
+    return _ref_attention(q, k, v, causal, scale, None, seq_len, 0)
+
+
+def attn_block_bwd(q, k, v, o, lse, do, causal, scale, seq_len):
+    """Gradient contribution of one (query block, key block) pair given the FINAL merged o / lse of the query
+    block (exact blockwise decomposition). Returns (dq, dk, dv); bf16 on the HIP path, fp32 on the reference."""
+    T = q.shape[0]
+    if native_supported(q):
+        dq = torch.empty(q.shape, device=q.device, dtype=q.dtype)
+        dk = torch.empty(k.shape, device=k.device, dtype=k.dtype)
+        dv = torch.empty(v.shape, device=v.device, dtype=v.dtype)
+        _native_bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, None, T // seq_len, seq_len, seq_len, 0)
+        return dq, dk, dv
+    return _ref_block_bwd(q, k, v, o, lse, do, causal, scale, seq_len)
+
+
+def merge_attn_out(o, lse, o_blk, lse_blk):
+    """Online-softmax merge of two partial attention results (fp32 o [T, H, D], lse [H, T])."""
+    if o is None:
+        return o_blk.float(), lse_blk.clone()
+    new = torch.logaddexp(lse, lse_blk)
+    a = torch.exp(lse - new).t()[..., None]
+    b = torch.exp(lse_blk - new).t()[..., None]
+    return o * a + o_blk.float() * b, new
