@@ -160,6 +160,23 @@ class DeepSpeedEngine(nn.Module):
             from .progressive_layer_drop import ProgressiveLayerDrop
             self.progressive_layer_drop = ProgressiveLayerDrop(cfg.pld_config.get("theta", 0.5),
                                                                cfg.pld_config.get("gamma", 0.001))
+        # compression training (reference engine.py:333-337 compression_scheduler + MoQ quantizer)
+        self.compression_scheduler = None
+        self._moq = None
+        if "compression_training" in cfg.raw:
+            from ..compression import compression_scheduler, get_compression_config
+            cc = get_compression_config(cfg.raw)
+            if any(cc[t]["shared_parameters"]["enabled"] for t in cc if t != "layer_reduction"):
+                self.compression_scheduler = compression_scheduler(self.module, cc)
+                self.compression_scheduler.step(step_zero_check=True)
+                wq = cc["weight_quantization"]["shared_parameters"]
+                if wq["enabled"] and not wq["quantize_weight_in_forward"]:
+                    from .quantize import Quantizer
+                    self._moq = Quantizer(q_groups=wq["quantize_groups"],
+                                          q_mixed_fp16=wq["fp16_mixed_quantize"]["enabled"],
+                                          q_change_ratio=wq["fp16_mixed_quantize"]["quantize_change_ratio"],
+                                          q_type=0 if wq["quantization_type"] == "symmetric" else 1,
+                                          q_rounding=0 if wq["rounding"] == "nearest" else 1)
         self._activation_cache = None
         if cfg.mi355x.host_act_cache.enabled:
             from ..offload.activation_cache import HostActivationCache
@@ -402,6 +419,11 @@ class DeepSpeedEngine(nn.Module):
                 self.lr_scheduler.step(**(lr_kwargs or {}))
             self.global_steps += 1
             self.global_samples += self.train_batch_size()
+            if self.compression_scheduler is not None:
+                self.compression_scheduler.step()
+                if self._moq is not None and self.compression_scheduler.weight_quantization_enabled:
+                    qparams = [p for p in self.module.parameters() if getattr(p, "start_bits", None)]
+                    self._moq.quantize([qparams], overflow=ok is False)
             if self.progressive_layer_drop is not None:
                 self.progressive_layer_drop.update_state(self.global_steps)
             if self._config.autotuning.get("enabled", False):

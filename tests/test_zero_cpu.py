@@ -133,8 +133,10 @@ def test_flops_profiler_counts_gemms_and_attention():
     from hcache_deepspeed_amd.profiling.flops_profiler import FlopsProfiler, get_model_profile
     torch.manual_seed(0)
     cfg = tiny(**TINY)
-    m = LlamaForCausalLM(cfg)
+    m = LlamaForCausalLM(cfg).eval()  # get_model_profile below profiles in eval mode too
     x = torch.randint(0, 97, (2, 12))
+    with torch.no_grad():
+        m(x)  # warm-up: the first forward also builds the RoPE tables (get_model_profile warms up too)
     prof = FlopsProfiler(m)
     prof.start_profile()
     with torch.no_grad():
