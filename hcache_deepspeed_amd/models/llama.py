@@ -240,6 +240,12 @@ class LlamaModel(nn.Module):
         h = self.embed_tokens(ids)
         sp = getattr(self, "_hds_sp_size", 1)
         cos, sin = self.rope(h.device, S * sp)
+        if (getattr(self, "_domino_group", None) is not None and input_ids.dim() == 2 and B % 2 == 0
+                and cu_seqlens is None and layer_hook is None and not self.gradient_checkpointing):
+            from ..parallel.domino import domino_decoder_forward
+            h, residual = domino_decoder_forward(self, h, cos, sin, S, B)
+            h, _ = self.norm(h, residual)
+            return h
         residual = None
         for i, layer in enumerate(self.layers):
             if layer_hook is not None:

@@ -111,3 +111,31 @@ def _ulysses_a2a(rank, world):
 
 def test_distributed_attention_api():
     run_distributed(_ulysses_a2a, 2)
+
+
+def _domino(rank, world):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.parallel.domino import enable_domino
+    g = torch.Generator().manual_seed(11)
+    batches = [torch.randint(0, 97, (4, 12), generator=g) for _ in range(3)]
+    ref_losses, _ = _ref_losses(batches, 3)
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(**TINY))
+    cfg = {"train_micro_batch_size_per_gpu": 4, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
+           "zero_optimization": {"stage": 1}, "tensor_parallel": {"autotp_size": 2}}
+    eng, _, _, _ = ds.initialize(model=m, config=cfg)
+    enable_domino(m)
+    assert m.model._domino_group is not None
+    losses = []
+    for b in batches:
+        loss = eng(b, labels=b)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss))
+    assert losses == pytest.approx(ref_losses, rel=1e-4, abs=1e-4), (losses, ref_losses)
+
+
+def test_domino_tp_matches_single():
+    """Domino half-batch overlap of the TP all-reduces reproduces single-process training."""
+    run_distributed(_domino, 2)
