@@ -1,0 +1,103 @@
+"""Evoformer attention with pair bias (AlphaFold / OpenFold MSA row- and triangle-attention).
+
+Reference parity: ops/deepspeed4science/evoformer_attn.py (``DS4Sci_EvoformerAttention(Q, K, V, biases)`` :88,
+``EvoformerFusedAttention`` autograd :59 with bias gradients) backed there by CUTLASS memory-efficient attention
+(csrc/deepspeed4science/evoformer_attn, 14.9k LoC).
+
+Shapes: Q/K/V ``[B, N, L, H, D]``; ``bias1 = [B, N, 1, 1, L]`` (MSA mask, broadcast over heads and queries);
+``bias2 = [B, 1, H, L, L]`` (pair bias, broadcast over the N rows). Output ``[B, N, L, H, D]``.
+
+Implementation: memory-efficient flash-style decomposition -- the forward keeps only the fp32 log-sum-exp per
+query, the backward recomputes the probabilities one query chunk at a time, so peak memory is O(chunk x L)
+instead of O(L^2) per (B, N, H). The per-chunk products run as batched GEMMs on the matrix cores; head_dim is
+arbitrary (Evoformer uses 16-64, below the 128 the FlashAttention HIP kernel is tiled for). Bias gradients
+are reduced exactly as the reference (dB2 summed over N, dB1 over heads and queries).
+"""
+import math
+
+import torch
+
+_CHUNK_BYTES = 256 << 20
+
+
+def _chunk_rows(B, N, H, L):
+    per_row = max(1, B * N * H * L * 4)
+    return max(16, min(L, _CHUNK_BYTES // per_row))
+
+
+def _scores(q, k, b1, b2, i0, i1, scale):
+    s = torch.matmul(q[..., i0:i1, :], k.transpose(-1, -2)).float() * scale  # [B, N, H, c, L]
+    if b1 is not None:
+        s = s + b1.float()  # [B, N, 1, 1, L]
+    if b2 is not None:
+        s = s + b2[..., i0:i1, :].float()  # [B, 1, H, c, L]
+    return s
+
+
+class EvoformerFusedAttention(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, q, k, v, bias1=None, bias2=None):
+        # [B, N, L, H, D] -> [B, N, H, L, D]
+        qh, kh, vh = (x.transpose(-2, -3) for x in (q, k, v))
+        B, N, H, L, D = qh.shape
+        scale = 1.0 / math.sqrt(D)
+        o = torch.empty(qh.shape, dtype=q.dtype, device=q.device)
+        lse = torch.empty(B, N, H, L, dtype=torch.float32, device=q.device)
+        c = _chunk_rows(B, N, H, L)
+        for i0 in range(0, L, c):
+            i1 = min(L, i0 + c)
+            s = _scores(qh, kh, bias1, bias2, i0, i1, scale)
+            m = torch.logsumexp(s, -1)
+            lse[..., i0:i1] = m
+            p = torch.exp(s - m[..., None])
+            o[..., i0:i1, :] = torch.matmul(p.to(v.dtype), vh)
+        ctx.save_for_backward(qh, kh, vh, o, lse, bias1, bias2)
+        ctx.scale = scale
+        return o.transpose(-2, -3)
+
+    @staticmethod
+    def backward(ctx, do):
+        qh, kh, vh, o, lse, bias1, bias2 = ctx.saved_tensors
+        scale = ctx.scale
+        B, N, H, L, D = qh.shape
+        doh = do.transpose(-2, -3)
+        delta = (doh.float() * o.float()).sum(-1)  # [B, N, H, L]
+        dq = torch.empty(qh.shape, dtype=torch.float32, device=qh.device)
+        dk = torch.zeros(kh.shape, dtype=torch.float32, device=qh.device)
+        dv = torch.zeros(vh.shape, dtype=torch.float32, device=qh.device)
+        want_b1 = bias1 is not None and ctx.needs_input_grad[3]
+        want_b2 = bias2 is not None and ctx.needs_input_grad[4]
+        db1 = torch.zeros(bias1.shape, dtype=torch.float32, device=qh.device) if want_b1 else None
+        db2 = torch.zeros(bias2.shape, dtype=torch.float32, device=qh.device) if want_b2 else None
+        c = _chunk_rows(B, N, H, L)
+        for i0 in range(0, L, c):
+            i1 = min(L, i0 + c)
+            p = torch.exp(_scores(qh, kh, bias1, bias2, i0, i1, scale) - lse[..., i0:i1, None])  # [B,N,H,c,L]
+            dob = doh[..., i0:i1, :]
+            dv += torch.matmul(p.transpose(-1, -2).to(vh.dtype), dob).float()
+            dp = torch.matmul(dob, vh.transpose(-1, -2)).float()
+            ds = p * (dp - delta[..., i0:i1, None])  # gradient wrt the biased scores
+            if want_b2:
+                db2[..., i0:i1, :] += ds.sum(1, keepdim=True)
+            if want_b1:
+                db1 += ds.sum((2, 3), keepdim=True)
+            dsq = ds.to(qh.dtype)
+            dq[..., i0:i1, :] = torch.matmul(dsq, kh).float() * scale
+            dk += torch.matmul(dsq.transpose(-1, -2), qh[..., i0:i1, :]).float() * scale
+        out = [x.to(qh.dtype).transpose(-2, -3) for x in (dq, dk, dv)]
+        return (out[0], out[1], out[2], db1.to(bias1.dtype) if want_b1 else None,
+                db2.to(bias2.dtype) if want_b2 else None)
+
+
+def DS4Sci_EvoformerAttention(Q, K, V, biases):
+    """Q/K/V ``[B, N, L, H, D]``; ``biases``: up to two of ``[B, N, 1, 1, L]`` and ``[B, 1, H, L, L]``."""
+    biases = list(biases)
+    assert len(biases) <= 2
+    while len(biases) < 2:
+        biases.append(None)
+    if biases[0] is not None:
+        assert biases[0].shape == (Q.shape[0], Q.shape[1], 1, 1, Q.shape[2]), "bias1 shape is incorrect"
+    if biases[1] is not None:
+        assert biases[1].shape == (Q.shape[0], 1, Q.shape[3], Q.shape[2], Q.shape[2]), "bias2 shape is incorrect"
+    return EvoformerFusedAttention.apply(Q, K, V, biases[0], biases[1])
