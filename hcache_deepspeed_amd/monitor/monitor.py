@@ -85,6 +85,33 @@ class WandbMonitor(Monitor):
             self.wandb.log({name: value}, step=step)
 
 
+class CometMonitor(Monitor):
+    """Comet ML experiment logging (reference monitor/comet.py); gated on ``comet_ml`` being importable."""
+
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        self.experiment = None
+        self.samples_log_interval = int(cfg.get("samples_log_interval", 100))
+        if self.enabled:
+            try:
+                import comet_ml
+                kw = {k: cfg.get(k) for k in ("api_key", "project", "workspace", "experiment_key", "mode", "online")
+                      if cfg.get(k) is not None}
+                self.experiment = comet_ml.start(**kw)
+                if cfg.get("experiment_name"):
+                    self.experiment.set_name(cfg["experiment_name"])
+            except Exception:
+                warning_once("comet monitor requested but comet_ml is not importable; disabled")
+                self.enabled = False
+
+    def write_events(self, events):
+        if self.experiment is None:
+            return
+        for name, value, step in events:
+            if step % self.samples_log_interval == 0:
+                self.experiment.log_metric(name, value, step=step)
+
+
 class MonitorMaster:
 
     def __init__(self, monitor_config):
@@ -96,6 +123,8 @@ class MonitorMaster:
             self.monitors.append(TensorBoardMonitor(monitor_config["tensorboard"]))
         if (monitor_config.get("wandb") or {}).get("enabled"):
             self.monitors.append(WandbMonitor(monitor_config["wandb"]))
+        if (monitor_config.get("comet") or {}).get("enabled"):
+            self.monitors.append(CometMonitor(monitor_config["comet"]))
         self.enabled = any(m.enabled for m in self.monitors)
 
     def write_events(self, events):
