@@ -1,6 +1,8 @@
-"""FP8-quantized frozen weights (reference linear/quantization.py ``QuantizedParameter`` :18 / ``QuantizedLinear``
-:129). The weight is stored as OCP e4m3 (or e5m2) bytes + fp32 group scales produced by the gfx950 conversion
-kernels (ops/quantizer.quantize_fp8) and dequantized to the compute dtype for each forward."""
+"""Quantized frozen weights (reference linear/quantization.py ``QuantizedParameter`` :18 / ``QuantizedLinear``
+:129). ``q_bits=8``: OCP e4m3 (or e5m2) bytes + fp32 group scales from the gfx950 conversion instructions
+(ops/quantizer.quantize_fp8). ``q_bits=6`` / ``12``: packed FP6 (e3m2 / e2m3) or FP12 minifloats (csrc/kernels/
+fpq.hip). The weight is dequantized to the compute dtype for each forward; FP6 linears with decode-sized inputs
+skip that and run the fused 6-bit GEMV (ops/quantizer.fp6_linear)."""
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -25,6 +27,10 @@ class QuantizedParameter(nn.Parameter):
     def fmt(self):
         return "e4m3" if self.quantization_config.mantissa_bits == 3 else "e5m2"
 
+    @property
+    def q_bits(self):
+        return self.quantization_config.q_bits
+
     def _ensure_quantized(self, tensor):
         if tensor.numel() == 0:
             self.q_data, self.q_scales = tensor, None
@@ -34,11 +40,18 @@ class QuantizedParameter(nn.Parameter):
         if flat.numel() % gs:
             gs = flat.numel()
         self.group_size = gs
-        self.q_data, self.q_scales = Q.quantize_fp8(flat.contiguous(), gs, self.fmt)
+        if self.q_bits == 8:
+            self.q_data, self.q_scales = Q.quantize_fp8(flat.contiguous(), gs, self.fmt)
+        else:
+            self.q_data, self.q_scales = Q.quantize_minifloat(flat.contiguous(), gs, self.q_bits,
+                                                              self.quantization_config.mantissa_bits)
 
     def dequantized(self):
-        return Q.dequantize_fp8(self.q_data, self.q_scales, self.group_size, self.fmt,
-                                self.orig_dtype).view(self.orig_shape)
+        if self.q_bits == 8:
+            return Q.dequantize_fp8(self.q_data, self.q_scales, self.group_size, self.fmt,
+                                    self.orig_dtype).view(self.orig_shape)
+        return Q.dequantize_minifloat(self.q_data, self.q_scales, self.group_size, self.q_bits,
+                                      self.quantization_config.mantissa_bits, self.orig_dtype).view(self.orig_shape)
 
     def offload(self, revert=False):
         dev = "cuda" if revert and torch.cuda.is_available() else "cpu"
@@ -67,4 +80,9 @@ class QuantizedLinear(nn.Linear):
         self.weight = QuantizedParameter(self.weight.data, quantization_config=quantization_config, dtype=dtype)
 
     def forward(self, x):
-        return F.linear(x, self.weight.dequantized().to(x.dtype), self.bias)
+        w = self.weight
+        if w.q_bits == 6 and len(w.orig_shape) == 2 and w.orig_shape[1] % w.group_size == 0:
+            y = Q.fp6_linear(x, w.q_data, w.q_scales, w.orig_shape[0], w.orig_shape[1], w.group_size,
+                             w.quantization_config.mantissa_bits)
+            return y + self.bias if self.bias is not None else y
+        return F.linear(x, w.dequantized().to(x.dtype), self.bias)

@@ -53,6 +53,9 @@ _KERNEL_SIGS = {
     "hds_quant_fp8": "i" + "ppp" + "l" + "ii" + "s",
     "hds_dequant_fp8": "i" + "ppp" + "l" + "ii" + "s",
     "hds_dequant_reduce": "i" + "ppp" + "i" + "l" + "iii" + "s",
+    "hds_quant_minifloat": "i" + "ppp" + "l" + "iiiii" + "s",
+    "hds_dequant_minifloat": "i" + "ppp" + "l" + "iii" + "s",
+    "hds_fp6_gemv": "pppp" + "iiiiii" + "s",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}

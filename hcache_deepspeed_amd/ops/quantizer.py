@@ -171,7 +171,8 @@ def dequantize_fp8(q, scales, group_size=512, fmt="e4m3", dtype=torch.bfloat16, 
 
 
 class FP_Quantize:
-    """Reference ops/fp_quantizer/quantize.py:43 API (q_bits 8 -> FP8; mantissa 3 -> e4m3, 2 -> e5m2)."""
+    """Reference ops/fp_quantizer/quantize.py:43 API: q_bits 8 (mantissa 3 -> e4m3, 2 -> e5m2), 6 (e3m2 / e2m3)
+    or 12 (e4m7); ``stochastic_mode`` rounds stochastically (minifloat kernel)."""
 
     def __init__(self, group_size=512):
         self.group_size = group_size
@@ -181,17 +182,28 @@ class FP_Quantize:
         self.fmt = "e4m3"
 
     def quantize(self, input, q_bits=8, q_mantisa_bits=3, stochastic_mode=False, return_meta_tensor=False):
-        assert q_bits == 8, "only 8-bit FP formats are supported on gfx950 here (FP6/FP12: not implemented)"
-        self.fmt = "e4m3" if q_mantisa_bits == 3 else "e5m2"
+        """FP8 (OCP e4m3 / e5m2 via the gfx950 cvt instructions) or FP6 / FP12 minifloats (fpq.hip)."""
+        self.q_bits, self.q_mantisa_bits = q_bits, q_mantisa_bits
         self.orig_dtype, self.orig_shape = input.dtype, input.shape
-        q, s = quantize_fp8(input.reshape(-1), self.group_size, self.fmt)
+        if q_bits == 8 and not stochastic_mode:
+            self.fmt = "e4m3" if q_mantisa_bits == 3 else "e5m2"
+            q, s = quantize_fp8(input.reshape(-1), self.group_size, self.fmt)
+        else:
+            q, s = quantize_minifloat(input.reshape(-1), self.group_size, q_bits, q_mantisa_bits,
+                                      stochastic=stochastic_mode, seed=torch.randint(0, 2**31 - 1, (1, )).item())
+            self.fmt = f"mini{q_bits}m{q_mantisa_bits}"
         self.scale = s
         return (q, s) if return_meta_tensor else q
 
+    def _deq(self, q, s, q_bits, q_mantisa_bits):
+        if q_bits == 8 and not getattr(self, "fmt", "e4m3").startswith("mini"):
+            return dequantize_fp8(q, s, self.group_size, "e4m3" if q_mantisa_bits == 3 else "e5m2",
+                                  self.orig_dtype or torch.bfloat16)
+        return dequantize_minifloat(q, s, self.group_size, q_bits, q_mantisa_bits, self.orig_dtype or torch.bfloat16)
+
     def dequantize(self, input_q, fp_out=None, q_bits=8, q_mantisa_bits=3, scale=None):
-        fmt = "e4m3" if q_mantisa_bits == 3 else "e5m2"
         s = scale if scale is not None else self.scale
-        y = dequantize_fp8(input_q.reshape(-1), s, self.group_size, fmt, self.orig_dtype or torch.bfloat16)
+        y = self._deq(input_q.reshape(-1), s, q_bits, q_mantisa_bits)
         y = y.view(self.orig_shape) if self.orig_shape is not None and y.numel() == _numel(self.orig_shape) else y
         if fp_out is not None:
             fp_out.copy_(y.view_as(fp_out))
@@ -200,13 +212,11 @@ class FP_Quantize:
 
     def selective_dequantize(self, input_q, indexes, fp_out=None, q_bits=8, q_mantisa_bits=3, scale=None):
         """Dequantize only rows ``indexes`` of a [rows, cols] quantized matrix (cols multiple of group_size)."""
-        fmt = "e4m3" if q_mantisa_bits == 3 else "e5m2"
         s = scale if scale is not None else self.scale
-        rows = self.orig_shape[0] if (input_q.dim() == 1 and self.orig_shape is not None) else input_q.shape[0]
+        rows = self.orig_shape[0] if self.orig_shape is not None else input_q.shape[0]
         qr = input_q.reshape(rows, -1)[indexes]
         sr = s.reshape(rows, -1)[indexes]
-        y = dequantize_fp8(qr.reshape(-1), sr.reshape(-1), self.group_size, fmt, self.orig_dtype or torch.bfloat16)
-        y = y.view(len(indexes), -1)
+        y = self._deq(qr.reshape(-1), sr.reshape(-1), q_bits, q_mantisa_bits).view(len(indexes), -1)
         if fp_out is not None:
             fp_out.copy_(y.view_as(fp_out))
             return fp_out
@@ -230,3 +240,135 @@ class Quantizer:
 
 def ds_quantizer(x, groups=1, bits=8, sr=False, asym=False):
     return Quantizer()(x, groups, bits, sr, asym)
+
+
+# ----------------------------------------------------------------------------------------
+# FP6 / FP12 (and generic E/M) minifloat group quantization with bit packing (csrc/kernels/fpq.hip)
+# ----------------------------------------------------------------------------------------
+def _mini_fmt(q_bits, mantissa_bits):
+    ebits = q_bits - 1 - mantissa_bits
+    assert q_bits in (6, 8, 12) and ebits >= 2 and mantissa_bits >= 1, f"unsupported FP{q_bits} e{ebits}m{mantissa_bits}"
+    bias = 2**(ebits - 1) - 1
+    maxval = (2.0 - 2.0**-mantissa_bits) * 2.0**((2**ebits - 1) - bias)
+    return ebits, bias, maxval
+
+
+def _ref_encode(x, q_bits, mbits, stochastic=False, gen=None):
+    """fp32 values (already scaled into range) -> integer codes sign|exp|mant (saturating, no inf/nan)."""
+    ebits, bias, maxval = _mini_fmt(q_bits, mbits)
+    sign = (x < 0).to(torch.int32)
+    a = x.abs().clamp(max=maxval)
+    _, k = torch.frexp(a)
+    e = k.to(torch.int32) - 1
+    emin = 1 - bias
+    msc = 2.0**mbits
+    u = torch.rand(a.shape, generator=gen) if stochastic else None
+    rnd = (lambda t: torch.floor(t + u)) if stochastic else torch.round  # torch.round = half-to-even
+    sub = e < emin
+    mf_sub = torch.ldexp(a, torch.tensor(mbits - emin, dtype=torch.int32))
+    mf_nrm = (torch.ldexp(a, -e) - 1.0) * msc
+    m = torch.where(sub, rnd(mf_sub), rnd(mf_nrm))
+    ef = torch.where(sub, torch.zeros_like(e), e + bias)
+    carry = m >= msc
+    ef = torch.where(carry, ef + 1, ef)
+    m = torch.where(carry, torch.zeros_like(m), m)
+    sat = ef > (2**ebits - 1)
+    ef = torch.where(sat, torch.full_like(ef, 2**ebits - 1), ef)
+    m = torch.where(sat, torch.full_like(m, msc - 1), m)
+    code = (sign << (ebits + mbits)) | (ef << mbits) | m.to(torch.int32)
+    return torch.where(a > 0, code, sign << (ebits + mbits))
+
+
+def _ref_decode(code, q_bits, mbits):
+    ebits, bias, _ = _mini_fmt(q_bits, mbits)
+    code = code.to(torch.int32)
+    mant = (code & (2**mbits - 1)).float()
+    ef = (code >> mbits) & (2**ebits - 1)
+    neg = ((code >> (ebits + mbits)) & 1).bool()
+    sub = torch.ldexp(mant, torch.tensor(1 - bias - mbits, dtype=torch.int32))
+    nrm = torch.ldexp(1.0 + mant / 2**mbits, ef - bias)
+    v = torch.where(ef == 0, sub, nrm)
+    return torch.where(neg, -v, v)
+
+
+def _pack(codes, bits):
+    c = codes.reshape(-1, 4).to(torch.int64)
+    if bits == 8:
+        return c.to(torch.uint8).reshape(-1)
+    if bits == 6:
+        w = c[:, 0] | (c[:, 1] << 6) | (c[:, 2] << 12) | (c[:, 3] << 18)
+        return torch.stack([w & 255, (w >> 8) & 255, (w >> 16) & 255], 1).to(torch.uint8).reshape(-1)
+    w0, w1 = c[:, 0] | (c[:, 1] << 12), c[:, 2] | (c[:, 3] << 12)
+    return torch.stack([w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255, w1 & 255, (w1 >> 8) & 255, (w1 >> 16) & 255],
+                       1).to(torch.uint8).reshape(-1)
+
+
+def _unpack(q, bits):
+    b = q.to(torch.int64)
+    if bits == 8:
+        return b
+    if bits == 6:
+        b = b.reshape(-1, 3)
+        w = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+        return torch.stack([w & 63, (w >> 6) & 63, (w >> 12) & 63, (w >> 18) & 63], 1).reshape(-1)
+    b = b.reshape(-1, 6)
+    w0, w1 = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16), b[:, 3] | (b[:, 4] << 8) | (b[:, 5] << 16)
+    return torch.stack([w0 & 4095, w0 >> 12, w1 & 4095, w1 >> 12], 1).reshape(-1)
+
+
+def quantize_minifloat(x, group_size=512, q_bits=6, mantissa_bits=2, stochastic=False, seed=0):
+    """Returns (packed uint8 [numel * q_bits / 8], scales fp32 [groups]). FP6 e3m2 by default."""
+    x = x.contiguous()
+    ng = _groups(x, group_size)
+    ebits, _, maxval = _mini_fmt(q_bits, mantissa_bits)
+    assert group_size % 4 == 0
+    if native.use_native(x):
+        q = torch.empty(x.numel() * q_bits // 8, dtype=torch.uint8, device=x.device)
+        scales = torch.empty(ng, dtype=torch.float32, device=x.device)
+        native.check(native.kernels().hds_quant_minifloat(native.dt(x), x.data_ptr(), q.data_ptr(), scales.data_ptr(),
+                                                          ng, group_size, ebits, mantissa_bits, int(stochastic),
+                                                          int(seed) & 0x7FFFFFFF, native.stream()), "quant_minifloat")
+        return q, scales
+    g = x.float().reshape(-1, group_size)
+    amax = g.abs().amax(1)
+    scale = torch.where(amax > 0, amax / maxval, torch.ones_like(amax))
+    gen = torch.Generator().manual_seed(int(seed)) if stochastic else None
+    codes = _ref_encode(g / scale[:, None], q_bits, mantissa_bits, stochastic, gen)
+    return _pack(codes, q_bits), scale
+
+
+def dequantize_minifloat(q, scales, group_size=512, q_bits=6, mantissa_bits=2, dtype=torch.bfloat16, out=None):
+    ng = scales.numel()
+    ebits, _, _ = _mini_fmt(q_bits, mantissa_bits)
+    if native.use_native(q):
+        y = out if out is not None else torch.empty(ng * group_size, dtype=dtype, device=q.device)
+        native.check(native.kernels().hds_dequant_minifloat(native.dt(y), q.data_ptr(), scales.data_ptr(),
+                                                            y.data_ptr(), ng, group_size, ebits, mantissa_bits,
+                                                            native.stream()), "dequant_minifloat")
+        return y
+    v = _ref_decode(_unpack(q, q_bits), q_bits, mantissa_bits).reshape(-1, group_size) * scales[:, None].float()
+    y = v.reshape(-1).to(dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def fp6_linear(x, q_weight, scales, out_features, in_features, group_size, mantissa_bits=2):
+    """y = x @ dequant(W)^T for an FP6-packed weight [out, in] (row-major, groups along ``in``).
+
+    Decode-sized inputs (<= 8 rows) run the fused HIP GEMV that reads 6-bit weights straight from HBM; larger
+    batches dequantize the weight once to bf16 and use the matrix cores (hipBLASLt)."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, in_features)
+    M = x2.shape[0]
+    if native.use_native(x2) and M <= 8 and x2.dtype == torch.bfloat16 and in_features % 16 == 0 \
+            and group_size % 16 == 0:
+        x2 = x2.contiguous()
+        y = torch.empty(M, out_features, dtype=torch.bfloat16, device=x.device)
+        native.check(native.kernels().hds_fp6_gemv(x2.data_ptr(), q_weight.data_ptr(), scales.data_ptr(),
+                                                   y.data_ptr(), M, out_features, in_features, group_size,
+                                                   5 - mantissa_bits, mantissa_bits, native.stream()), "fp6_gemv")
+        return y.view(*lead, out_features)
+    w = dequantize_minifloat(q_weight, scales, group_size, 6, mantissa_bits, x.dtype).view(out_features, in_features)
+    return torch.nn.functional.linear(x, w)
