@@ -82,7 +82,12 @@ __device__ __forceinline__ bool masked(const AttnParams& p, int qi, int kj, int 
 // =====================================================================================
 // forward
 // =====================================================================================
-template <int NW>
+// VAR bit 0: static s_setprio(1) for the second-dispatched half of the waves (guide T5 static form);
+// VAR bit 1: deferred running-max update -- the max (and the O / l rescale) only moves when some row of the
+//            wave grew by more than kDeferThr (log2 units), so P stays <= 2^kDeferThr (guide T13).
+constexpr float kDeferThr = 8.f;
+
+template <int NW, int VAR>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
@@ -145,6 +150,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   stage_tile64<NW>(smem + 0, kptr(kt_begin));
   stage_tile64<NW>(smem + 2 * 16384, vptr(kt_begin));
   __syncthreads();
+  if constexpr ((VAR & 1) != 0 && NW == 8) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
 
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = (kt - kt_begin) & 1;
@@ -180,9 +188,26 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
           tmax = fmaxf(tmax, x);
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(m, tmax);
-      const float muse = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = fast_exp2(m - muse);
+      float alpha = 1.f, muse;
+      if constexpr ((VAR & 2) != 0) {
+        if (!__all(tmax <= m + kDeferThr)) {  // some row outgrew the stale max: move every row's max now
+          const float mnew = fmaxf(m, tmax);
+          alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
+          m = mnew;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        }
+        muse = (m == -INFINITY) ? 0.f : m;
+      } else {
+        const float mnew = fmaxf(m, tmax);
+        muse = (mnew == -INFINITY) ? 0.f : mnew;
+        alpha = fast_exp2(m - muse);
+        m = mnew;
+        if (__any(alpha != 1.f)) {  // running max moved for some row of this wave: rescale O
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        }
+      }
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -194,11 +219,6 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         }
       rs += __shfl_xor(rs, 32, 64);
       l = l * alpha + rs;
-      m = mnew;
-      if (__any(alpha != 1.f)) {  // running max moved for some row of this wave: rescale O
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-      }
       bf16x8 pb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
@@ -406,6 +426,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
 // (128 regs) + one 32x32 S/dP pair, which fits 256 registers -> 2 waves per SIMD, so one wave's
 // softmax/VALU section overlaps the other wave's MFMAs. The two query halves' partial dK/dV are
 // summed through LDS once at the end.
+template <int PRIO>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) {
   constexpr int BK = 128;
   // LDS: K (2 x 16K), V (2 x 16K), Q[2] (16K each), dO[2] (16K each), lse[2][64], delta[2][64]
@@ -484,6 +505,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
 
   if (total > 0) stage(0, 0);
   __syncthreads();
+  if constexpr (PRIO != 0) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
     if (it + 1 < total) stage(it + 1, buf ^ 1);
@@ -564,7 +588,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
 // =====================================================================================
 // backward dQ
 // =====================================================================================
-template <int NW>
+template <int NW, int PRIO>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
@@ -627,6 +651,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   stage_tile64<NW>(smem + 0, kptr(kt_begin));
   stage_tile64<NW>(smem + 2 * 16384, vptr(kt_begin));
   __syncthreads();
+  if constexpr (PRIO != 0 && NW == 8) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = (kt - kt_begin) & 1;
     const char* Kt = smem + buf * 16384;
@@ -650,12 +677,15 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) dp[t] = mfma(read_rows(Vt, 32 * t, ks), df[ks], dp[t]);
       }
+      // only tiles that straddle the causal diagonal / window edge / sequence end need the per-element mask
+      const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
+                             (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float pr = fast_exp2(s[t][r] * c - lse2);
-          if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) pr = 0.f;
+          if (need_mask && masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) pr = 0.f;
           s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
         }
       const bf16x8 sb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
@@ -716,7 +746,20 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 }  // namespace
 
-int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8;
+int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1;
+
+// forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both
+HDS_EXPORT int hds_attn_fwd_variant(int var) {
+  if (var < 0 || var > 3) return hipErrorInvalidValue;
+  g_fwd_var = var;
+  return 0;
+}
+
+// backward: static s_setprio(1) for waves 4-7 of the 8-wave dK/dV and dQ kernels (0 / 1)
+HDS_EXPORT int hds_attn_bwd_prio(int on) {
+  g_bwd_prio = on ? 1 : 0;
+  return 0;
+}
 
 // runtime selection of the waves-per-workgroup variants (4 or 8)
 HDS_EXPORT int hds_attn_config(int fwd_nw, int dkdv_nw, int dq_nw) {
@@ -734,10 +777,17 @@ HDS_EXPORT int hds_attn_fwd(const void* q, const void* k, const void* v, void* o
   if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
   AttnParams p = make_params(q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, strides, cu_seqlens, batch,
                              seq_len, total_tokens, hq, hkv, scale, causal, window);
-  if (g_fwd_nw == 8)
-    hipLaunchKernelGGL(attn_fwd_kernel<8>, dim3((max_len + 255) / 256, hq, batch), dim3(512), 0, st, p);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<4>, dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
+  if (g_fwd_nw == 8) {
+    const dim3 grid((max_len + 255) / 256, hq, batch);
+    switch (g_fwd_var) {
+      case 1: hipLaunchKernelGGL((attn_fwd_kernel<8, 1>), grid, dim3(512), 0, st, p); break;
+      case 2: hipLaunchKernelGGL((attn_fwd_kernel<8, 2>), grid, dim3(512), 0, st, p); break;
+      case 3: hipLaunchKernelGGL((attn_fwd_kernel<8, 3>), grid, dim3(512), 0, st, p); break;
+      default: hipLaunchKernelGGL((attn_fwd_kernel<8, 0>), grid, dim3(512), 0, st, p); break;
+    }
+  } else {
+    hipLaunchKernelGGL((attn_fwd_kernel<4, 0>), dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
+  }
   return hipGetLastError();
 }
 
@@ -750,13 +800,23 @@ HDS_EXPORT int hds_attn_bwd(const void* q, const void* k, const void* v, const v
                              seq_len, total_tokens, hq, hkv, scale, causal, window);
   const int64_t rows = (int64_t)total_tokens * hq;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, st, p);
-  if (g_dkdv_nw == 8)
-    hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel, dim3((max_len + 127) / 128, hkv, batch), dim3(512), 0, st, p);
-  else
+  if (g_dkdv_nw == 8) {
+    const dim3 grid((max_len + 127) / 128, hkv, batch);
+    if (g_bwd_prio)
+      hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel<1>, grid, dim3(512), 0, st, p);
+    else
+      hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel<0>, grid, dim3(512), 0, st, p);
+  } else {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<4>, dim3((max_len + 127) / 128, hkv, batch), dim3(256), 0, st, p);
-  if (g_dq_nw == 8)
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<8>, dim3((max_len + 255) / 256, hq, batch), dim3(512), 0, st, p);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<4>, dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
+  }
+  if (g_dq_nw == 8) {
+    const dim3 grid((max_len + 255) / 256, hq, batch);
+    if (g_bwd_prio)
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<8, 1>), grid, dim3(512), 0, st, p);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<8, 0>), grid, dim3(512), 0, st, p);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 0>), dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
+  }
   return hipGetLastError();
 }

@@ -39,6 +39,8 @@ _KERNEL_SIGS = {
     "hds_attn_fwd": "p" * 7 + "i" * 7 + "f" + "ii" + "s",
     "hds_attn_bwd": "p" * 12 + "i" * 7 + "f" + "ii" + "s",
     "hds_attn_config": "iii",
+    "hds_attn_fwd_variant": "i",
+    "hds_attn_bwd_prio": "i",
     "hds_bsattn_fwd": "p" * 8 + "i" * 7 + "f" + "i" + "s",
     "hds_bsattn_bwd": "p" * 15 + "i" * 7 + "f" + "i" + "s",
     "hds_kv_rope_scatter": "i" + "p" + "l" + "pppp" + "i" + "pp" + "i" * 7 + "s",
