@@ -1,0 +1,100 @@
+"""``engine.compile()``: the DeepCompile entry point, realised by this framework's native runtime passes.
+
+Reference parity: compile/config.py (``CompileConfig``: deepcompile, free_activation, offload_activation,
+offload_opt_states, double_buffer, symmetric_memory, offload_parameters, sync_* switches), runtime/engine.py
+``compile`` :3876-3941 (``init_z1`` / ``init_z3`` graph passes, ``register_compile_pass``, ``get_compile_time``,
+``is_compiled``) and compile/passes/* (zero3 gather/release insertion, prefetch scheduling, selective gather,
+Adam-state offload, activation / parameter offload).
+
+MI355X design: the reference gets its schedule by tracing the model with torch.compile (Inductor, which emits
+Triton) and rewriting the FX graph. This framework has no tracing compiler; every pass the reference inserts is
+already a runtime mechanism of the engine, driven by the module-execution trace it records on the first step:
+
+  * zero3 gather/release + prefetch scheduling  -> ZeRO-3 trace-driven prefetch (``zero3_prefetch_depth``) with
+    all-gathers on RCCL's stream and release on last use (runtime/zero/optimizer.py);
+  * selective gather                            -> persistent small units (``stage3_param_persistence_threshold``);
+  * offload_activation                          -> HCache host activation cache (offload/activation_cache.py):
+    saved activations go D2H into pinned rings on a side stream, prefetched back in backward;
+  * offload_opt_states                          -> optimizer states move to pinned host right after
+    ``step()`` and return asynchronously at the start of the next forward (runtime/zero/offload_states.py),
+    overlapped with the forward of the first units;
+  * offload_parameters                          -> ZeRO-Infinity parameter offload (configured at init);
+  * double_buffer / symmetric_memory            -> RCCL reduce-scatter buckets are already double-buffered per
+    unit; symmetric memory has no RCCL analogue here and is ignored with a warning.
+
+``compile()`` therefore validates the configuration, switches those mechanisms on and records per-pass setup
+times (``get_compile_time``). User passes registered with ``register_compile_pass`` are called once with the
+engine (they may adjust knobs such as the prefetch depth).
+"""
+import time
+
+from ..utils.logging import log_dist, logger
+
+_FIELDS = {
+    "deepcompile": False, "free_activation": False, "offload_activation": False, "offload_opt_states": False,
+    "double_buffer": True, "symmetric_memory": False, "debug_log": False, "offload_parameters": False,
+    "sync_before_reduce": False, "sync_after_reduce": False, "sync_before_allgather": False,
+    "sync_after_allgather": False
+}
+
+_user_passes = {}
+
+
+class CompileConfig:
+
+    def __init__(self, d=None):
+        d = dict(d or {})
+        unknown = set(d) - set(_FIELDS)
+        if unknown:
+            raise ValueError(f"unknown compile config keys: {sorted(unknown)}")
+        for k, v in _FIELDS.items():
+            setattr(self, k, bool(d.get(k, v)))
+
+    def to_dict(self):
+        return {k: getattr(self, k) for k in _FIELDS}
+
+
+def register_compile_pass(name, fn):
+    _user_passes[name] = fn
+
+
+def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None):
+    """Apply the DeepCompile configuration to ``engine`` (see module docstring). Returns per-pass setup times."""
+    cfg = CompileConfig(engine._config.raw.get("compile", {}))
+    times = {}
+    if backend not in ("native", "eager", "inductor", "hip_graph"):
+        raise ValueError(f"backend {backend} is not supported")
+    if backend == "inductor":
+        logger.warning("compile(backend='inductor'): Inductor emits Triton, which this framework does not use; "
+                       "running the native runtime passes instead")
+    if cfg.deepcompile:
+        stage = engine.zero_optimization_stage()
+        assert stage in (1, 3), "DeepCompile supports ZeRO stage 1 or 3 only"
+        assert engine.optimizer is not None, "DeepCompile needs an optimizer"
+    t0 = time.perf_counter()
+    if cfg.offload_activation and engine._activation_cache is None:
+        from ..offload.activation_cache import HostActivationCache
+        hc = engine._config.mi355x.host_act_cache
+        engine._activation_cache = HostActivationCache.from_config(hc, engine.device).attach(engine.module)
+    times["offload_activation"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    engine._dc_offload_opt_states = bool(cfg.offload_opt_states)
+    times["offload_adam_states"] = time.perf_counter() - t0
+    if cfg.offload_parameters and not engine._config.zero_config.offload_param.enabled:
+        logger.warning("compile: offload_parameters requires zero_optimization.offload_param at initialize(); "
+                       "parameters stay on device")
+    if cfg.symmetric_memory:
+        logger.warning("compile: symmetric_memory has no RCCL equivalent here; ignored")
+    for name, fn in _user_passes.items():
+        t0 = time.perf_counter()
+        fn(engine)
+        times[name] = time.perf_counter() - t0
+    for step, passes in (schedule or []):
+        for p in passes:
+            if callable(p):
+                t0 = time.perf_counter()
+                p(engine)
+                times[getattr(p, "__name__", str(p))] = time.perf_counter() - t0
+    engine._compile_config = cfg
+    log_dist(f"compile: backend={backend} deepcompile={cfg.deepcompile} passes={sorted(times)}", ranks=[0])
+    return times

@@ -367,6 +367,9 @@ class DeepSpeedEngine(nn.Module):
                 kwargs["curriculum_seqlen"] = d
         if self.progressive_layer_drop is not None and self.module.training:
             kwargs.update(self.progressive_layer_drop.get_state())
+        if getattr(self, "_dc_states_offloaded", False):
+            self.reload_states(non_blocking=True)  # DeepCompile offload_opt_states: bring states back
+            self._dc_states_offloaded = False
         if self.optimizer is not None:
             self.optimizer.pre_forward()
         ctx = self._activation_cache.forward_context() if (self._activation_cache is not None and
@@ -432,6 +435,9 @@ class DeepSpeedEngine(nn.Module):
                 self.monitor.write_events([("Train/Samples/lr", self.get_lr()[0], self.global_samples)])
             if self.global_steps % self.steps_per_print() == 0 and self.wall_clock_breakdown():
                 self.timers.log([FORWARD_MICRO_TIMER, BACKWARD_MICRO_TIMER, STEP_MICRO_TIMER])
+        if boundary and getattr(self, "_dc_offload_opt_states", False):
+            self.offload_states(include=["optim_states"], non_blocking=True)
+            self._dc_states_offloaded = True
         self.micro_steps += 1
         self._force_boundary = None
         self.timers(STEP_MICRO_TIMER).stop()
@@ -503,6 +509,30 @@ class DeepSpeedEngine(nn.Module):
         if self.zero_optimization_stage() == 3 and self.optimizer.partitioned:
             return None
         return self.module.state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)
+
+    # ------------------------------------------------------------------------------------
+    # DeepCompile entry (reference engine.py:3876-3941); see runtime/compile.py
+    # ------------------------------------------------------------------------------------
+    def compile(self, backend="native", compile_kwargs=None, schedule=None):
+        if getattr(self, "_is_compiled", False):
+            return
+        from .compile import compile_engine
+        self._compile_times = compile_engine(self, backend, compile_kwargs or {}, schedule)
+        self._is_compiled = True
+
+    @property
+    def is_compiled(self):
+        return getattr(self, "_is_compiled", False)
+
+    def is_deepcompile_enabled(self):
+        return bool(self._config.raw.get("compile", {}).get("deepcompile", False))
+
+    def get_compile_time(self):
+        return dict(getattr(self, "_compile_times", {}))
+
+    def register_compile_pass(self, pass_name, pass_fn):
+        from .compile import register_compile_pass
+        register_compile_pass(pass_name, pass_fn)
 
     def offload_states(self, include=None, device="cpu", pin_memory=True, non_blocking=False):
         from .zero.offload_states import offload_states

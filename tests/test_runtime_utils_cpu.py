@@ -103,3 +103,37 @@ def test_nvtx_decorator_and_profiler_and_comet_gate():
     prof.log_events()
     m = MonitorMaster({"comet": {"enabled": True}})  # comet_ml is not installed -> disabled, no crash
     assert not m.enabled
+
+
+def test_engine_compile_offload_opt_states_roundtrip():
+    """engine.compile() with offload_opt_states: Adam states leave the device after each step and come back
+    for the next; training matches an uncompiled engine exactly."""
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from tests.test_zero_cpu import TINY
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=os.environ.get("MASTER_PORT", "29651"))
+    losses = {}
+    for compiled in (False, True):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(**TINY))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
+               "zero_optimization": {"stage": 1},
+               "compile": {"deepcompile": True, "offload_opt_states": True}}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        calls = []
+        if compiled:
+            eng.register_compile_pass("probe", lambda e: calls.append(e))
+            eng.compile()
+            assert eng.is_compiled and eng.is_deepcompile_enabled() and calls == [eng]
+            assert "offload_adam_states" in eng.get_compile_time()
+        g = torch.Generator().manual_seed(3)
+        out = []
+        for _ in range(3):
+            b = torch.randint(0, 97, (2, 12), generator=g)
+            loss = eng(b, labels=b)
+            eng.backward(loss)
+            eng.step()
+            out.append(float(loss))
+        losses[compiled] = out
+    assert losses[True] == pytest.approx(losses[False], rel=1e-6, abs=1e-6)
