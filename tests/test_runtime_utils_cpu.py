@@ -137,3 +137,11 @@ def test_engine_compile_offload_opt_states_roundtrip():
             out.append(float(loss))
         losses[compiled] = out
     assert losses[True] == pytest.approx(losses[False], rel=1e-6, abs=1e-6)
+
+
+def test_ds_io_and_nvme_tune(tmp_path):
+    from hcache_deepspeed_amd.nvme import ds_io_main, sweep
+    out = ds_io_main(["--folder", str(tmp_path), "--io_size", "1M", "--read", "--write", "--loops", "1"])
+    assert {r["op"] for r in out} == {"read", "write"} and all(r["GB/s"] > 0 for r in out)
+    _, best, cfg = sweep(str(tmp_path), "512K", ("128K", ), (4, ), (1, 2), loops=1)
+    assert best["read"]["GB/s"] > 0 and set(cfg["aio"]) >= {"block_size", "queue_depth", "intra_op_parallelism"}
