@@ -215,6 +215,14 @@ def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, prof=False, 
 
 @timed_op
 def inference_all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False):
+    """TP inference all-reduce: CPU fp32/bf16 tensors of single-host jobs go through the shared-memory
+    all-reduce (csrc/host/shm_comm.cpp, reference csrc/cpu/comm/shm.cpp); everything else uses the
+    process group (RCCL on GPU)."""
+    if op == ReduceOp.SUM and not _single(group):
+        from .shm import get_shm_comm, shm_eligible
+        if shm_eligible(tensor, group):
+            get_shm_comm(group).all_reduce_(tensor)
+            return _Done() if async_op else None
     return all_reduce(tensor, op=op, group=group, async_op=async_op)
 
 

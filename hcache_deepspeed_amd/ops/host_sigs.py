@@ -26,6 +26,11 @@ SIGS = {
     "hds_cpu_sumsq": (D, [P, I, L, P]),
     "hds_cpu_num_threads": (I, []),
     "hds_cpu_set_num_threads": (I, [I]),
+    # shm_comm.cpp
+    "hds_shm_open": (P, [ctypes.c_char_p, I, I, L, I]),
+    "hds_shm_close": (I, [P, I]),
+    "hds_shm_slot_bytes": (L, [P]),
+    "hds_shm_allreduce": (I, [P, P, L, I]),
     # aio.cpp
     "hds_aio_create": (P, [L, I, I, I, I]),
     "hds_aio_destroy": (I, [P]),
