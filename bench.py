@@ -23,6 +23,19 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def _use_tuned_gemms():
+    """Read the committed hipBLASLt/rocBLAS solution table (PyTorch TunableOp, tuned on MI355X for exactly the
+    bench's GEMM shapes by tools/gpu_tunableop.sh). Tuning is off: shapes missing from the table keep the
+    library heuristic. Must run before torch initialises its BLAS handles; HDS_TUNABLEOP=0 disables it."""
+    table = os.path.join(ROOT, "tuning", "tunableop_results%d.csv")
+    if os.environ.get("HDS_TUNABLEOP", "1") != "1" or not os.path.exists(table % 0):
+        return False
+    os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
+    os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "0")
+    os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", table)
+    return True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -43,6 +56,7 @@ def main():
     ap.add_argument("--offload-param", action="store_true")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
     args = ap.parse_args()
+    tuned = _use_tuned_gemms()
 
     import torch
     import torch.distributed as tdist
@@ -160,7 +174,7 @@ def main():
                        "activation_checkpointing": bool(args.ckpt)},
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
                       "final_loss": round(float(loss.item()), 4), "peak_mem_gib": round(mem, 1),
-                      "init_s": round(t_init, 1), "valid": not bool(args.layers)},
+                      "init_s": round(t_init, 1), "valid": not bool(args.layers), "tuned_gemm_table": tuned},
         }
         print(json.dumps(out), flush=True)
     tdist.barrier()

@@ -39,3 +39,15 @@ def test_shm_allreduce_2():
 
 def test_shm_allreduce_3():
     run_distributed(_shm, 3)
+
+
+def _bench(rank, world):
+    from hcache_deepspeed_amd.benchmarks.communication import bench
+    res = bench(sizes=(4096, ), dtype=torch.float32, trials=2, warmups=1)
+    assert {r["op"] for r in res} == {"all_reduce", "all_gather", "reduce_scatter", "all_to_all", "broadcast",
+                                      "pt2pt"}
+    assert all(r["lat_ms"] > 0 and r["busbw_GBps"] >= 0 for r in res)
+
+
+def test_ds_bench_collectives_gloo():
+    run_distributed(_bench, 2)
