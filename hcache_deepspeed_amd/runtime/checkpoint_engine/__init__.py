@@ -88,4 +88,64 @@ class AsyncCheckpointEngine(TorchCheckpointEngine):
         return True
 
 
-NebulaCheckpointEngine = AsyncCheckpointEngine
+
+class NebulaCheckpointEngine(AsyncCheckpointEngine):
+    """Tiered asynchronous checkpointing with the reference Nebula config (nebula/config.py: ``enabled``,
+    ``persistent_storage_path``, ``persistent_time_interval``, ``num_of_version_in_retention``,
+    ``enable_nebula_load``, ``load_path``).
+
+    Azure's Nebula service is replaced by the same two tiers on local resources: ``save`` writes each file to the
+    fast tier (the checkpoint directory) asynchronously from pinned host copies; every
+    ``persistent_time_interval``-th ``commit`` additionally copies the tag's files to ``persistent_storage_path``
+    in a background thread, keeping the newest ``num_of_version_in_retention`` tags there. ``load`` prefers the fast
+    tier and falls back to the persistent one when ``enable_nebula_load`` is set."""
+
+    def __init__(self, config_params=None):
+        super().__init__(config_params)
+        cfg = dict(getattr(config_params, "nebula", None) or (config_params or {}) if isinstance(
+            config_params, dict) else getattr(config_params, "nebula", None) or {})
+        self.persistent_path = cfg.get("persistent_storage_path")
+        self.interval = max(1, int(cfg.get("persistent_time_interval", 100) or 1))
+        self.retention = max(1, int(cfg.get("num_of_version_in_retention", 2) or 1))
+        self.enable_load = bool(cfg.get("enable_nebula_load", True))
+        self.load_path = cfg.get("load_path")
+        self._written = {}
+        self._commits = 0
+        self._persist_threads = []
+        self._persisted = []
+
+    def save(self, state_dict, path):
+        self._written.setdefault(self._tag, []).append(path)
+        super().save(state_dict, path)
+
+    def _persist(self, tag, files):
+        import shutil
+        dst = os.path.join(self.persistent_path, str(tag))
+        os.makedirs(dst, exist_ok=True)
+        for f in files:
+            shutil.copy2(f, os.path.join(dst, os.path.basename(f)))
+        self._persisted.append(dst)
+        while len(self._persisted) > self.retention:
+            shutil.rmtree(self._persisted.pop(0), ignore_errors=True)
+
+    def commit(self, tag):
+        super().commit(tag)
+        files = self._written.pop(tag, [])
+        self._commits += 1
+        if self.persistent_path and files and self._commits % self.interval == 0:
+            t = threading.Thread(target=self._persist, args=(tag, files), daemon=False)
+            t.start()
+            self._persist_threads.append(t)
+        return True
+
+    def wait_persisted(self):
+        for t in self._persist_threads:
+            t.join()
+        self._persist_threads = []
+
+    def load(self, path, map_location=None):
+        if os.path.exists(path) or not (self.enable_load and (self.load_path or self.persistent_path)):
+            return super().load(path, map_location)
+        base = self.load_path or self.persistent_path
+        tag = os.path.basename(os.path.dirname(path))
+        return super().load(os.path.join(base, tag, os.path.basename(path)), map_location)

@@ -145,3 +145,21 @@ def test_ds_io_and_nvme_tune(tmp_path):
     assert {r["op"] for r in out} == {"read", "write"} and all(r["GB/s"] > 0 for r in out)
     _, best, cfg = sweep(str(tmp_path), "512K", ("128K", ), (4, ), (1, 2), loops=1)
     assert best["read"]["GB/s"] > 0 and set(cfg["aio"]) >= {"block_size", "queue_depth", "intra_op_parallelism"}
+
+
+def test_nebula_engine_tiers(tmp_path):
+    from hcache_deepspeed_amd.runtime.checkpoint_engine import NebulaCheckpointEngine
+    fast, persist = tmp_path / "fast", tmp_path / "persist"
+    eng = NebulaCheckpointEngine({"persistent_storage_path": str(persist), "persistent_time_interval": 1,
+                                  "num_of_version_in_retention": 2, "enable_nebula_load": True})
+    for step in range(3):
+        tag = f"global_step{step}"
+        os.makedirs(fast / tag, exist_ok=True)
+        eng.create(tag)
+        eng.save({"w": torch.full((4, ), float(step))}, str(fast / tag / "model.pt"))
+        eng.commit(tag)
+    eng.wait_persisted()
+    assert sorted(os.listdir(persist)) == ["global_step1", "global_step2"]  # retention 2
+    os.remove(fast / "global_step2" / "model.pt")  # fast tier lost -> served from the persistent tier
+    sd = eng.load(str(fast / "global_step2" / "model.pt"))
+    assert torch.equal(sd["w"], torch.full((4, ), 2.0))
