@@ -222,3 +222,10 @@ def _released_memory(rank, world):
 
 def test_zero3_releases_gathered_weights_world2():
     run_distributed(_released_memory, 2)
+
+
+@pytest.mark.parametrize("world,stage,zinit", [(4, 3, False), (3, 3, True), (4, 1, False)])
+def test_zero_world3_4(world, stage, zinit):
+    """More ranks than the default harness (uneven shard padding at world 3, 4-way reduce-scatter / all-gather):
+    the flat-shard collectives used at 8 GPUs, rehearsed on gloo."""
+    run_distributed(_zero_vs_torch, world, stage, 1, zinit)
