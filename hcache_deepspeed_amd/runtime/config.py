@@ -164,6 +164,9 @@ class HostActCacheConfig:
     slots: int = 8
     slot_mb: int = 512
     min_layers_resident: int = 2
+    policy: str = "budget"  # "budget": spill only what exceeds gpu_budget_gib; "all": spill every eligible layer
+    gpu_budget_gib: float = 0.0  # 0: 92% of device memory
+    prefetch_layers: int = 2
 
 
 @dataclass

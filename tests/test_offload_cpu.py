@@ -110,3 +110,13 @@ def test_zero_offload_matches_device(stage, device, ratio, tmp_path):
 def test_zero_infinity_param_offload_matches_device(world, tmp_path):
     """ZeRO-Infinity: offload_param + offload_optimizer (cpu) reproduce the on-device ZeRO-3 trajectory."""
     run_distributed(_offload_vs_device, world, 3, "cpu", 1.0, str(tmp_path), True)
+
+
+def test_act_cache_plan_spills_earliest_layers_within_budget():
+    """Host activation cache budget planner: spill the shortest prefix of layers that fits the HBM budget."""
+    from hcache_deepspeed_amd.offload.activation_cache import plan_offload
+    lb = {i: 10 for i in range(8)}
+    assert plan_offload(lb, peak_all=100, budget=1000) == set()          # everything fits: spill nothing
+    assert plan_offload(lb, peak_all=100, budget=135) == set(range(5))   # 3 layers (30 B) fit next to the peak
+    assert plan_offload(lb, peak_all=100, budget=99) == set(range(8))    # nothing fits: spill all
+    assert plan_offload({}, peak_all=0, budget=1) == set()
