@@ -58,6 +58,11 @@ _KERNEL_SIGS = {
     "hds_quant_minifloat": "i" + "ppp" + "l" + "iiiii" + "s",
     "hds_dequant_minifloat": "i" + "ppp" + "l" + "iii" + "s",
     "hds_fp6_gemv": "pppp" + "iiiiii" + "s",
+    "hds_token_gather": "i" + "ppp" + "iiii" + "s",
+    "hds_token_scatter": "i" + "ppp" + "iiii" + "s",
+    "hds_token_sort": "p" + "ii" + "s",
+    "hds_slice_mask": "i" + "ppp" + "iiiii" + "s",
+    "hds_nhwc_bias_add": "i" + "ppppp" + "l" + "ii" + "s",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}

@@ -10,26 +10,27 @@ the reserved length. Gather/scatter are single index_select/index_copy passes ov
 import torch
 import torch.nn as nn
 
+from ...ops.random_ltd import GatherTokens, ScatterTokens, token_sort_
+
 
 def gpt_sample_tokens(reserved_length, seq_length, batch_size, layers=1, device="cpu", generator=None):
-    """Per (layer, batch) sorted random token indices [layers, B, reserved] (causal order preserved)."""
+    """Per (layer, batch) sorted random token indices [layers, B, reserved] (causal order preserved).
+
+    The rows are sorted with ``token_sort_`` (LDS bitonic sort on GPU, csrc/kernels/token_ops.hip)."""
     scores = torch.rand(layers * batch_size, seq_length, device=device, generator=generator)
-    idx = scores.topk(reserved_length, dim=1).indices.sort(dim=1).values
+    idx = scores.topk(reserved_length, dim=1).indices.to(torch.int32).contiguous()
+    token_sort_(idx)
     return idx.view(layers, batch_size, reserved_length)
 
 
 def token_gather(x, idx):
-    """x [B, S, H], idx [B, R] -> [B, R, H]."""
-    B, S, H = x.shape
-    flat = (idx + torch.arange(B, device=x.device)[:, None] * S).reshape(-1)
-    return x.reshape(B * S, H).index_select(0, flat).view(B, -1, H)
+    """x [B, S, H], idx [B, R] -> [B, R, H] (differentiable; HIP row gather on GPU)."""
+    return GatherTokens.apply(x, idx, True)[1]
 
 
 def token_scatter(full, part, idx):
-    """Write part [B, R, H] back into a copy of full [B, S, H] at idx [B, R]."""
-    B, S, H = full.shape
-    flat = (idx + torch.arange(B, device=full.device)[:, None] * S).reshape(-1)
-    return full.reshape(B * S, H).index_copy(0, flat, part.reshape(-1, H)).view(B, S, H)
+    """Copy of full [B, S, H] with rows idx [B, R] replaced by part [B, R, H] (differentiable)."""
+    return ScatterTokens.apply(full, part, idx, True)
 
 
 class RandomLTDScheduler:
