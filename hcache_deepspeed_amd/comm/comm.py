@@ -206,8 +206,40 @@ def _single(group):
     return get_world_size(group) == 1
 
 
+# Debug switches that turn whole collective families into no-ops (reference comm/torch.py:58-93): used to
+# measure how much of a step is communication-bound without changing the program.
+_OFF = {"all_gather": False, "reduce_scatter": False, "broadcast": False, "all_reduce": False, "reduce": False}
+
+
+def all_gather_comm_off(flag=False):
+    _OFF["all_gather"] = bool(flag)
+
+
+def reduce_scatter_comm_off(flag=False):
+    _OFF["reduce_scatter"] = bool(flag)
+
+
+def broadcast_comm_off(flag=False):
+    _OFF["broadcast"] = bool(flag)
+
+
+def all_reduce_comm_off(flag=False):
+    _OFF["all_reduce"] = bool(flag)
+
+
+def reduce_comm_off(flag=False):
+    _OFF["reduce"] = bool(flag)
+
+
+def backward_comm_off(flag=False):
+    all_gather_comm_off(flag)
+    reduce_scatter_comm_off(flag)
+
+
 @timed_op
 def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, prof=False, log_name="all_reduce"):
+    if _OFF["all_reduce"] and not _single(group):
+        return _Done() if async_op else None
     if _single(group):
         return _Done() if async_op else None
     return dist.all_reduce(tensor, op=op, group=group, async_op=async_op)
@@ -240,7 +272,33 @@ def all_reduce_coalesced(tensors, op=ReduceOp.SUM, group=None, async_op=False):
 
 
 @timed_op
+def all_gather_coalesced(output_tensors, input_tensors, group=None, async_op=False):
+    """All-gather a list of tensors with ONE collective: inputs are packed into one flat buffer, gathered
+    rank-major with ``all_gather_into_tensor`` and unpacked into ``output_tensors[i]`` (each ``world`` times the
+    size of ``input_tensors[i]``, rank-major)."""
+    world = get_world_size(group)
+    if _single(group):
+        for o, i in zip(output_tensors, input_tensors):
+            o.view(-1)[:i.numel()].copy_(i.reshape(-1))
+        return _Done() if async_op else None
+    if _OFF["all_gather"]:
+        return _Done() if async_op else None
+    sizes = [t.numel() for t in input_tensors]
+    flat = torch.cat([t.reshape(-1) for t in input_tensors])
+    out = torch.empty(world * flat.numel(), dtype=flat.dtype, device=flat.device)
+    dist.all_gather_into_tensor(out, flat, group=group)
+    out = out.view(world, -1)
+    off = 0
+    for o, n in zip(output_tensors, sizes):
+        o.view(world, n).copy_(out[:, off:off + n])
+        off += n
+    return _Done() if async_op else None
+
+
+@timed_op
 def reduce(tensor, dst, op=ReduceOp.SUM, group=None, async_op=False):
+    if _OFF["reduce"] and not _single(group):
+        return _Done() if async_op else None
     if _single(group):
         return _Done() if async_op else None
     return dist.reduce(tensor, dst, op=op, group=group, async_op=async_op)
@@ -248,6 +306,8 @@ def reduce(tensor, dst, op=ReduceOp.SUM, group=None, async_op=False):
 
 @timed_op
 def broadcast(tensor, src, group=None, async_op=False):
+    if _OFF["broadcast"] and not _single(group):
+        return _Done() if async_op else None
     if _single(group):
         return _Done() if async_op else None
     return dist.broadcast(tensor, src, group=group, async_op=async_op)
@@ -268,6 +328,8 @@ def all_gather_object(object_list, obj, group=None):
 
 @timed_op
 def all_gather(tensor_list, tensor, group=None, async_op=False):
+    if _OFF["all_gather"] and not _single(group):
+        return _Done() if async_op else None
     if _single(group):
         tensor_list[0].copy_(tensor)
         return _Done() if async_op else None
@@ -276,6 +338,8 @@ def all_gather(tensor_list, tensor, group=None, async_op=False):
 
 @timed_op
 def all_gather_into_tensor(output_tensor, tensor, group=None, async_op=False):
+    if _OFF["all_gather"] and not _single(group):
+        return _Done() if async_op else None
     if _single(group):
         if output_tensor.data_ptr() != tensor.data_ptr():
             output_tensor.copy_(tensor.view_as(output_tensor))
@@ -288,6 +352,8 @@ allgather_fn = all_gather_into_tensor
 
 @timed_op
 def reduce_scatter_tensor(output_tensor, tensor, op=ReduceOp.SUM, group=None, async_op=False):
+    if _OFF["reduce_scatter"] and not _single(group):
+        return _Done() if async_op else None
     if _single(group):
         if output_tensor.data_ptr() != tensor.data_ptr():
             output_tensor.copy_(tensor.view_as(output_tensor))
@@ -304,6 +370,8 @@ reduce_scatter_fn = reduce_scatter_tensor
 
 @timed_op
 def reduce_scatter(output, input_list, op=ReduceOp.SUM, group=None, async_op=False):
+    if _OFF["reduce_scatter"] and not _single(group):
+        return _Done() if async_op else None
     if _single(group):
         output.copy_(input_list[0])
         return _Done() if async_op else None
@@ -390,3 +458,42 @@ def initialize_mesh_device(mesh_shape, mesh_dim_names):
     from torch.distributed.device_mesh import init_device_mesh
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     return init_device_mesh(dev, mesh_shape, mesh_dim_names=mesh_dim_names)
+
+
+def get_all_ranks_from_group(group=None):
+    """Global ranks that make up ``group`` (reference comm.py:594)."""
+    if group is None or not is_initialized():
+        return list(range(get_world_size()))
+    return dist.get_process_group_ranks(group)
+
+
+def has_all_gather_into_tensor():
+    return hasattr(dist, "all_gather_into_tensor")
+
+
+def has_reduce_scatter_tensor():
+    return hasattr(dist, "reduce_scatter_tensor")
+
+
+def has_all_reduce_coalesced():
+    return True
+
+
+def has_coalescing_manager():
+    return hasattr(dist.distributed_c10d, "_coalescing_manager")
+
+
+def coalescing_manager(group=None, device=None, async_ops=False):
+    """Batch the collectives issued inside the ``with`` block into one RCCL group launch (torch's
+    ``_coalescing_manager``); a plain no-op context when unavailable or for a world of one."""
+    import contextlib
+    if not is_initialized() or _single(group) or not has_coalescing_manager():
+        return contextlib.nullcontext()
+    return dist.distributed_c10d._coalescing_manager(group, device=device, async_ops=async_ops)
+
+
+def enable_symm_mem_for_group(group_name):
+    """Reference comm.py:624 enables torch symmetric memory (CUDA multicast/NVLS). xGMI has no multicast object;
+    RCCL already uses direct peer writes inside a node, so this is a logged no-op that reports False."""
+    logger.info(f"symmetric memory not used on MI355X (group {group_name}): RCCL peer-to-peer over xGMI instead")
+    return False

@@ -19,6 +19,12 @@ import torch
 from . import native
 
 
+def _glr(group):
+    """Effective learning rate of a param group: ``lr`` times the muP width multiplier ``lr_mult`` (ops/mup.py);
+    schedulers keep writing the unscaled ``lr``."""
+    return group["lr"] * group.get("lr_mult", 1.0)
+
+
 def _f(x):
     return float(x)
 
@@ -204,7 +210,7 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
                 st["step"] = step
                 if not native.use_native(p):
-                    adam_flat(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], step, group["lr"], (b1, b2),
+                    adam_flat(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], step, _glr(group), (b1, b2),
                               group["eps"], group["weight_decay"], bool(self.adam_w_mode), group["bias_correction"],
                               grad_scale=grad_scale, dev_scale=dev_scale, found_inf=found_inf)
                     continue
@@ -216,7 +222,7 @@ class FusedAdam(torch.optim.Optimizer):
                 tensors, chunks, n = tab.get(rows, group["params"][0].device)
                 native.check(
                     native.kernels().hds_adam_multi(native.dt(pd), native.dt(gd), tensors.data_ptr(), chunks.data_ptr(),
-                                                    n, _f(group["lr"]), _f(b1), _f(b2), _f(group["eps"]),
+                                                    n, _f(_glr(group)), _f(b1), _f(b2), _f(group["eps"]),
                                                     _f(group["weight_decay"]), _f(bc1), _f(bc2), self.adam_w_mode,
                                                     _f(grad_scale), native.ptr(dev_scale), native.ptr(found_inf),
                                                     native.stream()), "adam_multi")
@@ -241,7 +247,7 @@ class FusedLion(torch.optim.Optimizer):
                 if len(st) == 0:
                     st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
                 g = p.grad.contiguous()
-                lion_flat(p.data, g, st["exp_avg"], group["lr"], group["betas"], group["weight_decay"],
+                lion_flat(p.data, g, st["exp_avg"], _glr(group), group["betas"], group["weight_decay"],
                           grad_scale=grad_scale, dev_scale=dev_scale, found_inf=found_inf)
         return loss
 
@@ -283,7 +289,7 @@ class FusedLamb(torch.optim.Optimizer):
                 norms = torch.zeros(2 * len(params), device=params[0].device, dtype=torch.float32)
                 native.check(
                     native.kernels().hds_lamb_multi(native.dt(pd), native.dt(gd), tensors.data_ptr(),
-                                                    chunks.data_ptr(), n, norms.data_ptr(), _f(group["lr"]), _f(b1),
+                                                    chunks.data_ptr(), n, norms.data_ptr(), _f(_glr(group)), _f(b1),
                                                     _f(b2), _f(group["eps"]), _f(group["weight_decay"]), _f(bc1),
                                                     _f(bc2), _f(group["max_coeff"]), _f(group["min_coeff"]),
                                                     _f(grad_scale), native.ptr(dev_scale), native.ptr(found_inf),
@@ -300,5 +306,5 @@ class FusedLamb(torch.optim.Optimizer):
                 pn, un = pf.norm(), u.norm()
                 trust = (pn / un) if (pn > 0 and un > 0) else torch.tensor(1.0)
                 trust = float(min(max(float(trust), group["min_coeff"]), group["max_coeff"]))
-                p.data.copy_(pf - group["lr"] * trust * u)
+                p.data.copy_(pf - _glr(group) * trust * u)
         return loss

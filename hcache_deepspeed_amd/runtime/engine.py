@@ -244,6 +244,11 @@ class DeepSpeedEngine(nn.Module):
             return torch.optim.Adagrad(model_parameters, **params)
         if name == "sgd":
             return torch.optim.SGD(model_parameters, **params)
+        if name in ("muadam", "muadamw", "musgd"):
+            from ..ops import mup
+            cls = {"muadam": mup.MuAdam, "muadamw": mup.MuAdamW, "musgd": mup.MuSGD}[name]
+            params.pop("torch_adam", None)
+            return cls(model_parameters, **params)
         if name in ("onebitadam", "zerooneadam", "onebitlamb"):
             from .fp16.onebit import make_onebit
             return make_onebit(name, model_parameters, params, self)

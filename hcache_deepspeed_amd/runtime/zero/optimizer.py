@@ -896,15 +896,15 @@ class ZeroOptimizer:
                 p32, gr, lp = s.seg(s.master, sg), s.seg(s.grad, sg), s.seg(s.lp, sg)
                 if self.kind == "adam":
                     fused.adam_flat(p32, gr, s.seg(s.states["exp_avg"], sg), s.seg(s.states["exp_avg_sq"], sg),
-                                    g["step"], g["lr"], tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
+                                    g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
                                     g.get("weight_decay", 0.0), self.adamw, g.get("bias_correction", True),
                                     lp_out=lp, grad_scale=1.0, dev_scale=coef, found_inf=found_inf)
                 elif self.kind == "lion":
-                    fused.lion_flat(p32, gr, s.seg(s.states["exp_avg"], sg), g["lr"],
+                    fused.lion_flat(p32, gr, s.seg(s.states["exp_avg"], sg), g["lr"] * g.get("lr_mult", 1.0),
                                     tuple(g.get("betas", (0.9, 0.99))), g.get("weight_decay", 0.0), lp_out=lp,
                                     dev_scale=coef, found_inf=found_inf)
                 elif self.kind == "adagrad":
-                    fused.adagrad_flat(p32, gr, s.seg(s.states["sum"], sg), g["lr"], g.get("eps", 1e-10),
+                    fused.adagrad_flat(p32, gr, s.seg(s.states["sum"], sg), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
                                        g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
         self._post_step_gather()
         self.zero_grad()

@@ -1,0 +1,6 @@
+# GPU: re-verify the restored tree (gpu test suite + default bench)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests4.log 2>&1 || { echo "tests rc=$?" >> gpurun_out/gpu_tests4.log; exit 1; }
+timeout -k 10 400 python bench.py --steps 6 --warmup 2 > gpurun_out/bench_r4.log 2>&1
