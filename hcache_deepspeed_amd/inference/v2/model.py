@@ -28,7 +28,8 @@ import torch.nn.functional as F
 
 from ... import comm as dist
 from ...ops.activations import bias_act, glu
-from ...ops.moe import moe_combine, moe_dispatch, topk_route
+from ...ops.grouped_gemm import moe_ffn_dropless
+from ...ops.moe import moe_combine, moe_dispatch, topk_assign, topk_route
 from ...ops.norm import layer_norm, rms_norm
 from ...ops.paged import build_atoms, kv_rope_scatter, paged_attention
 from ...ops.rope import rope_tables
@@ -195,22 +196,33 @@ class RaggedTransformer:
         return F.linear(h, L["down.w"], L["down.b"])
 
     def _moe(self, L, x):
-        """Inference top-k MoE (no token dropping): dispatch into expert-major slots, batched expert GEMMs."""
+        """Inference top-k MoE (no token dropping). On the GPU: sync-free routing + two grouped GEMMs over the
+        expert-contiguous rows (ops/grouped_gemm.py, HIP kernel). Elsewhere: capacity slots + batched GEMMs."""
         m = self.spec.moe
         T, H = x.shape
         logits = F.linear(x.float(), L["router.w"].float())
         E = logits.shape[-1]
-        expert, pos, w, C, _, _ = topk_route(logits, m["top_k"], 1.0, 1, drop_tokens=False, use_rts=False,
-                                             normalize=m["normalize"], training=False)
-        disp = moe_dispatch(x, expert, pos, E, C).view(E, C, H)
-        h = torch.bmm(disp, L["w13"].transpose(1, 2))
-        y = torch.bmm(glu(h.reshape(E * C, -1), self._act_name()).view(E, C, -1), L["w2"].transpose(1, 2))
-        out = moe_combine(y.reshape(E * C, H), expert, pos, w, C)
+        w13, w2 = L["w13"], L["w2"]
+        if x.is_cuda and x.dtype == torch.bfloat16 and H % 128 == 0 and w2.shape[2] % 128 == 0:
+            # dropless grouped-GEMM path: routing stays on the device (no capacity = max(count) sync)
+            expert, pos, w, counts = topk_assign(logits, m["top_k"], normalize=m["normalize"])
+            out = moe_ffn_dropless(x, expert, pos, w, counts, w13, w2, lambda h: glu(h, self._act_name()))
+        else:
+            out = self._moe_bmm(x, logits, m, E, H, w13, w2)
         if L["shared.w13"] is not None:
             s = F.linear(glu(F.linear(x, L["shared.w13"]), self._act_name()), L["shared.w2"])
             gate = torch.sigmoid(F.linear(x.float(), L["shared_gate.w"].float())).to(s.dtype)
             out = out + gate * s
         return out
+
+    def _moe_bmm(self, x, logits, m, E, H, w13, w2):
+        """Capacity formulation: dispatch into [E, max(count), H] slots and batched expert GEMMs."""
+        expert, pos, w, C, _, _ = topk_route(logits, m["top_k"], 1.0, 1, drop_tokens=False, use_rts=False,
+                                             normalize=m["normalize"], training=False)
+        disp = moe_dispatch(x, expert, pos, E, C).view(E, C, H)
+        h = torch.bmm(disp, w13.transpose(1, 2))
+        y = torch.bmm(glu(h.reshape(E * C, -1), self._act_name()).view(E, C, -1), w2.transpose(1, 2))
+        return moe_combine(y.reshape(E * C, H), expert, pos, w, C)
 
     def _prep(self, batch):
         atoms, n_atoms = build_atoms(batch.seq_meta_host, self.n_q, self.n_kv)

@@ -55,6 +55,20 @@ def topk_route(logits, k, capacity_factor=1.0, min_capacity=4, drop_tokens=True,
     return topi.to(torch.int32).contiguous(), pos.to(torch.int32), topw.contiguous(), C, l_aux, exp_counts
 
 
+def topk_assign(logits, k, normalize=True):
+    """Sync-free top-k routing for dropless MoE: (expert [T,k] int32, pos [T,k] int32, weights [T,k] fp32,
+    counts [E] int64). ``pos`` uses the same k-major priority as :func:`topk_route`; nothing is read back to the
+    host (no capacity)."""
+    T, E = logits.shape
+    probs = torch.softmax(logits.float(), dim=-1)
+    topw, topi = torch.topk(probs, k, dim=-1)
+    if normalize and k > 1:
+        topw = topw / topw.sum(-1, keepdim=True)
+    mask = F.one_hot(topi.t().reshape(-1), E)  # [k*T, E], k-major
+    pos = ((torch.cumsum(mask, 0) - 1) * mask).sum(-1).view(k, T).t()
+    return topi.to(torch.int32).contiguous(), pos.to(torch.int32).contiguous(), topw.contiguous(), mask.sum(0)
+
+
 def _ref_dispatch(x, expert, pos, E, C):
     T, H = x.shape
     out = x.new_zeros(E * C, H)
