@@ -163,9 +163,20 @@ def stream(device=None):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_DEBUG_SYNC = os.environ.get("HDS_DEBUG_SYNC", "0") == "1"
+
+
 def check(err, what):
+    """Raise on a launch error. With ``HDS_DEBUG_SYNC=1`` (race/fault debug mode, pair with
+    ``AMD_SERIALIZE_KERNEL=3``) every native launch is followed by a device synchronize, so an asynchronous fault
+    (illegal address, assert) is attributed to the kernel that caused it instead of a later unrelated call."""
     if err != 0:
         raise RuntimeError(f"hcache_deepspeed_amd: {what} failed with hipError {err}")
+    if _DEBUG_SYNC and torch.cuda.is_available():
+        try:
+            torch.cuda.synchronize()
+        except Exception as e:  # pragma: no cover - GPU fault path
+            raise RuntimeError(f"hcache_deepspeed_amd: device fault after {what}: {e}") from e
 
 
 def use_native(*tensors):

@@ -96,6 +96,7 @@ class ZeroConfig:
     pipeline_loading_checkpoint: bool = False
     override_module_apply: bool = True
     log_trace_cache_warnings: bool = False
+    safe_mode: bool = False
 
     _ALIASES = {
         "stage3_prefetch_bucket_size": "prefetch_bucket_size",

@@ -120,6 +120,8 @@ class DeepSpeedEngine(nn.Module):
         from ..monitor.monitor import MonitorMaster
         self.monitor = MonitorMaster(cfg.monitor_config)
         dist.configure(cfg)
+        from ..utils.fault_injection import FaultInjector
+        self.fault_injector = FaultInjector(cfg.raw.get("fault_injection"))
 
         # model
         self.module = model
@@ -427,6 +429,8 @@ class DeepSpeedEngine(nn.Module):
                 self.lr_scheduler.step(**(lr_kwargs or {}))
             self.global_steps += 1
             self.global_samples += self.train_batch_size()
+            if self.fault_injector.enabled:
+                self.fault_injector.maybe_fire(dist.get_rank(), self.global_steps)
             if self.compression_scheduler is not None:
                 self.compression_scheduler.step()
                 if self._moq is not None and self.compression_scheduler.weight_quantization_enabled:

@@ -80,6 +80,21 @@ class CheckOverflow:
         return bool(flag.item())
 
 
+def assert_ints_same_as_other_ranks(ints, group=None, what="values"):
+    """Raise unless every rank of ``group`` passes the same list of ints (reference runtime/zero/utils.py:80-91,
+    used by ZeRO ``safe_mode`` to catch ranks that disagree on parameter order or sizes before a collective
+    silently mixes up their buffers)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    mine = [int(i) for i in ints]
+    allv = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allv, mine, group=group)
+    for r, v in enumerate(allv):
+        if v != mine:
+            raise RuntimeError(f"safe_mode: rank {dist.get_rank()} and group rank {r} disagree on {what}: "
+                               f"{mine[:16]}... vs {v[:16]}...")
+
+
 def see_memory_usage(message, force=False):
     if not force:
         return

@@ -21,6 +21,7 @@ What is different by design (MI355X-first):
   gradients and the optimizer shard share storage and no copy kernel runs at all.
 """
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -201,6 +202,11 @@ class ZeroOptimizer:
         self._recording = True
         self.prefetch_depth = max(0, int(self.mi.zero3_prefetch_depth))
         nparams = sum(u.numel for u in self.units)
+        if self.zcfg.safe_mode or os.environ.get("HDS_SAFE_MODE", "0") == "1":
+            # every rank must build the identical unit layout, or the flat AG/RS would exchange mismatched bytes
+            from ..utils import assert_ints_same_as_other_ranks
+            assert_ints_same_as_other_ranks([len(self.units)] + [u.numel for u in self.units] +
+                                            [self.store.numel], group=self.dp_group, what="ZeRO unit layout")
         log_dist(f"ZeRO stage {self.stage}: {len(self.units)} flat units, {nparams / 1e6:.1f}M params, "
                  f"dp={self.dp_world}, shard={self.store.numel / 1e6:.1f}M elems, optimizer={self.kind}", ranks=[0])
 
