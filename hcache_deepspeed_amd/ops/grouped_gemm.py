@@ -31,7 +31,10 @@ def _ref_grouped(x, w, offs):
     return y
 
 
-def _grouped_fwd(x, w, offs):
+_VARIANT = int(__import__("os").environ.get("HDS_GG_VARIANT", "0"))  # 0 auto, 1 = 128^2 tiles, 2 = 256^2 tiles
+
+
+def _grouped_fwd(x, w, offs, variant=None):
     T, K = x.shape
     E, N, _ = w.shape
     if native.use_native(x, w) and _eligible(x, w):
@@ -45,7 +48,8 @@ def _grouped_fwd(x, w, offs):
         lib = native.kernels()
         work = torch.empty(2 * lib.hds_grouped_gemm_max_tiles(T, E) + 1, dtype=torch.int32, device=x.device)
         native.check(lib.hds_grouped_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), offs.data_ptr(), work.data_ptr(),
-                                          T, N, K, E, N, native.stream()), "grouped_gemm")
+                                          T, N, K, E, N, _VARIANT if variant is None else variant,
+                                          native.stream()), "grouped_gemm")
         return y
     return _ref_grouped(x, w, offs)
 
@@ -72,11 +76,12 @@ class _GroupedGemm(torch.autograd.Function):
         return dx, dw, None
 
 
-def grouped_gemm(x, w, offs):
-    """x [T, K] (rows sorted by expert), w [E, N, K], offs [E+1] int (exclusive prefix, offs[E] == T) -> [T, N]."""
+def grouped_gemm(x, w, offs, variant=None):
+    """x [T, K] (rows sorted by expert), w [E, N, K], offs [E+1] int (exclusive prefix, offs[E] == T) -> [T, N].
+    ``variant`` (GPU tile shape): None/0 = auto, 1 = 128x128 tiles (small experts / decode), 2 = 256x256 tiles."""
     if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
         return _GroupedGemm.apply(x, w, offs)
-    return _grouped_fwd(x, w, offs)
+    return _grouped_fwd(x, w, offs, variant)
 
 
 def expert_offsets(counts):

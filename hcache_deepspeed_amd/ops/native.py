@@ -63,7 +63,7 @@ _KERNEL_SIGS = {
     "hds_token_sort": "p" + "ii" + "s",
     "hds_slice_mask": "i" + "ppp" + "iiiii" + "s",
     "hds_grouped_gemm_max_tiles": "ii",
-    "hds_grouped_gemm": "ppppp" + "iiiii" + "s",
+    "hds_grouped_gemm": "ppppp" + "iiiiii" + "s",
     "hds_nhwc_bias_add": "i" + "ppppp" + "l" + "ii" + "s",
 }
 

@@ -53,14 +53,15 @@ def test_grouped_gemm_autograd_cpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("counts,N,K", [([300, 0, 1, 129, 128, 77], 256, 384), ([4096, 2048], 512, 1024),
-                                        ([0, 0, 3], 128, 128)])
-def test_grouped_gemm_hip(cuda, counts, N, K):
+                                        ([0, 0, 3], 256, 128), ([513, 255, 256, 1000], 768, 256)])
+def test_grouped_gemm_hip(cuda, counts, N, K, variant):
     torch.manual_seed(2)
     E, T = len(counts), sum(counts)
     x = torch.randn(T, K, device=cuda, dtype=torch.bfloat16)
     w = torch.randn(E, N, K, device=cuda, dtype=torch.bfloat16) / K**0.5
-    y = grouped_gemm(x, w, expert_offsets(torch.tensor(counts, device=cuda)))
+    y = grouped_gemm(x, w, expert_offsets(torch.tensor(counts, device=cuda)), variant=variant)
     ref = _ref(x, w, counts)
     assert y.dtype == torch.bfloat16
     torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
