@@ -51,7 +51,8 @@ class FusedGatedMLP(nn.Module):
 
 
 class QuantizedLinear(nn.Module):
-    """Weight-only quantized linear: int8/int4 groups along the input dim, dequantized per call on the GPU."""
+    """Weight-only quantized linear: int8/int4 groups along the input dim (fused GEMV for decode, dequantize +
+    GEMM for prefill)."""
 
     def __init__(self, linear, bits=8, group_size=128):
         super().__init__()
@@ -65,8 +66,9 @@ class QuantizedLinear(nn.Module):
         self.bias = linear.bias
 
     def forward(self, x):
-        w = Q.dequantize(self.qweight, self.scales, None, self.group_size, self.bits, True, x.dtype)
-        return F.linear(x, w.view(self.out_features, self.in_features), self.bias)
+        # decode (<= 8 rows): fused int8/int4 GEMV on the packed weight; prefill: dequantize + hipBLASLt
+        return Q.int_linear(x, self.qweight, self.scales, self.out_features, self.in_features, self.group_size,
+                            self.bits, self.bias)
 
 
 def _act_name(mlp):

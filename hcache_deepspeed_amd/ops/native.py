@@ -54,6 +54,7 @@ _KERNEL_SIGS = {
     "hds_dequant_int": "i" + "pppp" + "l" + "iii" + "s",
     "hds_quant_fp8": "i" + "ppp" + "l" + "ii" + "s",
     "hds_dequant_fp8": "i" + "ppp" + "l" + "ii" + "s",
+    "hds_int_gemv": "pppp" + "iiiii" + "s",
     "hds_dequant_reduce": "i" + "ppp" + "i" + "l" + "iii" + "s",
     "hds_quant_minifloat": "i" + "ppp" + "l" + "iiiii" + "s",
     "hds_dequant_minifloat": "i" + "ppp" + "l" + "iii" + "s",
