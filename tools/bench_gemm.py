@@ -2,7 +2,7 @@
 import torch
 import time
 
-T = 16384
+T = 24576
 shapes = {"qkv": (4096, 6144), "o": (4096, 4096), "gate_up": (4096, 28672), "down": (14336, 4096),
           "lm_head_chunk": (4096, 128256)}
 
