@@ -106,7 +106,7 @@ def build_host(force=False, verbose=False):
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = HOST_LIB + ".tmp"
     _run(["g++", *HOST_FLAGS, "-shared", *srcs, "-o", tmp, f"-L{ROCM}/lib", "-lamdhip64",
-          f"-Wl,-rpath,{ROCM}/lib", "-lpthread"])
+          f"-Wl,-rpath,{ROCM}/lib", "-lpthread", "-ldl"])
     os.replace(tmp, HOST_LIB)
     with open(HOST_LIB + ".sha256", "w") as f:
         f.write(digest)

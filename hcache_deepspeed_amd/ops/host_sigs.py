@@ -38,6 +38,21 @@ SIGS = {
     "hds_aio_pwrite": (I, [P, P, L, ctypes.c_char_p, L, I]),
     "hds_aio_wait": (L, [P]),
     "hds_aio_file_size": (L, [ctypes.c_char_p]),
+    # rccl_comm.cpp
+    "hds_rccl_load": (I, [ctypes.c_char_p]),
+    "hds_rccl_error_string": (ctypes.c_char_p, [I]),
+    "hds_rccl_unique_id": (I, [ctypes.c_char_p]),
+    "hds_rccl_init": (P, [ctypes.c_char_p, I, I, P, ctypes.POINTER(I)]),
+    "hds_rccl_destroy": (I, [P]),
+    "hds_rccl_stream": (P, [P]),
+    "hds_rccl_all_gather": (I, [P, P, P, Z, I, P, ctypes.POINTER(I)]),
+    "hds_rccl_reduce_scatter": (I, [P, P, P, Z, I, I, P, ctypes.POINTER(I)]),
+    "hds_rccl_all_reduce": (I, [P, P, P, Z, I, I, P, ctypes.POINTER(I)]),
+    "hds_rccl_broadcast": (I, [P, P, P, Z, I, I, P, ctypes.POINTER(I)]),
+    "hds_rccl_all_to_all": (I, [P, P, P, Z, I, I, P, ctypes.POINTER(I)]),
+    "hds_rccl_wait": (I, [P, I, P]),
+    "hds_rccl_query": (I, [P, I]),
+    "hds_rccl_synchronize": (I, [P]),
 }
 
 

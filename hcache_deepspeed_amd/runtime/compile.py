@@ -34,7 +34,7 @@ _FIELDS = {
     "deepcompile": False, "free_activation": False, "offload_activation": False, "offload_opt_states": False,
     "double_buffer": True, "symmetric_memory": False, "debug_log": False, "offload_parameters": False,
     "sync_before_reduce": False, "sync_after_reduce": False, "sync_before_allgather": False,
-    "sync_after_allgather": False
+    "sync_after_allgather": False, "native_comm": False
 }
 
 _user_passes = {}
@@ -83,6 +83,12 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
     if cfg.offload_parameters and not engine._config.zero_config.offload_param.enabled:
         logger.warning("compile: offload_parameters requires zero_optimization.offload_param at initialize(); "
                        "parameters stay on device")
+    t0 = time.perf_counter()
+    if cfg.native_comm and engine.optimizer is not None and hasattr(engine.optimizer, "enable_native_comm"):
+        # DeepCompile's private-communicator path (reference csrc/compile/deepcompile.cpp): ZeRO all-gathers and
+        # reduce-scatters go through the C++ RCCL executor (comm/native_rccl.py) on its own priority stream
+        engine.optimizer.enable_native_comm()
+    times["native_comm"] = time.perf_counter() - t0
     if cfg.symmetric_memory:
         logger.warning("compile: symmetric_memory has no RCCL equivalent here; ignored")
     for name, fn in _user_passes.items():

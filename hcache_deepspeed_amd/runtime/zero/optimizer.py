@@ -619,6 +619,40 @@ class ZeroOptimizer:
         full.record_stream(s)
         return work
 
+    # ------------------------------------------------------------------------------------
+    # collectives: torch.distributed (RCCL via c10d) or the native C++ RCCL executor
+    # ------------------------------------------------------------------------------------
+    def enable_native_comm(self):
+        """Route the unit all-gathers / reduce-scatters through comm/native_rccl.py (one private RCCL
+        communicator per process group, priority comm stream, GPU-side event ordering). GPU only."""
+        if self.device.type != "cuda":
+            log_dist("native_comm: CPU run, keeping torch.distributed", ranks=[0])
+            return False
+        self._native = {}
+        return True
+
+    def _ncomm(self, group):
+        cache = getattr(self, "_native", None)
+        if cache is None:
+            return None
+        key = id(group)
+        if key not in cache:
+            from ...comm.native_rccl import RcclCommunicator
+            cache[key] = RcclCommunicator(group)
+        return cache[key]
+
+    def _all_gather(self, out, inp, group):
+        c = self._ncomm(group)
+        if c is not None:
+            return c.all_gather_into_tensor(out, inp, async_op=True)
+        return dist.all_gather_into_tensor(out, inp, group=group, async_op=True)
+
+    def _reduce_scatter(self, out, inp, group):
+        c = self._ncomm(group)
+        if c is not None:
+            return c.reduce_scatter_tensor(out, inp, async_op=True)
+        return dist.reduce_scatter_tensor(out, inp, group=group, async_op=True)
+
     def _gather(self, u, wait=True):
         if u.status == NOT_AVAILABLE:
             full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
@@ -631,7 +665,7 @@ class ZeroOptimizer:
             elif self.qwz and u.expert_key is None:
                 u.work, u.post_gather = self._qwz_gather(u, full)
             else:
-                u.work = dist.all_gather_into_tensor(full, u.shard_tensor, group=u.ag_group, async_op=True)
+                u.work = self._all_gather(full, u.shard_tensor, u.ag_group)
             u.full = full
             u.bind_params(full)
             u.status = INFLIGHT
@@ -764,11 +798,11 @@ class ZeroOptimizer:
             self._after_reduce(u, src, w, post, (src, tmp))
             return
         if first and dst.dtype == self.comm_dtype:
-            w = dist.reduce_scatter_tensor(dst, src, group=u.rs_group, async_op=True)
+            w = self._reduce_scatter(dst, src, u.rs_group)
             post = None
         else:
             tmp = torch.empty(u.shard, dtype=self.comm_dtype, device=self.device)
-            w = dist.reduce_scatter_tensor(tmp, src, group=u.rs_group, async_op=True)
+            w = self._reduce_scatter(tmp, src, u.rs_group)
             if first:
                 post = (lambda d=dst, t=tmp: d.copy_(t))
             else:
