@@ -159,8 +159,7 @@ class InferenceEngineV2:
         if not lat:
             return
         batch.finalize()
-        latents = torch.cat(lat, dim=1)
-        self._model.restore_kv(batch, latents)
+        self._model.restore_kv(batch, lat)  # per-sequence pinned pieces, copied straight to the device
         for uid in restored:
             sm.get_sequence(uid).post_forward()
 

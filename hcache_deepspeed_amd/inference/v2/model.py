@@ -310,16 +310,24 @@ class RaggedTransformer:
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
     def restore_kv(self, batch, latents):
-        """Rebuild the paged KV of ``batch``'s sequences from host latents [L, T, W] (pinned preferred)."""
+        """Rebuild the paged KV of ``batch``'s sequences from host latents: one [L, T, W] tensor or a list of
+        per-sequence [L, n_s, W] pieces in batch order (pinned preferred). Pieces are copied straight into the
+        device layer buffer at their row offsets: no host-side concatenation (a pageable temporary that would also
+        have to be re-pinned — 2 extra host copies of every latent byte)."""
         T = batch.current_tokens
         L_ = self.spec.num_hidden_layers
+        pieces = list(latents) if isinstance(latents, (list, tuple)) else [latents]
         if self.copy_stream is None:
             for i, L in enumerate(self.layers):
-                self._restore_layer(i, L, latents[i].to(self.device), batch, T)
+                x = torch.cat([p[i] for p in pieces], 0) if len(pieces) > 1 else pieces[0][i]
+                self._restore_layer(i, L, x.to(self.device), batch, T)
             return
-        if not latents.is_pinned() and latents.device.type == "cpu":
-            latents = latents.pin_memory()
-        width = latents.shape[-1]
+        pieces = [p if p.device.type != "cpu" or p.is_pinned() else p.pin_memory() for p in pieces]
+        offs = [0]
+        for p in pieces:
+            offs.append(offs[-1] + p.shape[1])
+        assert offs[-1] == T, "latents must cover exactly the batch's tokens"
+        width = pieces[0].shape[-1]
         bufs = [torch.empty(T, width, dtype=self.dtype, device=self.device) for _ in range(2)]
         loaded = [torch.cuda.Event() for _ in range(2)]
         freed = [torch.cuda.Event() for _ in range(2)]
@@ -330,7 +338,8 @@ class RaggedTransformer:
             with torch.cuda.stream(self.copy_stream):
                 if i >= 2:
                     self.copy_stream.wait_event(freed[b])
-                bufs[b].copy_(latents[i], non_blocking=True)
+                for p, o0, o1 in zip(pieces, offs[:-1], offs[1:]):
+                    bufs[b][o0:o1].copy_(p[i], non_blocking=True)
                 loaded[b].record(self.copy_stream)
 
         issue(0)

@@ -1,0 +1,102 @@
+"""HCache serving benchmark (the fork's feature): how fast a sequence's KV cache comes back.
+
+Llama-3-8B (random bf16 weights, full 32 layers) in the ragged serving engine on one MI355X. A batch of contexts
+is prefilled, evicted, and brought back three ways:
+
+* recompute   — full prefill again (``put`` without latent capture),
+* HCache      — ``restore_kv`` from the per-layer hidden-state latents kept in pinned host memory
+                (H2D of layer i+1 overlapped with layer i's QKV GEMM + fused RoPE/paged-KV scatter),
+* KV offload  — ``restore_kv`` in ``latent_mode="kv"`` (pre-RoPE K|V rows on the host; RoPE + scatter only).
+
+Reports restored tokens/s and host bytes per token for each, plus the cost of capturing latents during prefill.
+
+    python tools/bench_hcache.py [--seqs 8] [--ctx 2048]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seqs", type=int, default=8)
+    ap.add_argument("--ctx", type=int, default=2048)
+    ap.add_argument("--layers", type=int, default=0)
+    args = ap.parse_args()
+    from hcache_deepspeed_amd.inference.v2 import build_engine_from_model
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, llama3_8b
+
+    dev = torch.device("cuda", 0)
+    cfg = llama3_8b() if not args.layers else llama3_8b(num_hidden_layers=args.layers)
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = LlamaForCausalLM(cfg).to(torch.bfloat16).eval()
+    S, C = args.seqs, args.ctx
+    n_tok = S * C
+    blocks = S * ((C + 63) // 64) + 16
+    econf = {"dtype": "bf16", "state_manager": {"max_ragged_batch_size": n_tok, "max_context": C + 64,
+                                                 "kv_block_size": 64, "max_tracked_sequences": 4 * S}}
+    g = torch.Generator().manual_seed(1)
+    prompts = [torch.randint(0, cfg.vocab_size, (C, ), generator=g) for _ in range(S)]
+    uids = list(range(1, S + 1))
+    res = {}
+    for mode in ("hidden", "kv"):
+        eng = build_engine_from_model(model, dict(econf, latent_mode=mode), device=dev, num_kv_blocks=blocks)
+
+        def prefill(capture):
+
+            def f():
+                for u in uids:
+                    eng.flush(u)
+                return eng.put(uids, prompts, capture_latents=capture)
+
+            return f
+
+        if mode == "hidden":
+            res["recompute (prefill)"] = timed(prefill(False))
+            res["prefill + latent capture"] = timed(prefill(True))
+        _, lats = prefill(True)()
+        torch.cuda.synchronize()
+        lat_bytes = sum(x.numel() * x.element_size() for x in lats)
+        assert all(x.is_pinned() for x in lats), "latents must live in pinned host memory"
+
+        def restore():
+            for u in uids:
+                eng.evict(u)
+            eng.restore_kv(uids, prompts, lats)
+
+        res[f"restore_kv latent_mode={mode}"] = timed(restore)
+        res[f"host bytes/token latent_mode={mode}"] = lat_bytes / n_tok
+        del eng, lats
+        torch.cuda.empty_cache()
+    print(f"Llama-3-8B ({cfg.num_hidden_layers} layers) bf16, {S} sequences x {C} tokens = {n_tok} tokens")
+    for k, v in res.items():
+        if k.startswith("host bytes"):
+            print(f"  {k:40s} {v / 1024:8.1f} KiB")
+        else:
+            print(f"  {k:40s} {v * 1e3:8.1f} ms  {n_tok / v:10.0f} tokens/s")
+    rc = res["recompute (prefill)"]
+    print(f"  HCache restore speedup vs recompute: {rc / res['restore_kv latent_mode=hidden']:.2f}x; "
+          f"KV-offload restore speedup vs recompute: {rc / res['restore_kv latent_mode=kv']:.2f}x")
+
+
+if __name__ == "__main__":
+    main()
