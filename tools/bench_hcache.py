@@ -40,12 +40,14 @@ def main():
     ap.add_argument("--seqs", type=int, default=8)
     ap.add_argument("--ctx", type=int, default=2048)
     ap.add_argument("--layers", type=int, default=0)
+    ap.add_argument("--model", default="llama3-8b", help="llama3-8b (GQA 32/8) or llama2-7b (MHA)")
     args = ap.parse_args()
     from hcache_deepspeed_amd.inference.v2 import build_engine_from_model
-    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, llama3_8b
+    from hcache_deepspeed_amd.models.llama import PRESETS, LlamaForCausalLM
 
     dev = torch.device("cuda", 0)
-    cfg = llama3_8b() if not args.layers else llama3_8b(num_hidden_layers=args.layers)
+    preset = PRESETS[args.model]
+    cfg = preset() if not args.layers else preset(num_hidden_layers=args.layers)
     torch.manual_seed(0)
     with torch.device(dev):
         model = LlamaForCausalLM(cfg).to(torch.bfloat16).eval()
@@ -87,7 +89,7 @@ def main():
         res[f"host bytes/token latent_mode={mode}"] = lat_bytes / n_tok
         del eng, lats
         torch.cuda.empty_cache()
-    print(f"Llama-3-8B ({cfg.num_hidden_layers} layers) bf16, {S} sequences x {C} tokens = {n_tok} tokens")
+    print(f"{args.model} ({cfg.num_hidden_layers} layers, {cfg.num_attention_heads}/{cfg.num_key_value_heads} heads) bf16, {S} sequences x {C} tokens = {n_tok} tokens")
     for k, v in res.items():
         if k.startswith("host bytes"):
             print(f"  {k:40s} {v / 1024:8.1f} KiB")
