@@ -7,7 +7,9 @@ Reference parity: ops/deepspeed4science/evoformer_attn.py (``DS4Sci_EvoformerAtt
 Shapes: Q/K/V ``[B, N, L, H, D]``; ``bias1 = [B, N, 1, 1, L]`` (MSA mask, broadcast over heads and queries);
 ``bias2 = [B, 1, H, L, L]`` (pair bias, broadcast over the N rows). Output ``[B, N, L, H, D]``.
 
-Implementation: memory-efficient flash-style decomposition -- the forward keeps only the fp32 log-sum-exp per
+Forward on the GPU (bf16, head_dim 32/64/128): the HIP kernel csrc/kernels/evoformer.hip (MFMA 32x32x16 flash
+attention with both biases fused, emits the LSE). Elsewhere, and for the backward: a memory-efficient flash-style
+decomposition -- the forward keeps only the fp32 log-sum-exp per
 query, the backward recomputes the probabilities one query chunk at a time, so peak memory is O(chunk x L)
 instead of O(L^2) per (B, N, H). The per-chunk products run as batched GEMMs on the matrix cores; head_dim is
 arbitrary (Evoformer uses 16-64, below the 128 the FlashAttention HIP kernel is tiled for). Bias gradients
@@ -34,6 +36,30 @@ def _scores(q, k, b1, b2, i0, i1, scale):
     return s
 
 
+def _hip_eligible(q, k, v, b1, b2):
+    from .. import native
+    if not native.use_native(q):
+        return False
+    ok_b = all(b is None or (b.dtype in (torch.bfloat16, torch.float32) and b.is_contiguous()) for b in (b1, b2))
+    same_b = b1 is None or b2 is None or b1.dtype == b2.dtype
+    return (q.dtype == k.dtype == v.dtype == torch.bfloat16 and q.shape[-1] in (32, 64, 128) and ok_b and same_b
+            and all(x.is_contiguous() for x in (q, k, v)))
+
+
+def _hip_forward(q, k, v, b1, b2, scale):
+    """HIP forward (csrc/kernels/evoformer.hip): O [B, N, L, H, D] and the natural-log LSE [B, N, H, L]."""
+    from .. import native
+    B, N, L, H, D = q.shape
+    o = torch.empty_like(q)
+    lse = torch.empty(B, N, H, L, dtype=torch.float32, device=q.device)
+    bdt = (b1 if b1 is not None else b2)
+    bdt = native.dt(bdt) if bdt is not None else 1
+    native.check(native.kernels().hds_evoformer_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), native.ptr(b1),
+                                                    native.ptr(b2), bdt, o.data_ptr(), lse.data_ptr(), B, N, L, H,
+                                                    D, float(scale), native.stream()), "evoformer_fwd")
+    return o, lse
+
+
 class EvoformerFusedAttention(torch.autograd.Function):
 
     @staticmethod
@@ -42,6 +68,11 @@ class EvoformerFusedAttention(torch.autograd.Function):
         qh, kh, vh = (x.transpose(-2, -3) for x in (q, k, v))
         B, N, H, L, D = qh.shape
         scale = 1.0 / math.sqrt(D)
+        if _hip_eligible(q, k, v, bias1, bias2):
+            o, lse = _hip_forward(q, k, v, bias1, bias2, scale)
+            ctx.save_for_backward(qh, kh, vh, o.transpose(-2, -3), lse, bias1, bias2)
+            ctx.scale = scale
+            return o
         o = torch.empty(qh.shape, dtype=q.dtype, device=q.device)
         lse = torch.empty(B, N, H, L, dtype=torch.float32, device=q.device)
         c = _chunk_rows(B, N, H, L)

@@ -65,6 +65,7 @@ _KERNEL_SIGS = {
     "hds_slice_mask": "i" + "ppp" + "iiiii" + "s",
     "hds_grouped_gemm_max_tiles": "ii",
     "hds_grouped_gemm": "ppppp" + "iiiiii" + "s",
+    "hds_evoformer_fwd": "ppppp" + "i" + "pp" + "iiiii" + "f" + "s",
     "hds_nhwc_bias_add": "i" + "ppppp" + "l" + "ii" + "s",
 }
 
