@@ -1,0 +1,6 @@
+# GPU: full gpu test suite + smoke()
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_full.log 2>&1 || { echo "tests rc=$?" >> gpurun_out/gpu_tests_full.log; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1
