@@ -118,8 +118,10 @@ class NebulaCheckpointEngine(AsyncCheckpointEngine):
         self._written.setdefault(self._tag, []).append(path)
         super().save(state_dict, path)
 
-    def _persist(self, tag, files):
+    def _persist(self, tag, files, prev=None):
         import shutil
+        if prev is not None:  # persist in commit order, so retention always drops the OLDEST tags
+            prev.join()
         dst = os.path.join(self.persistent_path, str(tag))
         os.makedirs(dst, exist_ok=True)
         for f in files:
@@ -133,7 +135,8 @@ class NebulaCheckpointEngine(AsyncCheckpointEngine):
         files = self._written.pop(tag, [])
         self._commits += 1
         if self.persistent_path and files and self._commits % self.interval == 0:
-            t = threading.Thread(target=self._persist, args=(tag, files), daemon=False)
+            prev = self._persist_threads[-1] if self._persist_threads else None
+            t = threading.Thread(target=self._persist, args=(tag, files, prev), daemon=False)
             t.start()
             self._persist_threads.append(t)
         return True
