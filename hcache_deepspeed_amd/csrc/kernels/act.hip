@@ -19,7 +19,7 @@ enum Act : int { kSilu = 0, kGeluTanh = 1, kRelu = 2, kGeluErf = 3, kIdentity = 
 
 template <int A>
 __device__ __forceinline__ float act_f(float x) {
-  if constexpr (A == kSilu) return x / (1.f + __expf(-x));
+  if constexpr (A == kSilu) return x * __builtin_amdgcn_rcpf(1.f + __expf(-x));
   if constexpr (A == kGeluTanh) {
     const float k0 = 0.7978845608028654f, k1 = 0.044715f;
     return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
@@ -31,7 +31,7 @@ __device__ __forceinline__ float act_f(float x) {
 template <int A>
 __device__ __forceinline__ float act_grad(float x) {
   if constexpr (A == kSilu) {
-    const float s = 1.f / (1.f + __expf(-x));
+    const float s = __builtin_amdgcn_rcpf(1.f + __expf(-x));
     return s * (1.f + x * (1.f - s));
   }
   if constexpr (A == kGeluTanh) {
@@ -49,14 +49,43 @@ __device__ __forceinline__ float act_grad(float x) {
   return 1.f;
 }
 
+// act(x) and act'(x) together: SiLU shares one exp + one v_rcp between value and derivative (the
+// backward is VALU-bound at Llama MLP sizes, so the precise-division sigmoid was the hot spot).
+template <int A>
+__device__ __forceinline__ void act_val_grad(float x, float& a, float& g) {
+  if constexpr (A == kSilu) {
+    const float s = __builtin_amdgcn_rcpf(1.f + __expf(-x));
+    a = x * s;
+    g = s * (1.f + x * (1.f - s));
+  } else {
+    a = act_f<A>(x);
+    g = act_grad<A>(x);
+  }
+}
+
+// Flat vector index -> (row, column) with 32-bit division when the problem fits (the 64-bit
+// division is a ~40-instruction software sequence per 8 elements).
+__device__ __forceinline__ void split_idx(int64_t idx, int vpr, bool small, int64_t& r, int& c) {
+  if (small) {
+    const unsigned q = (unsigned)idx / (unsigned)vpr;
+    r = q;
+    c = (int)((unsigned)idx - q * (unsigned)vpr) * 8;
+  } else {
+    r = idx / vpr;
+    c = (int)(idx - r * vpr) * 8;
+  }
+}
+
 // y[t, i] = act(g[t, i]) * u[t, i]     g = gu[t, 0:I], u = gu[t, I:2I]
 template <typename T, int A>
 __global__ __launch_bounds__(256) void glu_fwd(const T* __restrict__ gu, T* __restrict__ y, int64_t rows, int I) {
   const int vpr = I / 8;
   const int64_t total = rows * vpr;
+  const bool small = total < (int64_t)0x7fffffff;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int64_t r = idx / vpr;
-    const int c = (int)(idx - r * vpr) * 8;
+    int64_t r;
+    int c;
+    split_idx(idx, vpr, small, r, c);
     float g[8], u[8], o[8];
     Vec8<T>::load(gu + r * 2 * I + c, g);
     Vec8<T>::load(gu + r * 2 * I + I + c, u);
@@ -71,17 +100,21 @@ __global__ __launch_bounds__(256) void glu_bwd(const T* __restrict__ dy, const T
                                                T* __restrict__ dgu, int64_t rows, int I) {
   const int vpr = I / 8;
   const int64_t total = rows * vpr;
+  const bool small = total < (int64_t)0x7fffffff;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int64_t r = idx / vpr;
-    const int c = (int)(idx - r * vpr) * 8;
+    int64_t r;
+    int c;
+    split_idx(idx, vpr, small, r, c);
     float g[8], u[8], d[8], dg[8], du[8];
     Vec8<T>::load(gu + r * 2 * I + c, g);
     Vec8<T>::load(gu + r * 2 * I + I + c, u);
     Vec8<T>::load(dy + r * I + c, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      du[j] = d[j] * act_f<A>(g[j]);
-      dg[j] = d[j] * u[j] * act_grad<A>(g[j]);
+      float a, ga;
+      act_val_grad<A>(g[j], a, ga);
+      du[j] = d[j] * a;
+      dg[j] = d[j] * u[j] * ga;
     }
     Vec8<T>::store(dgu + r * 2 * I + c, dg);
     Vec8<T>::store(dgu + r * 2 * I + I + c, du);
@@ -94,9 +127,11 @@ __global__ __launch_bounds__(256) void bias_act_fwd(const T* __restrict__ x, con
                                                     T* __restrict__ y, int64_t rows, int C) {
   const int vpr = C / 8;
   const int64_t total = rows * vpr;
+  const bool small = total < (int64_t)0x7fffffff;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int64_t r = idx / vpr;
-    const int c = (int)(idx - r * vpr) * 8;
+    int64_t r;
+    int c;
+    split_idx(idx, vpr, small, r, c);
     float v[8], b[8] = {0, 0, 0, 0, 0, 0, 0, 0}, o[8];
     Vec8<T>::load(x + r * C + c, v);
     if (bias) Vec8<T>::load(bias + c, b);
@@ -113,9 +148,11 @@ __global__ __launch_bounds__(256) void bias_act_bwd(const T* __restrict__ dy, co
                                                     int C) {
   const int vpr = C / 8;
   const int64_t total = rows * vpr;
+  const bool small = total < (int64_t)0x7fffffff;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int64_t r = idx / vpr;
-    const int c = (int)(idx - r * vpr) * 8;
+    int64_t r;
+    int c;
+    split_idx(idx, vpr, small, r, c);
     float v[8], b[8] = {0, 0, 0, 0, 0, 0, 0, 0}, d[8], o[8];
     Vec8<T>::load(x + r * C + c, v);
     Vec8<T>::load(dy + r * C + c, d);
