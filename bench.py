@@ -70,9 +70,16 @@ def main():
     else:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=os.environ.get("MASTER_PORT", "29533"))
-    hds.init_distributed(verbose=False)
+    on_gpu = torch.cuda.is_available()
+    # no GPU: a CPU/gloo dry run of the same multi-rank code path (timing/all-reduce/JSON), never a result
+    hds.init_distributed(dist_backend=None if on_gpu else "gloo", verbose=False)
     rank = tdist.get_rank()
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if on_gpu:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     overrides = {}
     if args.model.startswith("gpt2"):
@@ -117,12 +124,12 @@ def main():
     S, mb = args.seq, args.micro_batch
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
-    batches = [torch.randint(0, cfg_model.vocab_size, (mb, S), device=dev, generator=gen) for _ in range(4)]
 
     def train_step(i):
         loss = None
         for g in range(args.gas):
-            x = batches[(i * args.gas + g) % len(batches)]
+            # a fresh synthetic batch every micro-step (no fixed batches to memorise)
+            x = torch.randint(0, cfg_model.vocab_size, (mb, S), device=dev, generator=gen)
             loss = engine(x, labels=x)
             engine.backward(loss)
             engine.step()
@@ -131,15 +138,15 @@ def main():
     loss = None
     for i in range(args.warmup):
         loss = train_step(i)
-    torch.cuda.synchronize()
+    sync()
     tdist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = train_step(args.warmup + i)
-    torch.cuda.synchronize()
+    sync()
     tdist.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
     tdist.all_reduce(dt_t, op=tdist.ReduceOp.MAX)
@@ -150,7 +157,7 @@ def main():
     flops = (cfg_model.flops_per_token(S) if hasattr(cfg_model, "flops_per_token") else
              6 * cfg_model.active_params() + 12 * cfg_model.num_hidden_layers * S * cfg_model.hidden_size) * tokens
     mfu = flops / dt / (2.5e15 * world)
-    mem = torch.cuda.max_memory_allocated(dev) / 2**30
+    mem = torch.cuda.max_memory_allocated(dev) / 2**30 if on_gpu else 0.0
     if rank == 0:
         out = {
             "metric": ("tokens/sec (node) Llama-3-8B ZeRO-3 at 1/2/4/8 MI355X" if args.model == "llama3-8b" else
@@ -174,7 +181,8 @@ def main():
                        "activation_checkpointing": bool(args.ckpt)},
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
                       "final_loss": round(float(loss.item()), 4), "peak_mem_gib": round(mem, 1),
-                      "init_s": round(t_init, 1), "valid": not bool(args.layers), "tuned_gemm_table": tuned},
+                      "init_s": round(t_init, 1), "valid": on_gpu and not bool(args.layers),
+                      "tuned_gemm_table": tuned, "device": "mi355x" if on_gpu else "cpu-dry-run"},
         }
         print(json.dumps(out), flush=True)
     tdist.barrier()

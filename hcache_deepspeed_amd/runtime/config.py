@@ -10,6 +10,7 @@ MI355X-specific knobs live under ``"mi355x"``::
     "mi355x": {
         "xgmi_bucket_mb": 256,          # default ZeRO-1/2 bucket / ZeRO-3 prefetch granularity
         "zero3_prefetch_depth": 2,      # units all-gathered ahead of compute
+        "zero3_max_reduce_inflight": 2, # gradient reduce-scatters in flight before the oldest is retired
         "host_act_cache": {"enabled": false, "slots": 8, "slot_mb": 512, "min_layers_resident": 2},
         "fused_lm_head_ce": true
     }
@@ -174,6 +175,7 @@ class HostActCacheConfig:
 class MI355XConfig:
     xgmi_bucket_mb: int = 256
     zero3_prefetch_depth: int = 2
+    zero3_max_reduce_inflight: int = 2
     fused_lm_head_ce: bool = True
     host_act_cache: HostActCacheConfig = field(default_factory=HostActCacheConfig)
 
@@ -291,6 +293,7 @@ class DeepSpeedConfig:
         hac = m.get("host_act_cache") or {}
         self.mi355x = MI355XConfig(
             xgmi_bucket_mb=int(m.get("xgmi_bucket_mb", 256)), zero3_prefetch_depth=int(m.get("zero3_prefetch_depth", 2)),
+            zero3_max_reduce_inflight=int(m.get("zero3_max_reduce_inflight", 2)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
             host_act_cache=HostActCacheConfig(**{f.name: hac[f.name]
                                                  for f in fields(HostActCacheConfig) if f.name in hac}))

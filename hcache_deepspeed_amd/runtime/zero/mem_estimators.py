@@ -20,14 +20,21 @@ def model_to_params(model):
 
 
 def estimate(total_params, stage, world, largest_unit_params=0, offload_optimizer=False, offload_param=False,
-             grad_accum_fp32=False, prefetch_depth=2):
-    """Returns (gpu_bytes, cpu_bytes) of model states per rank."""
+             grad_accum_fp32=False, prefetch_depth=2, reduce_inflight=2, root_params=0):
+    """Returns (gpu_bytes, cpu_bytes) of model states per rank.
+
+    ZeRO-3 working set at dp>1 (runtime/zero/optimizer.py): (prefetch_depth + 1) gathered units, the current
+    unit's unsharded gradient plus ``reduce_inflight`` gradients still in a reduce-scatter, and the persistent
+    root unit (embeddings / LM head / final norm: ``root_params``) gathered with its unsharded gradient."""
     P, W = float(total_params), max(1, world)
     g = 4.0 if grad_accum_fp32 else 2.0
     lp = 2 * P / W if stage == 3 else 2 * P
     grad = g * P / W if stage >= 2 else g * P
     opt = 12 * P / W if stage >= 1 else 12 * P
-    work = 2 * largest_unit_params * (prefetch_depth + 1) if stage == 3 else 0
+    work = 0
+    if stage == 3 and W > 1:
+        work = 2 * largest_unit_params * (prefetch_depth + 1) + 2 * largest_unit_params * (1 + reduce_inflight)
+        work += 2 * root_params + 2 * root_params
     cpu = 0.0
     if offload_optimizer:
         cpu += opt
@@ -94,3 +101,35 @@ def estimate_zero3_model_states_mem_needs_all_live(model, num_gpus_per_node=1, n
 def estimate_zero3_model_states_mem_needs_all_cold(total_params, largest_layer_params, num_gpus_per_node=1,
                                                    num_nodes=1, additional_buffer_factor=1.5):
     return _all(total_params, largest_layer_params, 3, num_gpus_per_node, num_nodes, additional_buffer_factor)
+
+
+def llama_activation_bytes(cfg, tokens, ckpt=False):
+    """Saved-activation bytes of one micro-batch of ``tokens`` tokens through models/llama.py (bf16, fused
+    FlashAttention saving O + LSE, fused SwiGLU saving its input, chunked fused LM-head CE saving nothing
+    of size V). Per layer and token: block input, the two RMSNorm outputs, Q|K|V, the attention output,
+    the MLP residual input, gate|up and the SwiGLU output (H*6 + 3*I + 2*KV elements). With activation
+    checkpointing only the block input survives. Calibrated against the measured 1-GPU bench
+    (Llama-3-8B, mb7, seq 4096: 244.5 GiB peak = 119.6 GiB states + ~125 GiB activations/workspace)."""
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    kv = cfg.num_key_value_heads * cfg.head_dim
+    per = H if ckpt else 6 * H + 3 * I + 2 * kv
+    return 2 * per * cfg.num_hidden_layers * tokens
+
+
+def estimate_llama_training(cfg, micro_batch, seq, world, stage=3, prefetch_depth=2, reduce_inflight=2,
+                            offload_optimizer=False, offload_param=False, ckpt=False, hbm_gib=268.0):
+    """Per-GPU HBM plan for one of the bench configs: model states + ZeRO-3 working set + activations.
+    Returns a dict of GiB figures and whether it fits in ``hbm_gib`` (MI355X: 288 GB HBM3E, of which
+    torch sees 268 GiB)."""
+    H, V, L = cfg.hidden_size, cfg.vocab_size, cfg.num_hidden_layers
+    kv = cfg.num_key_value_heads * cfg.head_dim
+    layer = H * (cfg.num_attention_heads * cfg.head_dim + 2 * kv) + cfg.num_attention_heads * cfg.head_dim * H \
+        + 3 * H * cfg.intermediate_size + 2 * H
+    root = V * H * (1 if getattr(cfg, "tie_word_embeddings", False) else 2) + H
+    total = layer * L + root
+    gpu, cpu = estimate(total, stage, world, layer, offload_optimizer, offload_param, False, prefetch_depth,
+                        reduce_inflight, root)
+    act = llama_activation_bytes(cfg, micro_batch * seq, ckpt)
+    tot = gpu + act
+    return {"params_b": total / 1e9, "states_gib": gpu / GB, "activations_gib": act / GB, "total_gib": tot / GB,
+            "host_gib": cpu / GB, "fits": tot / GB <= hbm_gib}

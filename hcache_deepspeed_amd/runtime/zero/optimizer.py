@@ -201,6 +201,25 @@ class ZeroOptimizer:
         self._fwd_trace, self._trace_ok, self._trace_pos = [], False, 0
         self._recording = True
         self.prefetch_depth = max(0, int(self.mi.zero3_prefetch_depth))
+        # parameter-coordinator policy (reference partitioned_param_coordinator.py:380-441,524-555 and
+        # stage3.py:372 max_param_reduce_events). The byte / live / reuse limits apply only when the user's
+        # config names them: on a 288 GB MI355X the depth-bounded default already fits every baseline config.
+        self.max_reduce_inflight = max(1, int(getattr(self.mi, "zero3_max_reduce_inflight", 2)))
+        zraw = config.raw.get("zero_optimization") or {}
+
+        def _explicit(*keys):
+            return any(k in zraw for k in keys)
+
+        self.prefetch_numel = (int(self.zcfg.prefetch_bucket_size)
+                               if _explicit("stage3_prefetch_bucket_size", "prefetch_bucket_size") else None)
+        self.max_live_numel = (int(self.zcfg.max_live_parameters)
+                               if _explicit("stage3_max_live_parameters", "max_live_parameters") else None)
+        self.max_reuse_distance = (int(self.zcfg.max_reuse_distance)
+                                   if _explicit("stage3_max_reuse_distance", "max_reuse_distance") else None)
+        self._reuse_keep = set()
+        self.pending_rs = []  # ZeRO-3 partitioned-unit reduce-scatters: bounded by max_reduce_inflight
+        self.track_live = os.environ.get("HDS_ZERO_TRACK_LIVE", "0") == "1"
+        self.live_peak_bytes = 0
         nparams = sum(u.numel for u in self.units)
         if self.zcfg.safe_mode or os.environ.get("HDS_SAFE_MODE", "0") == "1":
             # every rank must build the identical unit layout, or the flat AG/RS would exchange mismatched bytes
@@ -550,7 +569,8 @@ class ZeroOptimizer:
             grad_on = torch.is_grad_enabled()
             if grad_on and not self.in_backward:
                 output = self._wrap_outputs(u, output)
-            if self._partitioned(u) and not self.in_backward and not self._is_last_in_trace(u):
+            if self._partitioned(u) and not self.in_backward and not self._is_last_in_trace(u) and \
+                    u.uid not in self._reuse_keep:
                 self._release(u)
             return output
 
@@ -669,6 +689,7 @@ class ZeroOptimizer:
             u.full = full
             u.bind_params(full)
             u.status = INFLIGHT
+            self._note_live()
         if wait and u.status == INFLIGHT:
             u.work.wait()
             u.work = None
@@ -676,9 +697,11 @@ class ZeroOptimizer:
                 u.post_gather()
                 u.post_gather = None
             u.status = AVAILABLE
-        if self.in_backward and u.grad_full is None and u.requires_grad_count:
+        if wait and self.in_backward and u.grad_full is None and u.requires_grad_count:
+            # the unsharded gradient is allocated on demand, not for prefetched units
             u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=self.device)
             u.bind_grads(u.grad_full)
+            self._note_live()
         elif self.in_backward and u.direct and self.offload_param and u.requires_grad_count:
             u.bind_grads(u.grad_full)  # offloaded unit: grads land straight in the device grad shard
 
@@ -707,8 +730,7 @@ class ZeroOptimizer:
             return
         t = self._fwd_trace
         if self._trace_ok and self._trace_pos < len(t) and t[self._trace_pos] == u.uid:
-            for j in range(self._trace_pos + 1, min(len(t), self._trace_pos + 1 + self.prefetch_depth)):
-                self._gather(self.units[t[j]], wait=False)
+            self._prefetch(t[self._trace_pos + 1:])
         else:
             self._trace_ok = False
         self._trace_pos += 1
@@ -724,8 +746,60 @@ class ZeroOptimizer:
                 i = len(t) - 1 - t[::-1].index(u.uid)
             except ValueError:
                 return
-            for j in range(i - 1, max(-1, i - 1 - self.prefetch_depth), -1):
-                self._gather(self.units[t[j]], wait=False)
+            self._prefetch(t[:i][::-1])
+
+    def _live_numel(self):
+        return sum(u.padded for u in self.units if not u.persistent and u.full is not None)
+
+    def _prefetch(self, upcoming):
+        """Issue all-gathers for the next units of ``upcoming`` (uids in use order). Bounded by
+        ``zero3_prefetch_depth`` units, or -- when the config names them -- by stage3_prefetch_bucket_size
+        elements per prefetch window and stage3_max_live_parameters gathered elements."""
+        n = tot = 0
+        for uid in upcoming:
+            u = self.units[uid]
+            if self.prefetch_numel is not None:
+                if n and tot + u.numel > self.prefetch_numel:
+                    break
+            elif n >= self.prefetch_depth:
+                break
+            if u.status == NOT_AVAILABLE and self.max_live_numel is not None and \
+                    self._live_numel() + u.padded > self.max_live_numel:
+                break
+            self._gather(u, wait=False)
+            n += 1
+            tot += u.numel
+
+    def _compute_reuse_keep(self):
+        """Units whose next use (in backward) is within stage3_max_reuse_distance gathered elements stay
+        resident after their forward instead of being released and re-gathered."""
+        self._reuse_keep = set()
+        if self.max_reuse_distance is None:
+            return
+        t = self._fwd_trace
+        after = 0
+        for i in range(len(t) - 1, -1, -1):
+            if t[i] not in t[i + 1:] and 2 * after <= self.max_reuse_distance:
+                self._reuse_keep.add(t[i])
+            after += self.units[t[i]].numel
+
+    def _note_live(self):
+        """Debug/test accounting (HDS_ZERO_TRACK_LIVE=1): bytes of gathered parameters and unsharded
+        gradients of partitioned units that this optimizer still references, including in-flight reduces."""
+        if not self.track_live:
+            return
+        seen = {}
+        for u in self.units:
+            if u.persistent or not self._partitioned(u):
+                continue
+            for t in (u.full, u.grad_full):
+                if t is not None and t.numel():
+                    seen[t.data_ptr()] = t.numel() * t.element_size()
+        for item in self.pending_rs + self.pending_works:
+            for t in (item[2] if len(item) > 2 else ()):
+                if isinstance(t, torch.Tensor) and t.numel():
+                    seen[t.data_ptr()] = t.numel() * t.element_size()
+        self.live_peak_bytes = max(self.live_peak_bytes, sum(seen.values()))
 
     # ------------------------------------------------------------------------------------
     # gradient reduction
@@ -751,13 +825,20 @@ class ZeroOptimizer:
                 if u.grad_full is not None and not u.direct:
                     u.grad_full.zero_()
 
+    @staticmethod
+    def _retire(queue, limit):
+        """Wait on (and post-process) the oldest queued reductions until at most ``limit`` remain.
+        On RCCL ``wait()`` only orders the compute stream after the collective, so this does not block the
+        host; dropping the entry then returns its unsharded gradient buffer to the allocator."""
+        while len(queue) > limit:
+            item = queue.pop(0)
+            item[0].wait()
+            if item[1] is not None:
+                item[1]()
+
     def _drain_pending(self):
-        for item in self.pending_works:
-            w, post = item[0], item[1]
-            w.wait()
-            if post is not None:
-                post()
-        self.pending_works = []
+        self._retire(self.pending_rs, 0)
+        self._retire(self.pending_works, 0)
 
     def _reduce_unit(self, u):
         if self.stage == 0:
@@ -811,11 +892,16 @@ class ZeroOptimizer:
 
     def _after_reduce(self, u, src, w, post, keep):
         if self.stage == 3 and not u.persistent and u.world > 1:
-            gf = u.grad_full
+            # ZeRO-3: the unit's gathered parameters and unsharded gradient are dropped now. Only the
+            # collective's input (``keep``) lives on until the reduce retires, and at most
+            # ``max_reduce_inflight`` of those exist (reference stage3.py:1305-1308).
             u.unbind_grads()
             u.grad_full = None
-            keep = tuple(keep) + (gf, u.full)
             self._release(u)
+            self.pending_rs.append((w, post, keep))
+            self._note_live()
+            self._retire(self.pending_rs, self.max_reduce_inflight)
+            return
         self.pending_works.append((w, post, keep))
 
     def _qgz_reduce(self, u, src, dst, first):
@@ -866,6 +952,7 @@ class ZeroOptimizer:
         if self._recording and self._fwd_trace:
             self._recording = False
             self._trace_ok = True
+            self._compute_reuse_keep()
 
     # ------------------------------------------------------------------------------------
     # forward bracket (called by the engine around module.forward)
