@@ -1,76 +1,213 @@
 """Universal checkpoints: world-size independent per-parameter files, and re-sharded loading.
 
-Reference parity: checkpoint/ds_to_universal.py (:112-198, :469 -- writes
-``zero/<param_name>/{fp32,exp_avg,exp_avg_sq}.pt`` plus ``step``) and checkpoint/universal_checkpoint.py
-``load_hp_checkpoint_state`` (:22-143). Here the conversion reads the flat-shard optimizer files
-(see zero_to_fp32.py for the layout) and loading writes each new rank's shard of every unit from the
-per-parameter fp32/moment tensors, so a run can resume on a different number of GPUs.
+Layout (identical to the reference's, checkpoint/ds_to_universal.py:272-346,410-428)::
+
+    <out>/zero/<param name>/fp32.pt, exp_avg.pt, exp_avg_sq.pt [, step.pt]
+    <out>/zero/optimizer_state.pt          # non-sharded optimizer state + param_groups
+    <out>/mp_rank_XX_model_states.pt       # model file(s) of the source checkpoint
+
+ZeRO-0/1/2 sources give ``{"param": <full tensor>, "cat_dim": d, ...}`` files (plus ``step.pt``); ZeRO-3
+sources without TP give the bare full tensor -- exactly what each reference loader expects
+(universal_checkpoint.py:22-143 and stage3.py:2752-2827). Tensor-parallel slices are merged along the dims
+in the source's ``universal_checkpoint_info``; loading cuts this rank's TP slice back out (``cat_dim``,
+``sub_param_shape``, vocabulary padding) and then its data-parallel shard, so a run resumes on any number
+of GPUs and any TP degree. Both file flavours are read here.
 """
 import glob
 import os
+import shutil
 
 import torch
 
-from .zero_to_fp32 import expert_global_name, load_shards, unflatten
+from . import compat  # noqa: F401  (weights_only access to reference-pickled classes)
+from .zero_to_fp32 import (_files_by_mp, _dp_rank, _load, _one_mp_rank, expert_global_name, merge_tp_slices)
+
+_SHARDED = ("base_optimizer_state", "param_slice_mappings", "single_partition_of_fp32_groups", "fp32_flat_groups")
+
+
+def _resolve(input_dir, tag):
+    if tag is None and os.path.isfile(os.path.join(input_dir, "latest")):
+        with open(os.path.join(input_dir, "latest")) as f:
+            tag = f.read().strip()
+    return os.path.join(input_dir, tag) if tag else input_dir
+
+
+def _moment_keys(osd):
+    stage = int(osd["zero_stage"])
+    base = osd["optimizer_state_dict"] if stage == 3 else osd["base_optimizer_state"]
+    keys = []
+    for st in base.get("state", {}).values():
+        for k, v in st.items():
+            if torch.is_tensor(v) and v.dim() == 1 and k not in keys:
+                keys.append(k)
+    return keys
 
 
 def ds_to_universal(input_dir, output_dir, tag=None):
-    """Convert ``<input_dir>/<tag>`` ZeRO shards into ``<output_dir>/zero/<param>/{fp32,exp_avg,exp_avg_sq}.pt``."""
-    if tag is None and os.path.isfile(os.path.join(input_dir, "latest")):
-        tag = open(os.path.join(input_dir, "latest")).read().strip()
-    ckpt_dir = os.path.join(input_dir, tag) if tag else input_dir
-    f0 = sorted(glob.glob(os.path.join(ckpt_dir, "*_optim_states.pt")))[0]
-    sd0 = torch.load(f0, map_location="cpu", weights_only=True)["optimizer_state_dict"]
-    names = ["fp32"] + list(sd0["optimizer_states"].keys())
-    layout, shards = load_shards(ckpt_dir, states=tuple(names))
+    """Convert ``<input_dir>/<tag>`` (a ZeRO checkpoint in the reference schema) into a universal checkpoint."""
+    ckpt_dir = _resolve(input_dir, tag)
+    optim = _files_by_mp(ckpt_dir, "_optim_states.pt")
+    models = _files_by_mp(ckpt_dir, "_model_states.pt")
+    if not optim:
+        raise FileNotFoundError(f"no *_optim_states.pt in {ckpt_dir}")
+    osd0 = _load(optim[0][0])["optimizer_state_dict"]
+    stage = int(osd0["zero_stage"])
+    keys = ["fp32"] + _moment_keys(osd0)
+
+    def model_file(mp):
+        mf = models[mp]
+        if stage <= 2:
+            return [f for f in mf if os.path.basename(f).startswith("mp_rank_")][0]
+        return [f for f in mf if _dp_rank(f) == 0][0]
+
+    msd0 = _load(model_file(min(optim)))
+    info = msd0.get("universal_checkpoint_info") or {}
+    buffers = set(msd0.get("buffer_names") or [])
     zdir = os.path.join(output_dir, "zero")
-    for s in names:
-        full = unflatten(layout, shards[s])
-        for pname, t in full.items():
-            d = os.path.join(zdir, pname)
+    os.makedirs(zdir, exist_ok=True)
+    for key in keys:
+        per_mp = [_one_mp_rank(optim[mp], model_file(mp), models[mp], key=key)[0] for mp in sorted(optim)]
+        for name in per_mp[0]:
+            if name in buffers:
+                continue
+            full, extra = merge_tp_slices(name, [s[name] for s in per_mp], info)
+            d = os.path.join(zdir, name)
             os.makedirs(d, exist_ok=True)
-            torch.save({"param": t}, os.path.join(d, f"{s}.pt"))
-    step = sd0["param_groups"][0].get("step", 0) if sd0["param_groups"] else 0
-    torch.save(torch.tensor(step), os.path.join(zdir, "optimizer_step.pt"))
-    torch.save({"param_groups": sd0["param_groups"], "optimizer_kind": sd0["optimizer_kind"]},
-               os.path.join(output_dir, "universal_meta.pt"))
-    for mf in glob.glob(os.path.join(ckpt_dir, "*model_states.pt")):
-        pass
-    with open(os.path.join(output_dir, "latest_universal"), "w") as f:
-        f.write(os.path.basename(output_dir.rstrip("/")))
+            if stage == 3 and len(per_mp) == 1:
+                torch.save(full.clone(), os.path.join(d, f"{key}.pt"))  # bare tensor: the reference stage-3 flavour
+            else:
+                torch.save(dict(extra, param=full), os.path.join(d, f"{key}.pt"))
+        del per_mp
+    # global (non-sharded) optimizer state
+    if stage == 3:
+        gsd = dict(osd0)
+        gsd.pop("fp32_flat_groups", None)
+        base = gsd["optimizer_state_dict"]
+        base = dict(base, state={g: {k: v for k, v in st.items() if not (torch.is_tensor(v) and v.dim() == 1)}
+                                 for g, st in base.get("state", {}).items()})
+        gsd["optimizer_state_dict"] = base
+        gsd["param_groups"] = base.get("param_groups", [])
+    else:
+        gsd = {k: v for k, v in osd0.items() if k not in _SHARDED}
+        gsd["param_groups"] = osd0["base_optimizer_state"].get("param_groups", [])
+        steps = [st.get("step") for st in osd0["base_optimizer_state"].get("state", {}).values()]
+        step = next((s for s in steps if s is not None), None)
+        if step is not None:
+            for name in os.listdir(zdir):
+                if os.path.isdir(os.path.join(zdir, name)):
+                    torch.save(step, os.path.join(zdir, name, "step.pt"))
+    torch.save(gsd, os.path.join(zdir, "optimizer_state.pt"))
+    # model files: one per TP rank under the world-size independent name
+    for mp in sorted(optim):
+        src = model_file(mp)
+        shutil.copyfile(src, os.path.join(output_dir, f"mp_rank_{mp:02d}_model_states.pt"))
+    for f in glob.glob(os.path.join(ckpt_dir, "expp_rank_*")):
+        shutil.copy2(f, output_dir)
     return output_dir
 
 
+def _tp_slice(t, extra, target_shape, tp_rank, tp_world):
+    """This TP rank's slice of a universal tensor (reference universal_checkpoint.py:43-124)."""
+    if tuple(t.shape) == tuple(target_shape) or tp_world == 1:
+        return t
+    if extra.get("vocab_tensor", False):
+        padded = target_shape[0] * tp_world
+        if padded > t.shape[0]:
+            t = torch.nn.functional.pad(t, (0, 0, 0, padded - t.shape[0]))
+    sub = extra.get("sub_param_shape")
+    if sub:
+        sub = sub if isinstance(sub, dict) else vars(sub)
+        dim = sub["partition_dim"]
+        sizes = sub["shape"][dim]
+        sizes = sizes if isinstance(sizes, (tuple, list)) else (sizes, )
+        shape = [sum(d) if isinstance(d, (tuple, list)) else d for d in sub["shape"]]
+        t = t.view(shape)
+        chunks, off = [], 0
+        for s in sizes:
+            chunks.append(t.narrow(dim, off, s).chunk(tp_world, dim)[tp_rank])
+            off += s
+        return torch.cat(chunks, dim)
+    dim = int(extra.get("cat_dim", 0))
+    n_sub = int(extra.get("param_n_sub_params", 1))
+    if n_sub > 1:
+        return torch.cat([p.chunk(tp_world, dim)[tp_rank] for p in t.chunk(n_sub, dim)], dim)
+    return t.chunk(tp_world, dim)[tp_rank]
+
+
+def _read_universal(path):
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(obj, dict):
+        return obj["param"], {k: v for k, v in obj.items() if k != "param"}
+    return obj, {}
+
+
 def load_universal_into(zopt, universal_dir, load_optimizer_states=True):
-    """Fill a (possibly differently sized) ZeroOptimizer's shards from a universal checkpoint."""
+    """Fill a (possibly differently sized / TP-sliced) ZeroOptimizer's shards from a universal checkpoint.
+
+    Every rank reads only the parameter files overlapping its own shard. A missing ``fp32.pt`` is an error
+    (never a silent zero-fill); missing moments are an error when ``load_optimizer_states``."""
+    from ..utils import groups
+    from ..utils.logging import logger
     zdir = os.path.join(universal_dir, "zero")
-    s = zopt.store
-    states = ["fp32"] + (list(s.states.keys()) if load_optimizer_states else [])
+    if not os.path.isdir(zdir):
+        raise FileNotFoundError(f"{universal_dir} is not a universal checkpoint (no zero/ folder)")
+    tp_world, tp_rank = 1, 0
+    if groups._State.topo is not None:
+        tp_world, tp_rank = groups.get_model_parallel_world_size(), groups.get_model_parallel_rank()
+    flats = zopt._ckpt_flats()
+    keys = ["fp32"] + ([k for k in flats if k != "fp32"] if load_optimizer_states else [])
     with torch.no_grad():
         for u in zopt.units:
             lo, hi = u.rank * u.shard, (u.rank + 1) * u.shard
-            for st in states:
-                dst = s.master if st == "fp32" else s.states[st]
-                full = torch.zeros(u.padded, dtype=torch.float32)
-                for i, p in enumerate(u.params):
-                    name = zopt.param_names.get(id(p))
-                    j, nl = 0, int(getattr(p, "_hds_num_local", 1))
-                    if u.expert_key is not None:
-                        j = zopt._ep_rank(u.expert_key)
-                        if not getattr(p, "_hds_expert_stacked", False):
-                            name = expert_global_name(name, j, nl)
-                    f = os.path.join(zdir, name, f"{st}.pt")
-                    if os.path.exists(f):
-                        t = torch.load(f, map_location="cpu", weights_only=True)["param"]
-                        if u.expert_key is not None and getattr(p, "_hds_expert_stacked", False):
-                            t = t[j * nl:(j + 1) * nl]  # this EP rank's experts of the global stack
-                        full[u.offsets[i]:u.offsets[i] + u.numels[i]] = t.reshape(-1).float()
-                dst[u.store_off:u.store_off + u.shard].copy_(full[lo:hi].to(dst.device))
-        s.lp.copy_(s.master)
-    meta_f = os.path.join(universal_dir, "universal_meta.pt")
+            for i, p in enumerate(u.params):
+                a, b = max(lo, u.offsets[i]), min(hi, u.offsets[i] + u.numels[i])
+                if a >= b:
+                    continue
+                name = zopt.param_names.get(id(p))
+                if name is None:
+                    raise ValueError(f"parameter {i} of ZeRO unit {u.name!r} has no name: cannot map it to a "
+                                     "universal checkpoint file")
+                j, nl = 0, int(getattr(p, "_hds_num_local", 1))
+                stacked = getattr(p, "_hds_expert_stacked", False)
+                if u.expert_key is not None:
+                    j = zopt._ep_rank(u.expert_key)
+                    if not stacked:
+                        name = expert_global_name(name, j, nl)
+                for key in keys:
+                    f = os.path.join(zdir, name, f"{key}.pt")
+                    if not os.path.exists(f):
+                        raise FileNotFoundError(f"universal checkpoint has no {key!r} state for parameter {name!r} "
+                                                f"({f})" + ("" if key == "fp32" else
+                                                            "; pass load_optimizer_states=False to skip moments"))
+                    t, extra = _read_universal(f)
+                    if u.expert_key is not None and stacked:
+                        t = t.view(-1, *u.shapes[i][1:])[j * nl:(j + 1) * nl]  # this EP rank's experts
+                    if t.numel() != u.numels[i]:
+                        t = _tp_slice(t, extra, u.shapes[i], tp_rank, tp_world)
+                    if t.numel() != u.numels[i]:
+                        raise ValueError(f"universal {key} of {name!r}: {t.numel()} elements, parameter has "
+                                         f"{u.numels[i]} (shape {tuple(u.shapes[i])})")
+                    t = t.reshape(-1).float()
+                    dst = flats[key]
+                    so = u.store_off + a - lo
+                    dst[so:so + (b - a)].copy_(t[a - u.offsets[i]:b - u.offsets[i]])
+        zopt._ckpt_commit(flats)
+        zopt._master_to_lp()
+    meta_f = os.path.join(zdir, "optimizer_state.pt")
     if os.path.exists(meta_f):
         meta = torch.load(meta_f, map_location="cpu", weights_only=True)
-        for g, saved in zip(zopt.param_groups, meta["param_groups"]):
+        pgs = meta.get("param_groups") or []
+        if len(pgs) == len(zopt.param_groups):
+            targets = list(zip(zopt.param_groups, pgs))
+        else:
+            targets = [(g, pgs[0]) for g in zopt.param_groups] if pgs else []
+        for g, saved in targets:
             for k, v in saved.items():
-                g[k] = v
+                if k != "params":
+                    g[k] = v
+        ls = meta.get("loss_scaler")
+        if isinstance(ls, dict):
+            zopt.loss_scaler.load_state_dict(ls)
+    else:
+        logger.warning(f"{meta_f} missing: optimizer hyper-parameters / step count not restored")
     zopt._post_step_gather()

@@ -134,6 +134,19 @@ class _Embedding(nn.Embedding):
         nn.init.normal_(self.weight, std=self._std)
 
 
+def _fuse_hf_keys(parts, fused):
+    """load_state_dict pre-hook: accept HF / reference parameter names (separate q/k/v and gate/up projections)
+    for this model's fused GEMM weights, so HF and DeepSpeed state dicts load directly."""
+
+    def hook(state_dict, prefix, *args):
+        for kind in ("weight", "bias"):
+            keys = [f"{prefix}{p}.{kind}" for p in parts]
+            if all(k in state_dict for k in keys):
+                state_dict[f"{prefix}{fused}.{kind}"] = torch.cat([state_dict.pop(k) for k in keys], 0)
+
+    return hook
+
+
 class LlamaAttention(nn.Module):
 
     def __init__(self, cfg: LlamaConfig, layer_idx=0):
@@ -144,6 +157,7 @@ class LlamaAttention(nn.Module):
         self.qkv_proj = _Linear(cfg.hidden_size, (self.n_q + 2 * self.n_kv) * self.d, std=std)
         self.o_proj = _Linear(self.n_q * self.d, cfg.hidden_size, std=std / math.sqrt(2 * cfg.num_hidden_layers))
         self.layer_idx = layer_idx
+        self._register_load_state_dict_pre_hook(_fuse_hf_keys(("q_proj", "k_proj", "v_proj"), "qkv_proj"))
 
     sp_group = None  # Ulysses sequence-parallel group (parallel/ulysses.enable_sequence_parallel)
     fpdt = None  # FPDT settings (parallel/fpdt.enable_fpdt): chunked, optionally host-offloaded attention
@@ -185,6 +199,7 @@ class LlamaMLP(nn.Module):
         self.down_proj = _Linear(cfg.intermediate_size, cfg.hidden_size,
                                  std=std / math.sqrt(2 * cfg.num_hidden_layers))
         self.act = cfg.hidden_act
+        self._register_load_state_dict_pre_hook(_fuse_hf_keys(("gate_proj", "up_proj"), "gate_up_proj"))
 
     fpdt_chunks = 0  # >1: sequence-chunked MLP with per-chunk recompute (parallel/fpdt.enable_fpdt)
 
@@ -313,6 +328,25 @@ def convert_hf_state_dict(sd, cfg: LlamaConfig):
         out[p + "self_attn.qkv_proj.weight"] = torch.cat(
             [sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"], sd[p + "self_attn.v_proj.weight"]], 0)
         out[p + "mlp.gate_up_proj.weight"] = torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0)
+    return out
+
+
+def to_hf_state_dict(sd, cfg: LlamaConfig):
+    """This model's fused layout -> HF LlamaForCausalLM names (q/k/v_proj, gate/up_proj). Inverse of
+    :func:`convert_hf_state_dict`; use it to export checkpoints for HF / reference tooling."""
+    out = {}
+    qd, kd = cfg.num_attention_heads * cfg.head_dim, cfg.num_key_value_heads * cfg.head_dim
+    for k, v in sd.items():
+        if k.endswith("self_attn.qkv_proj.weight"):
+            base = k[:-len("qkv_proj.weight")]
+            q, kk, vv = v.split([qd, kd, kd], 0)
+            out[base + "q_proj.weight"], out[base + "k_proj.weight"], out[base + "v_proj.weight"] = q, kk, vv
+        elif k.endswith("mlp.gate_up_proj.weight"):
+            base = k[:-len("gate_up_proj.weight")]
+            g, u = v.chunk(2, 0)
+            out[base + "gate_proj.weight"], out[base + "up_proj.weight"] = g, u
+        else:
+            out[k] = v
     return out
 
 

@@ -76,19 +76,35 @@ def _mm_f32(a, b):
     return torch.mm(a.float(), b.float())
 
 
-_ADDMM_OUT_DTYPE = [True]
+_ADDMM_OUT_DTYPE = [None]  # None = not probed yet
+
+
+def _probe_addmm_out_dtype(device):
+    """One tiny probe: does this torch build accept ``addmm(..., out_dtype=float32)`` on bf16 inputs? Only the
+    capability probe may fail; real errors (OOM, HIP faults) in the hot path propagate."""
+    try:
+        a = torch.zeros(2, 2, dtype=torch.bfloat16, device=device)
+        acc = torch.zeros(2, 2, dtype=torch.float32, device=device)
+        torch.addmm(acc, a, a, out_dtype=torch.float32, out=acc)
+        _ADDMM_OUT_DTYPE[0] = True
+    except (TypeError, RuntimeError) as e:
+        from ..utils.logging import logger
+        logger.warning(f"fused linear CE: addmm(out_dtype=fp32) unsupported ({e}); using mm + add")
+        _ADDMM_OUT_DTYPE[0] = False
+    return _ADDMM_OUT_DTYPE[0]
 
 
 def _addmm_f32_(acc, a, b):
     """acc += a @ b with bf16 inputs and the fp32 accumulator folded into the GEMM (hipBLASLt beta=1): saves
     one full fp32 read+write of the [V, H] LM-head gradient per chunk (7 x 1.07 ms per step at the bench
     shape, profiles/rocprof_kernel_stats_r1_final.csv)."""
-    if acc.is_cuda and _ADDMM_OUT_DTYPE[0]:
-        try:
+    if acc.is_cuda:
+        ok = _ADDMM_OUT_DTYPE[0]
+        if ok is None:
+            ok = _probe_addmm_out_dtype(acc.device)
+        if ok:
             torch.addmm(acc, a, b, out_dtype=torch.float32, out=acc)
             return
-        except (TypeError, RuntimeError):
-            _ADDMM_OUT_DTYPE[0] = False
     acc.add_(_mm_f32(a, b))
 
 

@@ -146,6 +146,7 @@ class AutoTP:
         nw = torch.cat([q[r * lq * D:(r + 1) * lq * D], k[r * lkv * D:(r + 1) * lkv * D],
                         v[r * lkv * D:(r + 1) * lkv * D]], 0).clone()
         attn.qkv_proj = LinearLayer(nw, None, self.group)
+        attn.qkv_proj.weight.ds_tp_sub_params = (nq * D, nkv * D, nkv * D)  # q/k/v sliced independently
         attn.o_proj = LinearAllreduce(_cols(attn.o_proj.weight.data, r, self.n).clone(), None, self.group)
         attn.n_q, attn.n_kv = lq, lkv
 
@@ -155,6 +156,7 @@ class AutoTP:
         g, u = w.split([I, I], 0)
         nw = torch.cat([_rows(g, self.r, self.n), _rows(u, self.r, self.n)], 0).clone()
         mlp.gate_up_proj = LinearLayer(nw, None, self.group)
+        mlp.gate_up_proj.weight.ds_tp_sub_params = (I, I)
         mlp.down_proj = LinearAllreduce(_cols(mlp.down_proj.weight.data, self.r, self.n).clone(), None, self.group)
 
     def shard(self):
@@ -181,8 +183,11 @@ class AutoTP:
         for m in self.model.modules():
             if isinstance(m, (LinearLayer, LinearAllreduce)):
                 m.weight.ds_tensor_model_parallel = True
+                # checkpoint metadata: the dim the TP slices concatenate along (universal_checkpoint_info)
+                m.weight.ds_tp_cat_dim = 1 if isinstance(m, LinearAllreduce) else 0
                 if m.bias is not None and isinstance(m, LinearLayer):
                     m.bias.ds_tensor_model_parallel = True
+                    m.bias.ds_tp_cat_dim = 0
         return self.model
 
 

@@ -15,6 +15,7 @@ on-device fused-Adam path (Twin-Flow). With ``device: nvme`` the moments of each
 swapped in/out through the async file I/O handle around its CPU update.
 """
 import os
+from collections import OrderedDict
 
 import torch
 
@@ -221,26 +222,52 @@ class OffloadZeroOptimizer(ZeroOptimizer):
                             g.get("eps", 1e-8), g.get("weight_decay", 0.0), self.adamw, True, lp_out=s.lp[lo:hi],
                             dev_scale=coef)
 
-    def state_dict(self):
-        s = self.store
-        master_dev = s.master
-        states_dev = s.states
-        full_master = self.h_master.clone()
-        if self.n_off < s.numel:
-            full_master = torch.cat([full_master, master_dev[self.n_off:].cpu()])
-        s.master = full_master
-        hs = {}
-        for k in states_dev:
-            part = self.h_states[k].clone() if self.nvme is None else torch.from_file(
-                self._nvme_file(k), size=self.n_off, dtype=torch.float32).clone()
-            if self.n_off < s.numel:
-                part = torch.cat([part, states_dev[k][self.n_off:].cpu()])
-            hs[k] = part
-        s.states = hs
-        try:
-            return super().state_dict()
-        finally:
-            s.master, s.states = master_dev, states_dev
+    # checkpoint hooks: the fp32 master / moments of the offloaded range live in host DRAM (or NVMe)
+    def _ckpt_flats(self):
+        s, n, k0 = self.store, self.store.numel, self.n_off
+        out = OrderedDict()
+        m = torch.empty(n, dtype=torch.float32)
+        m[:k0].copy_(self.h_master)
+        if k0 < n:
+            m[k0:].copy_(s.master[k0:])
+        out["fp32"] = m
+        for k in self._STATE_KEYS[self.kind]:
+            t = torch.empty(n, dtype=torch.float32)
+            if self.nvme is None:
+                t[:k0].copy_(self.h_states[k])
+            elif k0:
+                self.nvme.sync_pread(t[:k0], self._nvme_file(k))
+            if k0 < n:
+                t[k0:].copy_(s.states[k][k0:])
+            out[k] = t
+        return out
+
+    def _ckpt_commit(self, flats):
+        s, n, k0 = self.store, self.store.numel, self.n_off
+        self.h_master.copy_(flats["fp32"][:k0])
+        if k0 < n:
+            s.master[k0:].copy_(flats["fp32"][k0:])
+        for k, t in flats.items():
+            if k == "fp32":
+                continue
+            if self.nvme is None:
+                self.h_states[k].copy_(t[:k0])
+            elif k0:
+                self.nvme.sync_pwrite(t[:k0].contiguous(), self._nvme_file(k))
+            if k0 < n:
+                s.states[k][k0:].copy_(t[k0:])
+
+    def _lp_to_master(self):
+        s, n, k0 = self.store, self.store.numel, self.n_off
+        self.h_master.copy_(s.lp[:k0])
+        if k0 < n:
+            s.master[k0:].copy_(s.lp[k0:])
+
+    def _master_to_lp(self):
+        s, n, k0 = self.store, self.store.numel, self.n_off
+        s.lp[:k0].copy_(self.h_master)
+        if k0 < n:
+            s.lp[k0:].copy_(s.master[k0:])
 
     def full_fp32_state_dict(self, names):
         s = self.store

@@ -1122,50 +1122,106 @@ class ZeroOptimizer:
         return {"stage": self.stage, "world": self.layout_world, "rank": self.layout_rank, "units": units,
                 "store_numel": self.store.numel}
 
-    def state_dict(self):
-        s = self.store
-        sd = OrderedDict()
-        sd["loss_scaler"] = self.loss_scaler.state_dict()
-        sd["dynamic_loss_scale"] = self.loss_scaler.dynamic
-        sd["overflow"] = self.overflow
-        sd["clip_grad"] = self.clip_grad
-        sd["zero_stage"] = self.stage
-        sd["partition_count"] = self.layout_world
-        sd["param_groups"] = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
-        sd["optimizer_kind"] = self.kind
-        sd["fp32_flat_shard"] = s.master.detach().cpu()
-        sd["optimizer_states"] = {k: v.detach().cpu() for k, v in s.states.items()}
+    def _ckpt_flats(self):
+        """Store-sized fp32 tensors a checkpoint holds: the master weights and every optimizer moment."""
+        d = OrderedDict(fp32=self.store.master)
         if self.kind == "generic":
-            sd["base_optimizer_state"] = self._generic_opt.state_dict()
-        sd["layout"] = self.layout()
-        sd["ds_version"] = "hds-0.1"
-        return sd
+            d.update(self._generic_flat_states())
+        else:
+            d.update(self.store.states)
+        return d
 
-    def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
+    def _ckpt_commit(self, flats):
+        """Called after a checkpoint load wrote ``flats`` (hook for host/NVMe-resident states)."""
+        if self.kind == "generic":
+            self._generic_set_flat_states(flats)
+
+    def _generic_flat_states(self):
         s = self.store
-        assert sd["layout"]["store_numel"] == s.numel, "checkpoint shard layout mismatch (different world size?)"
-        self.loss_scaler.load_state_dict(sd["loss_scaler"])
-        for g, saved in zip(self.param_groups, sd["param_groups"]):
-            for k, v in saved.items():
-                g[k] = v
+        out = OrderedDict()
+        for mp, sg in self._generic_params:
+            for k, v in self._generic_opt.state.get(mp, {}).items():
+                if torch.is_tensor(v) and v.numel() == sg.numel and v.numel() > 1:
+                    if k not in out:
+                        out[k] = torch.zeros(s.numel, dtype=torch.float32, device=s.master.device)
+                    s.seg(out[k], sg).copy_(v.reshape(-1))
+        return out
+
+    def _generic_set_flat_states(self, flats):
+        s = self.store
+        for mp, sg in self._generic_params:
+            st = self._generic_opt.state[mp]
+            for k, flat in flats.items():
+                if k == "fp32":
+                    continue
+                st[k] = s.seg(flat, sg).clone().view_as(mp)
+            gi = sg.group
+            if "step" not in st and "exp_avg" in st:
+                st["step"] = torch.tensor(float(self.param_groups[gi].get("step", 0)))
+
+    def ref_param_shapes(self):
+        """Model-file ``param_shapes`` matching :meth:`state_dict`'s flat groups (reference engine.py:3592)."""
+        from .ds_state import param_shapes, ref_groups
+        return param_shapes(ref_groups(self))
+
+    def state_dict(self):
+        """Reference-schema ZeRO optimizer state (stage_1_and_2.py:2156 / stage3.py:2544): collective over
+        every unit's data-parallel group -- call on all ranks."""
+        from .ds_state import build_state_dict
+        scalars = {gi: {"step": int(g.get("step", 0))} for gi, g in enumerate(self.param_groups)}
+        return build_state_dict(self, self._ckpt_flats(), scalars)
+
+    def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True, param_shapes=None):
+        """Load a reference-schema optimizer state written by this framework or by the reference for the same
+        data-parallel size (other sizes: universal checkpoint). Collective over every unit's group."""
+        from .ds_state import import_partitions, read_state_dict
+        order = None
+        if sd.get("hds_param_order") is None and param_shapes is not None:
+            order = [list(d.keys()) for d in param_shapes]
+        groups, parts, scalars, hps = read_state_dict(self, sd, order)
+        ls = sd.get("loss_scaler")
+        if ls is not None:
+            self.loss_scaler.load_state_dict(ls if isinstance(ls, dict) else
+                                             {k: v for k, v in vars(ls).items()
+                                              if k in ("cur_scale", "cur_iter", "last_overflow_iter",
+                                                       "cur_hysteresis")})
+        for g, hp in zip(groups, hps):
+            self.param_groups[g.param_group].update(hp)
+        for g, sc in zip(groups, scalars):
+            if "step" in sc:
+                self.param_groups[g.param_group]["step"] = int(sc["step"])
+        flats = self._ckpt_flats()
+        want = OrderedDict()
+        if load_from_fp32_weights:
+            want["fp32"] = flats["fp32"]
+        if load_optimizer_states:
+            for k in parts:
+                if k == "fp32" or any(t is None for t in parts[k]):
+                    continue
+                if k in flats:
+                    want[k] = flats[k]
+                elif self.kind == "generic":
+                    want[k] = torch.zeros_like(flats["fp32"])
+                    flats[k] = want[k]
         with torch.no_grad():
+            import_partitions(self, parts, groups, want)
+            self._ckpt_commit(flats)
             if load_from_fp32_weights:
-                s.master.copy_(sd["fp32_flat_shard"].to(s.master.device))
-                s.lp.copy_(s.master)
-            if load_optimizer_states:
-                for k, v in sd["optimizer_states"].items():
-                    if k in s.states:
-                        s.states[k].copy_(v.to(s.states[k].device))
-                if self.kind == "generic" and "base_optimizer_state" in sd:
-                    self._generic_opt.load_state_dict(sd["base_optimizer_state"])
+                self._master_to_lp()
         self._post_step_gather()
+
+    def _master_to_lp(self):
+        self.store.lp.copy_(self.store.master)
 
     def refresh_fp32_from_lp(self):
         with torch.no_grad():
             for u in self.units:
                 if u.full is not None and self._partitioned(u) and u.status == AVAILABLE:
                     self.store.lp_slice(u).copy_(u.full[u.rank * u.shard:(u.rank + 1) * u.shard])
-            self.store.master.copy_(self.store.lp)
+            self._lp_to_master()
+
+    def _lp_to_master(self):
+        self.store.master.copy_(self.store.lp)
 
     # ------------------------------------------------------------------------------------
     # full-parameter access

@@ -7,9 +7,22 @@ contiguous range of its unit's rank-major flat buffer; the "local" fragment is t
 range with this rank's shard, the "full" value is ONE all-gather of the unit's shard (collective over the
 unit's data-parallel group: call on every rank).
 """
+from dataclasses import dataclass
+
 import torch
 
 from .. import comm as dist
+
+
+@dataclass
+class fragment_address:
+    """Where one parameter's fragment sits inside a rank's flat optimizer partition (reference
+    utils/tensor_fragment.py:13). Written into ZeRO-1/2 ``param_slice_mappings``."""
+    numel: int
+    start: int
+
+
+torch.serialization.add_safe_globals([fragment_address])
 
 _GRAD = "__grad__"
 _FP32 = "__fp32__"

@@ -204,6 +204,8 @@ def test_fused_linear_cross_entropy():
     (2 * ref).backward()
     assert _rel(h.grad, hr.grad) < 3e-2
     assert _rel(w.grad, wr.grad) < 3e-2
+    from hcache_deepspeed_amd.ops import cross_entropy as C
+    assert C._ADDMM_OUT_DTYPE[0] is True, "fused fp32-accumulating LM-head GEMM silently disabled"
 
 
 def _attn_ref(q, k, v, causal, window=0, cu=None, S=None):
