@@ -20,6 +20,22 @@ from .runtime.engine import DeepSpeedEngine  # noqa: F401
 from .runtime.lr_schedules import VALID_LR_SCHEDULES  # noqa: F401
 from .utils.logging import logger, log_dist  # noqa: F401
 from .runtime.activation_checkpointing import checkpointing  # noqa: F401
+from . import ops  # noqa: F401
+from .accelerator import get_accelerator  # noqa: F401
+from .runtime.config import ConfigError as DeepSpeedConfigError  # noqa: F401
+from .runtime.lr_schedules import add_tuning_arguments  # noqa: F401
+from .runtime.compiler import is_compile_supported  # noqa: F401
+from .utils.init_on_device import OnDevice  # noqa: F401
+from .pipe import PipelineModule  # noqa: F401
+from .runtime.pipe.engine import PipelineEngine  # noqa: F401
+from .runtime.hybrid_engine import DeepSpeedHybridEngine  # noqa: F401
+from .inference.engine import InferenceEngine  # noqa: F401
+from .inference.config import DeepSpeedInferenceConfig  # noqa: F401
+from .ops.transformer import DeepSpeedTransformerConfig, DeepSpeedTransformerLayer  # noqa: F401
+from .module_inject import replace_transformer_layer, revert_transformer_layer, set_autotp_mode  # noqa: F401
+from .runtime import domino  # noqa: F401
+
+version = __version__
 
 
 def initialize(args=None, model=None, optimizer=None, model_parameters=None, training_data=None, lr_scheduler=None,
@@ -33,6 +49,13 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
         config = getattr(args, "deepspeed_config", None)
     init_distributed(distributed_port=distributed_port, dist_init_required=dist_init_required)
     cfg = DeepSpeedConfig(config, mpu=mpu)
+    if mesh_param is not None:
+        # (data_parallel, sequence_parallel) device mesh (reference __init__.py:141-148): the SP extent becomes the
+        # Ulysses group size; ZeRO then shards over the dp x sp sequence-data-parallel group
+        dp, sp = (int(x) for x in mesh_param)
+        if dp * sp != comm.get_world_size():
+            raise ValueError(f"mesh_param {mesh_param} does not cover the world size {comm.get_world_size()}")
+        cfg.sequence_parallel_size = sp
     from .runtime.pipe.module import PipelineModule
     if isinstance(model, PipelineModule):
         from .runtime.pipe.engine import PipelineEngine

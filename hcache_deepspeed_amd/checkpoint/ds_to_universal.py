@@ -1,0 +1,30 @@
+"""``deepspeed.checkpoint.ds_to_universal`` import path and CLI (reference checkpoint/ds_to_universal.py:50,469)::
+
+    python -m hcache_deepspeed_amd.checkpoint.ds_to_universal --input_folder ckpt/global_step10 \
+        --output_folder ckpt/global_step10_universal
+"""
+import argparse
+
+from .universal import ds_to_universal  # noqa: F401
+
+
+def parse_arguments(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--input_folder", required=True, help="ZeRO checkpoint folder (a tag directory or its parent)")
+    ap.add_argument("--output_folder", required=True, help="universal checkpoint output folder")
+    ap.add_argument("--tag", default=None)
+    ap.add_argument("--num_extract_workers", type=int, default=1)
+    ap.add_argument("--num_merge_workers", type=int, default=1)
+    ap.add_argument("--keep_temp_folder", action="store_true")
+    ap.add_argument("--strict", action="store_true")
+    ap.add_argument("--inject_missing_state", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(args):
+    print(f"Converting DeepSpeed checkpoint in {args.input_folder} to Universal checkpoint in {args.output_folder}")
+    ds_to_universal(args.input_folder, args.output_folder, tag=args.tag)
+
+
+if __name__ == "__main__":
+    main(parse_arguments())

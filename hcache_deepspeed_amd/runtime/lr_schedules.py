@@ -165,3 +165,32 @@ def get_scheduler(name, optimizer, params):
         import torch
         cls = getattr(torch.optim.lr_scheduler, name)
     return cls(optimizer, **params)
+
+
+def add_tuning_arguments(parser):
+    """LR-schedule command-line arguments (reference runtime/lr_schedules.py add_tuning_arguments)."""
+    g = parser.add_argument_group("Convergence Tuning", "Convergence tuning configurations")
+    g.add_argument("--lr_schedule", type=str, default=None, help="LR schedule for training.")
+    g.add_argument("--lr_range_test_min_lr", type=float, default=0.001)
+    g.add_argument("--lr_range_test_step_rate", type=float, default=1.0)
+    g.add_argument("--lr_range_test_step_size", type=int, default=1000)
+    g.add_argument("--lr_range_test_staircase", type=bool, default=False)
+    g.add_argument("--cycle_first_step_size", type=int, default=1000)
+    g.add_argument("--cycle_first_stair_count", type=int, default=-1)
+    g.add_argument("--cycle_second_step_size", type=int, default=-1)
+    g.add_argument("--cycle_second_stair_count", type=int, default=-1)
+    g.add_argument("--decay_step_size", type=int, default=1000)
+    g.add_argument("--cycle_min_lr", type=float, default=0.01)
+    g.add_argument("--cycle_max_lr", type=float, default=0.1)
+    g.add_argument("--decay_lr_rate", type=float, default=0.0)
+    g.add_argument("--cycle_momentum", default=False, action="store_true")
+    g.add_argument("--cycle_min_mom", type=float, default=0.8)
+    g.add_argument("--cycle_max_mom", type=float, default=0.9)
+    g.add_argument("--decay_mom_rate", type=float, default=0.0)
+    g.add_argument("--warmup_min_lr", type=float, default=0)
+    g.add_argument("--warmup_max_lr", type=float, default=0.001)
+    g.add_argument("--warmup_num_steps", type=int, default=1000)
+    g.add_argument("--warmup_type", type=str, default="log")
+    g.add_argument("--warmup_min_ratio", type=float, default=0.0)
+    g.add_argument("--cos_min_ratio", type=float, default=0.0001)
+    return parser

@@ -52,7 +52,7 @@ def test_autotp_training_matches_single(stage):
     run_distributed(_tp, 2, stage)
 
 
-def _sp(rank, world, stage):
+def _sp(rank, world, stage, use_mesh=False):
     import hcache_deepspeed_amd as ds
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
     g = torch.Generator().manual_seed(9)
@@ -67,7 +67,11 @@ def _sp(rank, world, stage):
     m = LlamaForCausalLM(tiny(**TINY))
     cfg = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
            "zero_optimization": {"stage": stage}, "sequence_parallel_size": 2}
-    eng, _, _, _ = ds.initialize(model=m, config=cfg)
+    if use_mesh:  # the same layout requested through initialize(mesh_param=(dp, sp))
+        del cfg["sequence_parallel_size"]
+        eng, _, _, _ = ds.initialize(model=m, config=cfg, mesh_param=(1, 2))
+    else:
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
     half = S // 2
     losses = []
     for x, t in batches:
@@ -87,6 +91,10 @@ def _sp(rank, world, stage):
 @pytest.mark.parametrize("stage", [1, 3])
 def test_ulysses_sp_matches_single(stage):
     run_distributed(_sp, 2, stage)
+
+
+def test_mesh_param_sets_sequence_parallel():
+    run_distributed(_sp, 2, 3, True)
 
 
 def _ulysses_a2a(rank, world):
