@@ -87,5 +87,64 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// ---- head-dim generic tiles -------------------------------------------------------------------
+// A D-wide 64-row tile is ceil(D/128) 128-column sub-tiles in the layout above; only the first D/8 16-byte
+// chunks of each row are staged. Contractions over D use exactly D/16 k-steps; products that produce D
+// columns compute ceil(D/32) 32-column blocks and never store columns >= D (those blocks only read
+// unstaged LDS columns, and an MFMA output row depends on one A-operand row, so nothing leaks).
+template <int D>
+struct Dim {
+  static constexpr int KS = D / 16;           // 16-wide k-steps of the head-dim contraction
+  static constexpr int DT = (D + 31) / 32;    // 32-column output blocks
+  static constexpr int NT = (D + 127) / 128;  // 128-column LDS sub-tiles
+  static constexpr int TILE = NT * 16384;     // bytes of one 64-row tile
+  static_assert(D % 16 == 0 && D <= 256, "head_dim must be a multiple of 16, at most 256");
+};
+
+// row-fragment (A or B operand) for k-step ks of a D-wide tile
+__device__ __forceinline__ bf16x8 rows_d(const char* tile, int row0, int ks) {
+  return read_rows(tile + (ks >> 3) * 16384, row0, ks & 7);
+}
+// transposed fragment for k-step s and 32-column block dt of a D-wide tile
+__device__ __forceinline__ bf16x8 tr_d(const char* tile, int s, int dt) { return read_tr(tile + (dt >> 2) * 16384, s, dt & 3); }
+
+// Stage a 64-row x D-column tile: sub-tile c holds columns [128c, 128c + 128); only valid 16-B chunks load.
+template <int NW, int D, typename RowPtr>
+__device__ __forceinline__ void stage_tile_d(char* tile, RowPtr row_ptr) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < Dim<D>::NT; ++c) {
+    constexpr int kFull = 16;
+    const int nch = (D - 128 * c) >= 128 ? kFull : (D - 128 * c) / 8;
+#pragma unroll
+    for (int i = 0; i < 16 / NW; ++i) {
+      const int n = w * (16 / NW) + i;
+      const int row = 4 * n + (lane >> 4);
+      const int ch = (lane & 15) ^ swz(row);
+      if (nch == kFull || ch < nch) {
+        const char* src = (const char*)(row_ptr(row) + 128 * c) + ch * 16;
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(tile + c * 16384 + n * 1024), 16, 0, 0);
+      }
+    }
+  }
+}
+
+// store 32-column block dt of a lane's accumulator row (column = 32dt + 8g + 4h + j) with scale; cols >= D skipped
+template <int D>
+__device__ __forceinline__ void store_row_block(bf16* dst, const f32x16& acc, int dt, int h, float mul) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int col = 32 * dt + 8 * g + 4 * h;
+    if (D % 32 == 0 || col < D) {
+      bf16x4 v4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v4[j] = (bf16)(acc[4 * g + j] * mul);
+      *reinterpret_cast<bf16x4*>(dst + col) = v4;
+    }
+  }
+}
+
+
 }  // namespace attn
 }  // namespace hds

@@ -1,5 +1,12 @@
 // FlashAttention forward + backward for gfx950 (causal / sliding-window / full, GQA, varlen),
-// head_dim 128, bf16 in/out, fp32 softmax statistics (LSE) exposed for FPDT / ring merges.
+// head_dim D in {32, 48, 64, 80, 96, 112, 128, 160, 192, 256} (any multiple of 16 up to 256 that is instantiated
+// below), bf16 in/out, fp32 softmax statistics (LSE) exposed for FPDT / ring merges.
+//
+// Head-dim generality: tiles are stored as 128-column LDS sub-tiles (256-B rows, the XOR layout of
+// attn_common.h); a D-wide tile is ceil(D/128) of them and only the first D/8 16-byte chunks of each row are
+// staged. Q.K^T / dO.V^T contract over exactly D/16 k-steps; the P.V / dS.Q / dS.K products produce
+// ceil(D/32) 32-column blocks whose columns >= D are never stored (they only see unstaged LDS columns, which
+// cannot leak into valid columns: each MFMA output row depends on one A-operand row).
 //
 // Capability parity: replaces the reference's prebuilt NVIDIA-only `libblockedflash`
 // (deepspeed/inference/v2/kernels/ragged_ops/blocked_flash), the `flash_attn`
@@ -24,7 +31,6 @@ using namespace hds::attn;
 
 namespace {
 
-constexpr int D = 128;
 constexpr int BN = 64;   // keys per LDS tile (fwd, dq) / query rows per tile (dkdv)
 // query rows per workgroup (fwd, dq) = 32 * NW ; keys per workgroup (dkdv) = 32 * NW
 constexpr float kLog2e = 1.4426950408889634f;
@@ -42,6 +48,7 @@ struct AttnParams {
   float* delta;  // [Hq][total_tokens]
   int64_t sq, sk, sv, so, sdo, sdq, sdk, sdv;  // token strides (elements)
   const int* cu_seqlens;                       // [B+1] or null
+  const int* seq_lens;                         // [B] valid lengths of a right-padded batch (null: all seq_len)
   int seq_len;                                 // when cu_seqlens is null
   int total_tokens;
   int batch, hq, hkv;
@@ -56,7 +63,7 @@ __device__ __forceinline__ void seq_bounds(const AttnParams& p, int b, int& star
     len = p.cu_seqlens[b + 1] - start;
   } else {
     start = b * p.seq_len;
-    len = p.seq_len;
+    len = p.seq_lens ? p.seq_lens[b] : p.seq_len;
   }
 }
 
@@ -87,10 +94,11 @@ __device__ __forceinline__ bool masked(const AttnParams& p, int qi, int kj, int 
 //            wave grew by more than kDeferThr (log2 units), so P stays <= 2^kDeferThr (guide T13).
 constexpr float kDeferThr = 8.f;
 
-template <int NW, int VAR>
+template <int D, int NW, int VAR>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
-  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
+  constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TL];  // K[2], V[2]
   int blk, hq, b;
   lpt_ids(blk, hq, b);
   int start, len;
@@ -105,12 +113,12 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   const float c = p.scale * kLog2e;
 
   // Q fragments (B operand of S^T = K.Q^T): Q[myq][16ks + 8h .. +7]
-  bf16x8 qf[8];
+  bf16x8 qf[KS];
   {
     const int qr = myq < len ? myq : len - 1;
     const bf16* qp = p.q + (int64_t)(start + qr) * p.sq + (int64_t)hq * D + 8 * h;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
   }
 
   // key-tile range
@@ -140,15 +148,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     };
   };
 
-  f32x16 o[4];
+  f32x16 o[DT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x16{};
+  for (int i = 0; i < DT; ++i) o[i] = f32x16{};
   float m = -INFINITY, l = 0.f;
 
   const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
 
-  stage_tile64<NW>(smem + 0, kptr(kt_begin));
-  stage_tile64<NW>(smem + 2 * 16384, vptr(kt_begin));
+  stage_tile_d<NW, D>(smem + 0, kptr(kt_begin));
+  stage_tile_d<NW, D>(smem + 2 * TL, vptr(kt_begin));
   __syncthreads();
   if constexpr ((VAR & 1) != 0 && NW == 8) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
@@ -156,11 +164,11 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = (kt - kt_begin) & 1;
-    char* Kt = smem + buf * 16384;
-    char* Vt = smem + 2 * 16384 + buf * 16384;
+    char* Kt = smem + buf * TL;
+    char* Vt = smem + 2 * TL + buf * TL;
     if (kt + 1 < kt_end) {
-      stage_tile64<NW>(smem + (buf ^ 1) * 16384, kptr(kt + 1));
-      stage_tile64<NW>(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
+      stage_tile_d<NW, D>(smem + (buf ^ 1) * TL, kptr(kt + 1));
+      stage_tile_d<NW, D>(smem + 2 * TL + (buf ^ 1) * TL, vptr(kt + 1));
     }
     const int k0 = kt * BN;
     // wave-uniform skip of fully masked tiles
@@ -173,7 +181,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       for (int t = 0; t < 2; ++t) {
         s[t] = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) s[t] = mfma(read_rows(Kt, 32 * t, ks), qf[ks], s[t]);
+        for (int ks = 0; ks < KS; ++ks) s[t] = mfma(rows_d(Kt, 32 * t, ks), qf[ks], s[t]);
       }
       const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
                              (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
@@ -195,7 +203,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
           alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
           m = mnew;
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+          for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
         }
         muse = (m == -INFINITY) ? 0.f : m;
       } else {
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         m = mnew;
         if (__any(alpha != 1.f)) {  // running max moved for some row of this wave: rescale O
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+          for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
         }
       }
       float rs = 0.f;
@@ -221,9 +229,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       l = l * alpha + rs;
       bf16x8 pb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int st = 0; st < 4; ++st) o[dt] = mfma(read_tr(Vt, st, dt), pb[st], o[dt]);
+        for (int st = 0; st < 4; ++st) o[dt] = mfma(tr_d(Vt, st, dt), pb[st], o[dt]);
     }
     __syncthreads();
   }
@@ -233,14 +241,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     bf16* op = p.o + (int64_t)(start + myq) * p.so + (int64_t)hq * D;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = (bf16)(o[dt][4 * g + j] * inv);
-        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * h) = v4;
-      }
+    for (int dt = 0; dt < DT; ++dt) store_row_block<D>(op, o[dt], dt, h, inv);
     if (h == 0 && p.lse) {
       const float lse = (l > 0.f) ? (m + __log2f(l)) / kLog2e : -INFINITY;
       p.lse[(int64_t)hq * p.total_tokens + start + myq] = lse;
@@ -251,6 +252,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 // =====================================================================================
 // backward pre-pass: delta[hq][t] = sum_d dO * O   (16 lanes per row, 4 rows per wave)
 // =====================================================================================
+template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams p) {
   const int64_t rows = (int64_t)p.total_tokens * p.hq;
   const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
@@ -261,11 +263,14 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams p) {
   if (row < rows) {
     t = row / p.hq;
     hq = (int)(row - t * p.hq);
-    float a[8], bb[8];
-    Vec8<bf16>::load(p.o + t * p.so + (int64_t)hq * D + sub * 8, a);
-    Vec8<bf16>::load(p.dout + t * p.sdo + (int64_t)hq * D + sub * 8, bb);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
+    for (int c = sub; c < D / 8; c += 16) {
+      float a[8], bb[8];
+      Vec8<bf16>::load(p.o + t * p.so + (int64_t)hq * D + c * 8, a);
+      Vec8<bf16>::load(p.dout + t * p.sdo + (int64_t)hq * D + c * 8, bb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
+    }
   }
 #pragma unroll
   for (int off = 8; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 16);
@@ -275,11 +280,15 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams p) {
 // =====================================================================================
 // backward dK, dV
 // =====================================================================================
-template <int NW>
+// C0 / CN: this launch produces the 32-column blocks [C0, C0 + CN) of dK and dV. Head dims > 128 run two
+// launches over the two column halves (S and dP are recomputed per half) so the accumulators fit the register
+// file without scratch spills.
+template <int D, int NW, int C0 = 0, int CN = Dim<D>::DT>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
   constexpr int BK = 32 * NW;
-  // LDS: Q[2] (16K each), dO[2] (16K each), lse[2][64], delta[2][64]
-  __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + 4 * 256];
+  constexpr int KS = Dim<D>::KS, TL = Dim<D>::TILE;
+  // LDS: Q[2], dO[2] (TL bytes each), lse[2][64], delta[2][64]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TL + 4 * 256];
   const int b = blockIdx.z, hk = blockIdx.y;
   int start, len;
   seq_bounds(p, b, start, len);
@@ -293,20 +302,20 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
   const float c = p.scale * kLog2e;
 
   // K and V fragments (B operands): K[myk][16ks + 8h ..]
-  bf16x8 kf[8], vf[8];
+  bf16x8 kf[KS], vf[KS];
   {
     const int kr = myk < len ? myk : len - 1;
     const bf16* kp = p.k + (int64_t)(start + kr) * p.sk + (int64_t)hk * D + 8 * h;
     const bf16* vp = p.v + (int64_t)(start + kr) * p.sv + (int64_t)hk * D + 8 * h;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       kf[ks] = *reinterpret_cast<const bf16x8*>(kp + 16 * ks);
       vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 16 * ks);
     }
   }
-  f32x16 dk[4], dv[4];
+  f32x16 dk[CN], dv[CN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x16{};
+  for (int i = 0; i < CN; ++i) dk[i] = dv[i] = f32x16{};
 
   // query-tile range (same for every q-head of the group)
   int qt_begin = 0;
@@ -326,16 +335,16 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
   auto stage = [&](int it, int buf) {
     const int g = it / nqt, qt = qt_begin + it % nqt;
     const int hq = hk * G + g;
-    char* Qt = smem + buf * 16384;
-    char* Ot = smem + 2 * 16384 + buf * 16384;
-    float* Lt = reinterpret_cast<float*>(smem + 4 * 16384 + buf * 256);
-    float* Dt = reinterpret_cast<float*>(smem + 4 * 16384 + 512 + buf * 256);
-    stage_tile64<NW>(Qt, [=](int row) {
+    char* Qt = smem + buf * TL;
+    char* Ot = smem + 2 * TL + buf * TL;
+    float* Lt = reinterpret_cast<float*>(smem + 4 * TL + buf * 256);
+    float* Dt = reinterpret_cast<float*>(smem + 4 * TL + 512 + buf * 256);
+    stage_tile_d<NW, D>(Qt, [=](int row) {
       int r = qt * BN + row;
       r = r < len ? r : len - 1;
       return p.q + (int64_t)(start + r) * p.sq + (int64_t)hq * D;
     });
-    stage_tile64<NW>(Ot, [=](int row) {
+    stage_tile_d<NW, D>(Ot, [=](int row) {
       int r = qt * BN + row;
       r = r < len ? r : len - 1;
       return p.dout + (int64_t)(start + r) * p.sdo + (int64_t)hq * D;
@@ -356,10 +365,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
     const int buf = it & 1;
     if (it + 1 < total) stage(it + 1, buf ^ 1);
     const int qt = qt_begin + it % nqt;
-    const char* Qt = smem + buf * 16384;
-    const char* Ot = smem + 2 * 16384 + buf * 16384;
-    const float* Lt = reinterpret_cast<const float*>(smem + 4 * 16384 + buf * 256);
-    const float* Dt = reinterpret_cast<const float*>(smem + 4 * 16384 + 512 + buf * 256);
+    const char* Qt = smem + buf * TL;
+    const char* Ot = smem + 2 * TL + buf * TL;
+    const float* Lt = reinterpret_cast<const float*>(smem + 4 * TL + buf * 256);
+    const float* Dt = reinterpret_cast<const float*>(smem + 4 * TL + 512 + buf * 256);
     const int qbase = qt * BN;
     // wave-uniform skip: all queries of the tile before this wave's keys (causal)
     bool skip = (kw0 >= len);
@@ -371,9 +380,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
         // S = Q.K^T (key on lane): rows = queries 32*sub + acc_row
         f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) sacc = mfma(read_rows(Qt, 32 * sub, ks), kf[ks], sacc);
+        for (int ks = 0; ks < KS; ++ks) sacc = mfma(rows_d(Qt, 32 * sub, ks), kf[ks], sacc);
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) dpacc = mfma(read_rows(Ot, 32 * sub, ks), vf[ks], dpacc);
+        for (int ks = 0; ks < KS; ++ks) dpacc = mfma(rows_d(Ot, 32 * sub, ks), vf[ks], dpacc);
         // P and dS
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -387,11 +396,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
         const bf16x8 p0 = acc_to_b<0>(sacc), p1 = acc_to_b<1>(sacc);
         const bf16x8 s0 = acc_to_b<0>(dpacc), s1 = acc_to_b<1>(dpacc);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          dv[dt] = mfma(read_tr(Ot, 2 * sub, dt), p0, dv[dt]);
-          dv[dt] = mfma(read_tr(Ot, 2 * sub + 1, dt), p1, dv[dt]);
-          dk[dt] = mfma(read_tr(Qt, 2 * sub, dt), s0, dk[dt]);
-          dk[dt] = mfma(read_tr(Qt, 2 * sub + 1, dt), s1, dk[dt]);
+        for (int i = 0; i < CN; ++i) {
+          const int dt = C0 + i;
+          dv[i] = mfma(tr_d(Ot, 2 * sub, dt), p0, dv[i]);
+          dv[i] = mfma(tr_d(Ot, 2 * sub + 1, dt), p1, dv[i]);
+          dk[i] = mfma(tr_d(Qt, 2 * sub, dt), s0, dk[i]);
+          dk[i] = mfma(tr_d(Qt, 2 * sub + 1, dt), s1, dk[i]);
         }
       }
     }
@@ -401,18 +411,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
     bf16* kp = p.dk + (int64_t)(start + myk) * p.sdk + (int64_t)hk * D;
     bf16* vp = p.dv + (int64_t)(start + myk) * p.sdv + (int64_t)hk * D;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 a4, b4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a4[j] = (bf16)(dk[dt][4 * g + j] * p.scale);
-          b4[j] = (bf16)(dv[dt][4 * g + j]);
-        }
-        *reinterpret_cast<bf16x4*>(kp + 32 * dt + 8 * g + 4 * h) = a4;
-        *reinterpret_cast<bf16x4*>(vp + 32 * dt + 8 * g + 4 * h) = b4;
-      }
+    for (int i = 0; i < CN; ++i) {
+      store_row_block<D>(kp, dk[i], C0 + i, h, p.scale);
+      store_row_block<D>(vp, dv[i], C0 + i, h, 1.f);
+    }
   }
 }
 
@@ -426,9 +428,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
 // (128 regs) + one 32x32 S/dP pair, which fits 256 registers -> 2 waves per SIMD, so one wave's
 // softmax/VALU section overlaps the other wave's MFMAs. The two query halves' partial dK/dV are
 // summed through LDS once at the end.
-template <int PRIO>
+template <int D, int PRIO>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) {
   constexpr int BK = 128;
+  constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT;
+  static_assert(D <= 128, "split dK/dV kernel keeps 8 tiles in LDS: head_dim <= 128");
   // LDS: K (2 x 16K), V (2 x 16K), Q[2] (16K each), dO[2] (16K each), lse[2][64], delta[2][64]
   __shared__ __attribute__((aligned(16))) char smem[8 * 16384 + 4 * 256];
   char* const Kt = smem;
@@ -455,21 +459,21 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
   // K / V tiles of the block (rows clamped to the sequence)
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    stage_tile64<8>(Kt + t * 16384, [=](int row) {
+    stage_tile_d<8, D>(Kt + t * 16384, [=](int row) {
       int r = kb * BK + 64 * t + row;
       r = r < len ? r : len - 1;
       return p.k + (int64_t)(start + r) * p.sk + (int64_t)hk * D;
     });
-    stage_tile64<8>(Vt + t * 16384, [=](int row) {
+    stage_tile_d<8, D>(Vt + t * 16384, [=](int row) {
       int r = kb * BK + 64 * t + row;
       r = r < len ? r : len - 1;
       return p.v + (int64_t)(start + r) * p.sv + (int64_t)hk * D;
     });
   }
 
-  f32x16 dk[4], dv[4];
+  f32x16 dk[DT], dv[DT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x16{};
+  for (int i = 0; i < DT; ++i) dk[i] = dv[i] = f32x16{};
 
   int qt_begin = 0;
   if (p.causal) qt_begin = (kb * BK) / BN;
@@ -485,12 +489,12 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
   auto stage = [&](int it, int buf) {
     const int g = it / nqt, qt = qt_begin + it % nqt;
     const int hq = hk * G + g;
-    stage_tile64<8>(Qbase + buf * 16384, [=](int row) {
+    stage_tile_d<8, D>(Qbase + buf * 16384, [=](int row) {
       int r = qt * BN + row;
       r = r < len ? r : len - 1;
       return p.q + (int64_t)(start + r) * p.sq + (int64_t)hq * D;
     });
-    stage_tile64<8>(Obase + buf * 16384, [=](int row) {
+    stage_tile_d<8, D>(Obase + buf * 16384, [=](int row) {
       int r = qt * BN + row;
       r = r < len ? r : len - 1;
       return p.dout + (int64_t)(start + r) * p.sdo + (int64_t)hq * D;
@@ -524,9 +528,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
       const bool need_mask = (p.causal && q0 < kw0 + 31) || p.window > 0 || q0 + 32 > len || kw0 + 32 > len;
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) sacc = mfma(read_rows(Qt, 32 * qh, ks), read_rows(Kw, krow0, ks), sacc);
+      for (int ks = 0; ks < KS; ++ks) sacc = mfma(read_rows(Qt, 32 * qh, ks), read_rows(Kw, krow0, ks), sacc);
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) dpacc = mfma(read_rows(Ot, 32 * qh, ks), read_rows(Vw, krow0, ks), dpacc);
+      for (int ks = 0; ks < KS; ++ks) dpacc = mfma(read_rows(Ot, 32 * qh, ks), read_rows(Vw, krow0, ks), dpacc);
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
         const int qr0 = 32 * qh + 8 * r4 + 4 * h;  // rows acc_row(4*r4 + j, h) = qr0 + j
@@ -544,7 +548,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
       const bf16x8 p0 = acc_to_b<0>(sacc), p1 = acc_to_b<1>(sacc);
       const bf16x8 s0 = acc_to_b<0>(dpacc), s1 = acc_to_b<1>(dpacc);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < DT; ++dt) {
         dv[dt] = mfma(read_tr(Ot, 2 * qh, dt), p0, dv[dt]);
         dv[dt] = mfma(read_tr(Ot, 2 * qh + 1, dt), p1, dv[dt]);
         dk[dt] = mfma(read_tr(Qt, 2 * qh, dt), s0, dk[dt]);
@@ -557,7 +561,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
   float* red = reinterpret_cast<float*>(smem) + kg * 8192;
   if (qh == 1) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         red[(dt * 16 + r) * 64 + lane] = dk[dt][r];
@@ -569,29 +573,27 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
     bf16* kp = p.dk + (int64_t)(start + myk) * p.sdk + (int64_t)hk * D;
     bf16* vp = p.dv + (int64_t)(start + myk) * p.sdv + (int64_t)hk * D;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < DT; ++dt) {
+      f32x16 a, b;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 a4, b4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g + j;
-          a4[j] = (bf16)((dk[dt][r] + red[(dt * 16 + r) * 64 + lane]) * p.scale);
-          b4[j] = (bf16)(dv[dt][r] + red[(64 + dt * 16 + r) * 64 + lane]);
-        }
-        *reinterpret_cast<bf16x4*>(kp + 32 * dt + 8 * g + 4 * h) = a4;
-        *reinterpret_cast<bf16x4*>(vp + 32 * dt + 8 * g + 4 * h) = b4;
+      for (int r = 0; r < 16; ++r) {
+        a[r] = dk[dt][r] + red[(dt * 16 + r) * 64 + lane];
+        b[r] = dv[dt][r] + red[(64 + dt * 16 + r) * 64 + lane];
       }
+      store_row_block<D>(kp, a, dt, h, p.scale);
+      store_row_block<D>(vp, b, dt, h, 1.f);
+    }
   }
 }
 
 // =====================================================================================
 // backward dQ
 // =====================================================================================
-template <int NW, int PRIO>
+template <int D, int NW, int PRIO>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
-  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
+  constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TL];  // K[2], V[2]
   int blk, hq, b;
   lpt_ids(blk, hq, b);
   int start, len;
@@ -606,12 +608,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   const float c = p.scale * kLog2e;
   const int qr = myq < len ? myq : len - 1;
 
-  bf16x8 qf[8], df[8];
+  bf16x8 qf[KS], df[KS];
   {
     const bf16* qp = p.q + (int64_t)(start + qr) * p.sq + (int64_t)hq * D + 8 * h;
     const bf16* dp = p.dout + (int64_t)(start + qr) * p.sdo + (int64_t)hq * D + 8 * h;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
       df[ks] = *reinterpret_cast<const bf16x8*>(dp + 16 * ks);
     }
@@ -643,24 +645,24 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
       return p.v + (int64_t)(start + r) * p.sv + (int64_t)hk * D;
     };
   };
-  f32x16 dq[4];
+  f32x16 dq[DT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dq[i] = f32x16{};
+  for (int i = 0; i < DT; ++i) dq[i] = f32x16{};
   const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
 
-  stage_tile64<NW>(smem + 0, kptr(kt_begin));
-  stage_tile64<NW>(smem + 2 * 16384, vptr(kt_begin));
+  stage_tile_d<NW, D>(smem + 0, kptr(kt_begin));
+  stage_tile_d<NW, D>(smem + 2 * TL, vptr(kt_begin));
   __syncthreads();
   if constexpr (PRIO != 0 && NW == 8) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = (kt - kt_begin) & 1;
-    const char* Kt = smem + buf * 16384;
-    const char* Vt = smem + 2 * 16384 + buf * 16384;
+    const char* Kt = smem + buf * TL;
+    const char* Vt = smem + 2 * TL + buf * TL;
     if (kt + 1 < kt_end) {
-      stage_tile64<NW>(smem + (buf ^ 1) * 16384, kptr(kt + 1));
-      stage_tile64<NW>(smem + 2 * 16384 + (buf ^ 1) * 16384, vptr(kt + 1));
+      stage_tile_d<NW, D>(smem + (buf ^ 1) * TL, kptr(kt + 1));
+      stage_tile_d<NW, D>(smem + 2 * TL + (buf ^ 1) * TL, vptr(kt + 1));
     }
     const int k0 = kt * BN;
     bool skip = (k0 >= len) || (wq_lo >= len);
@@ -673,9 +675,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
         s[t] = f32x16{};
         dp[t] = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) s[t] = mfma(read_rows(Kt, 32 * t, ks), qf[ks], s[t]);
+        for (int ks = 0; ks < KS; ++ks) s[t] = mfma(rows_d(Kt, 32 * t, ks), qf[ks], s[t]);
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) dp[t] = mfma(read_rows(Vt, 32 * t, ks), df[ks], dp[t]);
+        for (int ks = 0; ks < KS; ++ks) dp[t] = mfma(rows_d(Vt, 32 * t, ks), df[ks], dp[t]);
       }
       // only tiles that straddle the causal diagonal / window edge / sequence end need the per-element mask
       const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
@@ -690,29 +692,23 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
         }
       const bf16x8 sb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int st = 0; st < 4; ++st) dq[dt] = mfma(read_tr(Kt, st, dt), sb[st], dq[dt]);
+        for (int st = 0; st < 4; ++st) dq[dt] = mfma(tr_d(Kt, st, dt), sb[st], dq[dt]);
     }
     __syncthreads();
   }
   if (myq < len) {
     bf16* qp = p.dq + (int64_t)(start + myq) * p.sdq + (int64_t)hq * D;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = (bf16)(dq[dt][4 * g + j] * p.scale);
-        *reinterpret_cast<bf16x4*>(qp + 32 * dt + 8 * g + 4 * h) = v4;
-      }
+    for (int dt = 0; dt < DT; ++dt) store_row_block<D>(qp, dq[dt], dt, h, p.scale);
   }
 }
 
 AttnParams make_params(const void* q, const void* k, const void* v, void* o, float* lse, const void* dout, void* dq,
-                       void* dk, void* dv, float* delta, const int64_t* strides, const int* cu_seqlens, int batch,
-                       int seq_len, int total_tokens, int hq, int hkv, float scale, int causal, int window) {
+                       void* dk, void* dv, float* delta, const int64_t* strides, const int* cu_seqlens,
+                       const int* seq_lens, int batch, int seq_len, int total_tokens, int hq, int hkv, float scale,
+                       int causal, int window) {
   AttnParams p;
   p.q = (const bf16*)q;
   p.k = (const bf16*)k;
@@ -733,6 +729,7 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
   p.sdk = strides[6];
   p.sdv = strides[7];
   p.cu_seqlens = cu_seqlens;
+  p.seq_lens = seq_lens;
   p.seq_len = seq_len;
   p.total_tokens = total_tokens;
   p.batch = batch;
@@ -769,54 +766,119 @@ HDS_EXPORT int hds_attn_config(int fwd_nw, int dkdv_nw, int dq_nw) {
   return 0;
 }
 
+namespace {
+
+template <int D>
+int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t st) {
+  if constexpr (D <= 128) {
+    if (g_fwd_nw == 8) {
+      const dim3 grid((max_len + 255) / 256, hq, batch);
+      if constexpr (D == 128) {  // the A/B variants exist for the training head dim only
+        switch (g_fwd_var) {
+          case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
+          case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
+          case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;
+          default: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 2>), grid, dim3(512), 0, st, p); break;
+        }
+      } else {
+        hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 2>), grid, dim3(512), 0, st, p);
+      }
+      return hipGetLastError();
+    }
+  }
+  // head_dim > 128 keeps 1 wave per SIMD (accumulators need the full register file)
+  hipLaunchKernelGGL((attn_fwd_kernel<D, 4, 2>), dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+template <int D>
+int launch_bwd(const AttnParams& p, int batch, int max_len, int total_tokens, int hq, int hkv, hipStream_t st) {
+  const int64_t rows = (int64_t)total_tokens * hq;
+  hipLaunchKernelGGL(attn_bwd_delta_kernel<D>, dim3((rows + 15) / 16), dim3(256), 0, st, p);
+  bool done = false;
+  if constexpr (D <= 128) {
+    if (g_dkdv_nw == 8) {
+      const dim3 grid((max_len + 127) / 128, hkv, batch);
+      if (g_bwd_prio)
+        hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 1>), grid, dim3(512), 0, st, p);
+      else
+        hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 0>), grid, dim3(512), 0, st, p);
+      done = true;
+    }
+  }
+  if (!done) {
+    const dim3 grid((max_len + 127) / 128, hkv, batch);
+    constexpr int DT = Dim<D>::DT;
+    if constexpr (D <= 128) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, 4>), grid, dim3(256), 0, st, p);
+    } else if constexpr (D < 256) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, 4, 0, DT / 2>), grid, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, 4, DT / 2, DT - DT / 2>), grid, dim3(256), 0, st, p);
+    } else {  // 256: column quarters (K/V fragments alone take 128 registers)
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, 4, 0, 2>), grid, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, 4, 2, 2>), grid, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, 4, 4, 2>), grid, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, 4, 6, 2>), grid, dim3(256), 0, st, p);
+    }
+  }
+  done = false;
+  if constexpr (D <= 128) {
+    if (g_dq_nw == 8) {
+      const dim3 grid((max_len + 255) / 256, hq, batch);
+      if (g_bwd_prio)
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 1>), grid, dim3(512), 0, st, p);
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 0>), grid, dim3(512), 0, st, p);
+      done = true;
+    }
+  }
+  if (!done)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 4, 0>), dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+#define HDS_ATTN_DIMS(X) X(32) X(48) X(64) X(80) X(96) X(112) X(128) X(160) X(192) X(256)
+
+}  // namespace
+
+// head dims with a compiled kernel (for python-side dispatch)
+HDS_EXPORT int hds_attn_head_dim_supported(int head_dim) {
+#define HDS_CASE(d) \
+  if (head_dim == d) return 1;
+  HDS_ATTN_DIMS(HDS_CASE)
+#undef HDS_CASE
+  return 0;
+}
+
 // strides: int64[8] token strides (elements) for q, k, v, o, dout, dq, dk, dv
 // max_len: max sequence length in the batch (grid sizing)
+// seq_lens: optional [B] valid lengths of a right-padded [B, seq_len] batch (key-padding masks); rows past a
+// sequence's length are neither read as keys nor written as outputs
 HDS_EXPORT int hds_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int64_t* strides,
-                            const int* cu_seqlens, int batch, int seq_len, int max_len, int total_tokens, int hq,
-                            int hkv, int head_dim, float scale, int causal, int window, hipStream_t st) {
-  if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
-  AttnParams p = make_params(q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, strides, cu_seqlens, batch,
-                             seq_len, total_tokens, hq, hkv, scale, causal, window);
-  if (g_fwd_nw == 8) {
-    const dim3 grid((max_len + 255) / 256, hq, batch);
-    switch (g_fwd_var) {
-      case 1: hipLaunchKernelGGL((attn_fwd_kernel<8, 1>), grid, dim3(512), 0, st, p); break;
-      case 2: hipLaunchKernelGGL((attn_fwd_kernel<8, 2>), grid, dim3(512), 0, st, p); break;
-      case 3: hipLaunchKernelGGL((attn_fwd_kernel<8, 3>), grid, dim3(512), 0, st, p); break;
-      default: hipLaunchKernelGGL((attn_fwd_kernel<8, 0>), grid, dim3(512), 0, st, p); break;
-    }
-  } else {
-    hipLaunchKernelGGL((attn_fwd_kernel<4, 0>), dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
-  }
-  return hipGetLastError();
+                            const int* cu_seqlens, const int* seq_lens, int batch, int seq_len, int max_len,
+                            int total_tokens, int hq, int hkv, int head_dim, float scale, int causal, int window,
+                            hipStream_t st) {
+  if (hq % hkv) return hipErrorInvalidValue;
+  AttnParams p = make_params(q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, strides, cu_seqlens,
+                             seq_lens, batch, seq_len, total_tokens, hq, hkv, scale, causal, window);
+#define HDS_CASE(d) \
+  if (head_dim == d) return launch_fwd<d>(p, batch, max_len, hq, st);
+  HDS_ATTN_DIMS(HDS_CASE)
+#undef HDS_CASE
+  return hipErrorInvalidValue;
 }
 
 HDS_EXPORT int hds_attn_bwd(const void* q, const void* k, const void* v, const void* o, const float* lse,
                             const void* dout, void* dq, void* dk, void* dv, float* delta, const int64_t* strides,
-                            const int* cu_seqlens, int batch, int seq_len, int max_len, int total_tokens, int hq,
-                            int hkv, int head_dim, float scale, int causal, int window, hipStream_t st) {
-  if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
-  AttnParams p = make_params(q, k, v, (void*)o, (float*)lse, dout, dq, dk, dv, delta, strides, cu_seqlens, batch,
-                             seq_len, total_tokens, hq, hkv, scale, causal, window);
-  const int64_t rows = (int64_t)total_tokens * hq;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, st, p);
-  if (g_dkdv_nw == 8) {
-    const dim3 grid((max_len + 127) / 128, hkv, batch);
-    if (g_bwd_prio)
-      hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel<1>, grid, dim3(512), 0, st, p);
-    else
-      hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel<0>, grid, dim3(512), 0, st, p);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<4>, dim3((max_len + 127) / 128, hkv, batch), dim3(256), 0, st, p);
-  }
-  if (g_dq_nw == 8) {
-    const dim3 grid((max_len + 255) / 256, hq, batch);
-    if (g_bwd_prio)
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<8, 1>), grid, dim3(512), 0, st, p);
-    else
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<8, 0>), grid, dim3(512), 0, st, p);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 0>), dim3((max_len + 127) / 128, hq, batch), dim3(256), 0, st, p);
-  }
-  return hipGetLastError();
+                            const int* cu_seqlens, const int* seq_lens, int batch, int seq_len, int max_len,
+                            int total_tokens, int hq, int hkv, int head_dim, float scale, int causal, int window,
+                            hipStream_t st) {
+  if (hq % hkv) return hipErrorInvalidValue;
+  AttnParams p = make_params(q, k, v, (void*)o, (float*)lse, dout, dq, dk, dv, delta, strides, cu_seqlens, seq_lens,
+                             batch, seq_len, total_tokens, hq, hkv, scale, causal, window);
+#define HDS_CASE(d) \
+  if (head_dim == d) return launch_bwd<d>(p, batch, max_len, total_tokens, hq, hkv, st);
+  HDS_ATTN_DIMS(HDS_CASE)
+#undef HDS_CASE
+  return hipErrorInvalidValue;
 }

@@ -10,6 +10,10 @@
 // (K then V for each slot). Any block_size works: every staged tile row computes its own
 // (block, slot) address, and LDS-DMA takes a per-lane global source address.
 //
+// Head dims: every multiple of 16 up to 256 that flash_attn.hip instantiates (HDS_PAGED_DIMS below), via the
+// generic tile helpers of attn_common.h. The RoPE scatter takes any head_dim % 4 == 0 with a rotary prefix
+// of rot_dim (% 8 == 0) dims -- partial rotary (Phi, GPT-NeoX) rotates the prefix and copies the rest.
+//
 // Attention work unit ("atom"): (sequence, kv head, 128 packed rows). Rows pack the G = Hq/Hkv
 // query heads that share a kv head with the tokens of the chunk (row = token * G + head_in_group),
 // so K/V of a kv head are read ONCE for all of its query heads -- for decode (1 token) one wave
@@ -21,7 +25,6 @@ using namespace hds::attn;
 
 namespace {
 
-constexpr int D = 128;
 constexpr int BN = 64;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -29,15 +32,37 @@ constexpr float kLog2e = 1.4426950408889634f;
 // fused RoPE (q in place, k rotated into the cache) + V copy into the cache
 // ------------------------------------------------------------------------------------------
 template <typename T>
+struct Vec4 {  // 4 x 16-bit elements = one 8-byte access
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  __device__ __forceinline__ static void load(const T* p, float (&v)[4]) {
+    const u2 r = *reinterpret_cast<const u2*>(p);
+    const T* e = reinterpret_cast<const T*>(&r);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (float)e[i];
+  }
+  __device__ __forceinline__ static void store(T* p, const float (&v)[4]) {
+    u2 r;
+    T* e = reinterpret_cast<T*>(&r);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = (T)v[i];
+    *reinterpret_cast<u2*>(p) = r;
+  }
+};
+
+// per head: rot/8 rotation groups of 4 pairs (i, i + rot/2), then (D - rot)/4 plain 4-element chunks. 4-element
+// granularity covers every rotary prefix the HF families use (Phi partial_rotary 0.4 / 0.5 of 80 -> 32 / 40).
+template <typename T>
 __global__ __launch_bounds__(256) void kv_rope_scatter_kernel(T* __restrict__ qkv, int64_t sq, T* __restrict__ cache,
                                                               const int* __restrict__ tok_seq,
                                                               const int* __restrict__ tok_pos,
                                                               const int* __restrict__ block_tables, int max_blocks,
                                                               const float* __restrict__ cos_t,
                                                               const float* __restrict__ sin_t, int n_tok, int hq,
-                                                              int hkv, int block_size, int rotate_q, int do_rope) {
-  const int half = D / 2;
-  const int gph = D / 16;  // thread groups per head (8 rotation pairs each)
+                                                              int hkv, int D, int rot, int block_size, int rotate_q,
+                                                              int do_rope) {
+  const int half = rot / 2;
+  const int nrot = rot / 8;
+  const int gph = nrot + (D - rot) / 4;
   const int heads = hq + 2 * hkv;
   const int64_t total = (int64_t)n_tok * heads * gph;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
@@ -47,38 +72,40 @@ __global__ __launch_bounds__(256) void kv_rope_scatter_kernel(T* __restrict__ qk
     if (h < hq && !rotate_q) continue;
     const int pos = tok_pos[t];
     T* src = qkv + (int64_t)t * sq + (int64_t)h * D;
-    float a[8], b[8];
-    Vec8<T>::load(src + g * 8, a);
-    Vec8<T>::load(src + half + g * 8, b);
-    if (h < hq + hkv && do_rope) {
-      float c[8], s[8];
-      Vec8<float>::load(cos_t + (int64_t)pos * half + g * 8, c);
-      Vec8<float>::load(sin_t + (int64_t)pos * half + g * 8, s);
-      float oa[8], ob[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        oa[j] = a[j] * c[j] - b[j] * s[j];
-        ob[j] = b[j] * c[j] + a[j] * s[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        a[j] = oa[j];
-        b[j] = ob[j];
-      }
+    T* dst = nullptr;
+    if (h >= hq) {
+      const int kv = (h < hq + hkv) ? 0 : 1;
+      const int hk = h - hq - kv * hkv;
+      const int seq = tok_seq[t];
+      const int blk = block_tables[(int64_t)seq * max_blocks + pos / block_size];
+      const int slot = pos % block_size;
+      dst = cache + ((((int64_t)blk * block_size + slot) * 2 + kv) * hkv + hk) * D;
     }
-    if (h < hq) {
-      Vec8<T>::store(src + g * 8, a);
-      Vec8<T>::store(src + half + g * 8, b);
+    if (g >= nrot) {  // un-rotated tail (and every V chunk past the rotary prefix)
+      if (dst == nullptr) continue;
+      const int c0 = rot + (g - nrot) * 4;
+      float a[4];
+      Vec4<T>::load(src + c0, a);
+      Vec4<T>::store(dst + c0, a);
       continue;
     }
-    const int kv = (h < hq + hkv) ? 0 : 1;
-    const int hk = h - hq - kv * hkv;
-    const int seq = tok_seq[t];
-    const int blk = block_tables[(int64_t)seq * max_blocks + pos / block_size];
-    const int slot = pos % block_size;
-    T* dst = cache + ((((int64_t)blk * block_size + slot) * 2 + kv) * hkv + hk) * D;
-    Vec8<T>::store(dst + g * 8, a);
-    Vec8<T>::store(dst + half + g * 8, b);
+    float a[4], b[4];
+    Vec4<T>::load(src + g * 4, a);
+    Vec4<T>::load(src + half + g * 4, b);
+    if (h < hq + hkv && do_rope) {
+      const f32x4 c = *reinterpret_cast<const f32x4*>(cos_t + (int64_t)pos * half + g * 4);
+      const f32x4 sn = *reinterpret_cast<const f32x4*>(sin_t + (int64_t)pos * half + g * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float oa = a[j] * c[j] - b[j] * sn[j];
+        const float ob = b[j] * c[j] + a[j] * sn[j];
+        a[j] = oa;
+        b[j] = ob;
+      }
+    }
+    T* out = dst != nullptr ? dst : src;  // q rotates in place
+    Vec4<T>::store(out + g * 4, a);
+    Vec4<T>::store(out + half + g * 4, b);
   }
 }
 
@@ -100,9 +127,10 @@ struct PagedParams {
   int window;
 };
 
-template <int NW>
+template <int D, int NW>
 __global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];  // K[2], V[2]
+  constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TL];  // K[2], V[2]
   const int* at = p.atoms + blockIdx.x * 3;
   const int seq = at[0], hk = at[1], row_start = at[2];
   const int q_start = p.seq_meta[seq * 3], n_new = p.seq_meta[seq * 3 + 1], seen = p.seq_meta[seq * 3 + 2];
@@ -118,11 +146,11 @@ __global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
   const int* table = p.block_tables + (int64_t)seq * p.max_blocks;
   const int64_t kv_row = 2LL * p.hkv * D;  // elements between consecutive slots
 
-  bf16x8 qf[8];
+  bf16x8 qf[KS];
   {
     const bf16* qp = p.q + (int64_t)(q_start + tok) * p.sq + (int64_t)head * D + 8 * h;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
   }
   // last query position covered by this workgroup (rows are token-major)
   const int last_row = min(row_start + 32 * NW, n_rows) - 1;
@@ -148,21 +176,21 @@ __global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
   const int w_qpos_hi = seen + min(w_row_lo + 31, n_rows - 1) / G;
   const bool wave_active = w_row_lo < n_rows;
 
-  f32x16 o[4];
+  f32x16 o[DT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x16{};
+  for (int i = 0; i < DT; ++i) o[i] = f32x16{};
   float m = -INFINITY, l = 0.f;
 
-  stage_tile64<NW>(smem, rowp(kt_begin, 0));
-  stage_tile64<NW>(smem + 2 * 16384, rowp(kt_begin, 1));
+  stage_tile_d<NW, D>(smem, rowp(kt_begin, 0));
+  stage_tile_d<NW, D>(smem + 2 * TL, rowp(kt_begin, 1));
   __syncthreads();
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = (kt - kt_begin) & 1;
-    const char* Kt = smem + buf * 16384;
-    const char* Vt = smem + 2 * 16384 + buf * 16384;
+    const char* Kt = smem + buf * TL;
+    const char* Vt = smem + 2 * TL + buf * TL;
     if (kt + 1 < kt_end) {
-      stage_tile64<NW>(smem + (buf ^ 1) * 16384, rowp(kt + 1, 0));
-      stage_tile64<NW>(smem + 2 * 16384 + (buf ^ 1) * 16384, rowp(kt + 1, 1));
+      stage_tile_d<NW, D>(smem + (buf ^ 1) * TL, rowp(kt + 1, 0));
+      stage_tile_d<NW, D>(smem + 2 * TL + (buf ^ 1) * TL, rowp(kt + 1, 1));
     }
     const int k0 = kt * BN;
     bool skip = !wave_active || k0 > w_qpos_hi;
@@ -173,7 +201,7 @@ __global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
       for (int t = 0; t < 2; ++t) {
         s[t] = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) s[t] = mfma(read_rows(Kt, 32 * t, ks), qf[ks], s[t]);
+        for (int ks = 0; ks < KS; ++ks) s[t] = mfma(rows_d(Kt, 32 * t, ks), qf[ks], s[t]);
       }
       float tmax = -INFINITY;
 #pragma unroll
@@ -204,13 +232,13 @@ __global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
       m = mnew;
       if (__any(alpha != 1.f)) {
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
       }
       const bf16x8 pb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int st = 0; st < 4; ++st) o[dt] = mfma(read_tr(Vt, st, dt), pb[st], o[dt]);
+        for (int st = 0; st < 4; ++st) o[dt] = mfma(tr_d(Vt, st, dt), pb[st], o[dt]);
     }
     __syncthreads();
   }
@@ -218,33 +246,32 @@ __global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     bf16* op = p.o + ((int64_t)(q_start + tok) * p.hq + head) * D;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = (bf16)(o[dt][4 * g + j] * inv);
-        *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g + 4 * h) = v4;
-      }
+    for (int dt = 0; dt < DT; ++dt) store_row_block<D>(op, o[dt], dt, h, inv);
   }
 }
 
 }  // namespace
 
+#define HDS_PAGED_DIMS(X) X(32) X(48) X(64) X(80) X(96) X(112) X(128) X(160) X(192) X(256)
+
+// rot_dim: rotary prefix (0 = the whole head); cos/sin tables are [pos][rot_dim / 2]
 HDS_EXPORT int hds_kv_rope_scatter(int dtype, void* qkv, int64_t sq, void* cache, const int* tok_seq,
                                    const int* tok_pos, const int* block_tables, int max_blocks, const float* cos_t,
-                                   const float* sin_t, int n_tok, int hq, int hkv, int head_dim, int block_size,
-                                   int rotate_q, int do_rope, hipStream_t st) {
-  if (head_dim != D || n_tok <= 0) return n_tok <= 0 ? 0 : hipErrorInvalidValue;
-  const int64_t work = (int64_t)n_tok * (hq + 2 * hkv) * (D / 16);
+                                   const float* sin_t, int n_tok, int hq, int hkv, int head_dim, int rot_dim,
+                                   int block_size, int rotate_q, int do_rope, hipStream_t st) {
+  if (n_tok <= 0) return 0;
+  const int rot = (rot_dim <= 0 || rot_dim > head_dim) ? head_dim : rot_dim;
+  if (head_dim % 4 || rot % 8 || (head_dim - rot) % 4) return hipErrorInvalidValue;
+  const int64_t work = (int64_t)n_tok * (hq + 2 * hkv) * (rot / 8 + (head_dim - rot) / 4);
   dim3 grid(stream_grid(work, 256, 4096)), block(256);
   if (dtype == kBF16)
     hipLaunchKernelGGL(kv_rope_scatter_kernel<bf16>, grid, block, 0, st, (bf16*)qkv, sq, (bf16*)cache, tok_seq, tok_pos,
-                       block_tables, max_blocks, cos_t, sin_t, n_tok, hq, hkv, block_size, rotate_q, do_rope);
+                       block_tables, max_blocks, cos_t, sin_t, n_tok, hq, hkv, head_dim, rot, block_size, rotate_q,
+                       do_rope);
   else if (dtype == kF16)
     hipLaunchKernelGGL(kv_rope_scatter_kernel<_Float16>, grid, block, 0, st, (_Float16*)qkv, sq, (_Float16*)cache,
-                       tok_seq, tok_pos, block_tables, max_blocks, cos_t, sin_t, n_tok, hq, hkv, block_size, rotate_q,
-                       do_rope);
+                       tok_seq, tok_pos, block_tables, max_blocks, cos_t, sin_t, n_tok, hq, hkv, head_dim, rot,
+                       block_size, rotate_q, do_rope);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -254,12 +281,18 @@ HDS_EXPORT int hds_kv_rope_scatter(int dtype, void* qkv, int64_t sq, void* cache
 HDS_EXPORT int hds_paged_attn(const void* q, int64_t sq, const void* cache, void* o, const int* atoms, int n_atoms,
                               const int* seq_meta, const int* block_tables, int max_blocks, int block_size, int hq,
                               int hkv, int head_dim, float scale, int window, hipStream_t st) {
-  if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
+  if (hq % hkv) return hipErrorInvalidValue;
   if (n_atoms <= 0) return 0;
   PagedParams p{(const bf16*)q, sq, (const bf16*)cache, (bf16*)o, atoms, seq_meta, block_tables, max_blocks,
                 block_size, hq, hkv, scale, window};
-  hipLaunchKernelGGL(paged_attn_kernel<4>, dim3(n_atoms), dim3(256), 0, st, p);
-  return hipGetLastError();
+#define HDS_CASE(d)                                                                          \
+  if (head_dim == d) {                                                                       \
+    hipLaunchKernelGGL((paged_attn_kernel<d, 4>), dim3(n_atoms), dim3(256), 0, st, p);       \
+    return hipGetLastError();                                                                \
+  }
+  HDS_PAGED_DIMS(HDS_CASE)
+#undef HDS_CASE
+  return hipErrorInvalidValue;
 }
 
 HDS_EXPORT int hds_paged_rows_per_atom() { return 128; }

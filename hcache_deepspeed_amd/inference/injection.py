@@ -166,12 +166,12 @@ def _inject_up_act(module):
 
 def _hds_attention(module, query, key, value, attention_mask, scaling, dropout=0.0, **kwargs):
     """transformers AttentionInterface function: q [B,H,Sq,D], k/v [B,Hkv,Skv,D] -> ([B,Sq,H,D], None)."""
-    from ..ops.attention import flash_attn
+    from ..ops.attention import flash_attn, head_dim_supported
     B, H, Sq, D = query.shape
     Skv = key.shape[2]
     causal = bool(getattr(module, "is_causal", True))
-    use_flash = (query.is_cuda and D == 128 and Sq == Skv and query.dtype == torch.bfloat16 and causal and
-                 dropout == 0.0)
+    use_flash = (query.is_cuda and head_dim_supported(D) and Sq == Skv and query.dtype == torch.bfloat16 and causal
+                 and dropout == 0.0)
     if use_flash:
         o = flash_attn(query.transpose(1, 2), key.transpose(1, 2).contiguous(), value.transpose(1, 2).contiguous(),
                        causal=True, softmax_scale=scaling)

@@ -13,7 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.activations import bias_act
-from ..ops.attention import flash_attn
+from ..ops.attention import flash_attn, native_supported
 from ..ops.cross_entropy import fused_linear_cross_entropy
 from ..ops.norm import LayerNorm
 from ..runtime.activation_checkpointing.checkpointing import checkpoint as _ckpt
@@ -76,7 +76,7 @@ class GPT2Block(nn.Module):
         D = H // self.n_head
         qkv = self.c_attn(x).view(B, S, 3, self.n_head, D)
         q, k, v = qkv.unbind(2)
-        if x.is_cuda and D == 128 and x.dtype == torch.bfloat16:
+        if native_supported(x.view(-1, self.n_head, D)):
             o = flash_attn(q.contiguous(), k.contiguous(), v.contiguous(), causal=True)
         else:
             o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),

@@ -4,6 +4,10 @@ Reference parity: replaces ``BlockedFlashAttn`` (inference/v2/kernels/ragged_ops
 a prebuilt NVIDIA-only library), the ``flash_attn`` dependency of FPDT
 (sequence/fpdt_layer.py:234-254) and the training attention that HF models run unfused.
 
+Head dims: every multiple of 16 up to 256 that the kernel library instantiates (32 ... 256, see
+``head_dim_supported``) runs the HIP kernels; bf16 only. A right-padded batch with a key-padding mask runs
+the same kernels with per-sequence lengths (``seq_lens``).
+
 Two entry points:
 
 * :func:`flash_attn` -- q/k/v as ``[B, S, H, D]`` or varlen ``[T, H, D]`` + ``cu_seqlens``;
@@ -20,7 +24,14 @@ import torch
 from . import native
 from .rope import rope_
 
-_HEAD_DIMS_NATIVE = (128, )
+_HEAD_DIMS_NATIVE = (32, 48, 64, 80, 96, 112, 128, 160, 192, 256)  # mirrors HDS_ATTN_DIMS in flash_attn.hip
+
+
+def head_dim_supported(d):
+    """True when the HIP attention kernels are instantiated for head_dim ``d``."""
+    if torch.cuda.is_available():
+        return bool(native.kernels().hds_attn_head_dim_supported(int(d)))
+    return d in _HEAD_DIMS_NATIVE
 
 
 def _strides8(*ts):
@@ -78,24 +89,26 @@ def _ref_attention(q, k, v, causal, scale, cu_seqlens, seq_len, window):
     return o.to(q.dtype), lse
 
 
-def _native_fwd(q, k, v, o, lse, causal, scale, cu, B, seq_len, max_len, window):
+def _native_fwd(q, k, v, o, lse, causal, scale, cu, B, seq_len, max_len, window, seq_lens=None):
     T, Hq, D = q.shape
     strides = _strides8(q, k, v, o)
     native.check(
         native.kernels().hds_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
-                                      strides.data_ptr(), native.ptr(cu), B, seq_len, max_len, T, Hq, k.shape[1], D,
-                                      float(scale), int(causal), int(window), native.stream()), "attn_fwd")
+                                      strides.data_ptr(), native.ptr(cu), native.ptr(seq_lens), B, seq_len, max_len,
+                                      T, Hq, k.shape[1], D, float(scale), int(causal), int(window), native.stream()),
+        "attn_fwd")
 
 
-def _native_bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, cu, B, seq_len, max_len, window):
+def _native_bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, cu, B, seq_len, max_len, window, seq_lens=None):
     T, Hq, D = q.shape
     delta = torch.empty(Hq, T, device=q.device, dtype=torch.float32)
     strides = _strides8(q, k, v, o, do, dq, dk, dv)
     native.check(
         native.kernels().hds_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
                                       do.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), delta.data_ptr(),
-                                      strides.data_ptr(), native.ptr(cu), B, seq_len, max_len, T, Hq, k.shape[1], D,
-                                      float(scale), int(causal), int(window), native.stream()), "attn_bwd")
+                                      strides.data_ptr(), native.ptr(cu), native.ptr(seq_lens), B, seq_len, max_len,
+                                      T, Hq, k.shape[1], D, float(scale), int(causal), int(window), native.stream()),
+        "attn_bwd")
 
 
 def _ref_bwd(q, k, v, do, causal, scale, cu_seqlens, seq_len, window):
@@ -136,41 +149,73 @@ def _ref_attention_f32(q, k, v, causal, scale, cu_seqlens, seq_len, window):
 
 
 def native_supported(q):
-    return native.use_native(q) and q.shape[-1] in _HEAD_DIMS_NATIVE and q.dtype == torch.bfloat16
+    """bf16 on the GPU with an instantiated head dim -> HIP kernels. A bf16 GPU tensor with any other head dim is
+    an error (no silent fp32 fallback on the device); fp16/fp32 inputs use the fp32 reference."""
+    if not (native.use_native(q) and q.dtype == torch.bfloat16):
+        return False
+    if not head_dim_supported(q.shape[-1]):
+        raise NotImplementedError(f"HIP attention: head_dim {q.shape[-1]} is not instantiated "
+                                  f"(supported: multiples of 16 up to 256)")
+    return True
+
+
+def _padded_ref(q, k, v, causal, scale, seq_len, window, seq_lens):
+    """Reference for a right-padded batch: each sequence's first seq_lens[b] rows; padded outputs are zero."""
+    lens = seq_lens.tolist()
+    o = torch.zeros(q.shape, dtype=q.dtype, device=q.device)
+    lse = torch.full((q.shape[1], q.shape[0]), float("-inf"), dtype=torch.float32, device=q.device)
+    for b, L in enumerate(lens):
+        s = b * seq_len
+        if L > 0:
+            ob, lb = _ref_attention(q[s:s + L], k[s:s + L], v[s:s + L], causal, scale, None, L, window)
+            o[s:s + L] = ob
+            lse[:, s:s + L] = lb
+    return o, lse
 
 
 class _FlashAttnFn(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale, cu_seqlens, seq_len, window, return_lse):
+    def forward(ctx, q, k, v, causal, scale, cu_seqlens, seq_len, window, return_lse, seq_lens):
         T, Hq, D = q.shape
         cu, B, sl, max_len = _cu_info(cu_seqlens, T, seq_len)
+        sls = None if seq_lens is None else seq_lens.to(device=q.device, dtype=torch.int32).contiguous()
         if native_supported(q):
-            o = torch.empty(T, Hq, D, device=q.device, dtype=q.dtype)
+            alloc = torch.zeros if sls is not None else torch.empty  # padded rows are never written
+            o = alloc(T, Hq, D, device=q.device, dtype=q.dtype)
             lse = torch.empty(Hq, T, device=q.device, dtype=torch.float32)
-            _native_fwd(q, k, v, o, lse, causal, scale, cu, B, sl, max_len, window)
+            _native_fwd(q, k, v, o, lse, causal, scale, cu, B, sl, max_len, window, sls)
+        elif sls is not None:
+            o, lse = _padded_ref(q, k, v, causal, scale, seq_len, window, sls)
         else:
             o, lse = _ref_attention(q, k, v, causal, scale, cu_seqlens, seq_len, window)
-        ctx.save_for_backward(q, k, v, o, lse, cu_seqlens)
+        ctx.save_for_backward(q, k, v, o, lse, cu_seqlens, sls)
         ctx.args = (causal, scale, seq_len, window)
         ctx.mark_non_differentiable(lse)
         return o, lse
 
     @staticmethod
     def backward(ctx, do, dlse):
-        q, k, v, o, lse, cu_seqlens = ctx.saved_tensors
+        q, k, v, o, lse, cu_seqlens, sls = ctx.saved_tensors
         causal, scale, seq_len, window = ctx.args
         T = q.shape[0]
         cu, B, sl, max_len = _cu_info(cu_seqlens, T, seq_len)
         if native_supported(q):
-            dq = torch.empty_like(q, memory_format=torch.contiguous_format)
-            dk = torch.empty(k.shape, device=k.device, dtype=k.dtype)
-            dv = torch.empty(v.shape, device=v.device, dtype=v.dtype)
-            _native_bwd(q, k, v, o, lse, do.contiguous(), dq, dk, dv, causal, scale, cu, B, sl, max_len, window)
+            alloc = torch.zeros if sls is not None else torch.empty
+            dq = alloc(q.shape, device=q.device, dtype=q.dtype)
+            dk = alloc(k.shape, device=k.device, dtype=k.dtype)
+            dv = alloc(v.shape, device=v.device, dtype=v.dtype)
+            _native_bwd(q, k, v, o, lse, do.contiguous(), dq, dk, dv, causal, scale, cu, B, sl, max_len, window, sls)
+        elif sls is not None:
+            with torch.enable_grad():
+                qf, kf, vf = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+                of, _ = _padded_ref(qf, kf, vf, causal, scale, seq_len, window, sls)
+                dq, dk, dv = torch.autograd.grad(of, (qf, kf, vf), do.float())
+            dq, dk, dv = dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
         else:
             dq, dk, dv = _ref_bwd(q, k, v, do, causal, scale, cu_seqlens, seq_len, window)
             dq, dk, dv = dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
-        return dq, dk, dv, None, None, None, None, None, None
+        return dq, dk, dv, None, None, None, None, None, None, None
 
 
 def _count_attn_flops(T, H, D, seq_len, causal, cu_seqlens):
@@ -186,8 +231,11 @@ def _count_attn_flops(T, H, D, seq_len, causal, cu_seqlens):
     counters.add(4 * pairs * H * D, 2 * pairs * H * D, "flash_attn")
 
 
-def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window=0, return_lse=False):
-    """q: [B, S, Hq, D] or [T, Hq, D] (+cu_seqlens); k/v: [.., Hkv, D]. Returns o like q (and lse [Hq, T])."""
+def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window=0, return_lse=False, seq_lens=None):
+    """q: [B, S, Hq, D] or [T, Hq, D] (+cu_seqlens); k/v: [.., Hkv, D]. Returns o like q (and lse [Hq, T]).
+
+    seq_lens: optional int [B] valid lengths of a right-padded [B, S] batch (a key-padding mask); outputs and
+    gradients of padded rows are zero."""
     batched = q.dim() == 4
     if batched:
         B, S = q.shape[:2]
@@ -201,7 +249,7 @@ def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     _count_attn_flops(q3.shape[0], q3.shape[1], q3.shape[2], seq_len, causal, cu_seqlens)
     o, lse = _FlashAttnFn.apply(q3, k3, v3, bool(causal), float(scale), cu_seqlens, int(seq_len), int(window or 0),
-                                return_lse)
+                                return_lse, seq_lens)
     if batched:
         o = o.view(q.shape)
     return (o, lse) if return_lse else o
@@ -327,6 +375,21 @@ def attn_block_bwd(q, k, v, o, lse, do, causal, scale, seq_len):
         _native_bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, None, T // seq_len, seq_len, seq_len, 0)
         return dq, dk, dv
     return _ref_block_bwd(q, k, v, o, lse, do, causal, scale, seq_len)
+
+
+def padding_mask_lengths(mask, seq_len):
+    """Valid lengths ``[B]`` if an additive attention mask ([B, 1, 1, S] or [B, S]; 0 = keep, large negative =
+    drop) is a right-padding key mask, else None (the caller then needs a general masked attention)."""
+    m = mask.reshape(mask.shape[0], -1) if mask.dim() == 4 and mask.shape[1] == 1 and mask.shape[2] == 1 else \
+        (mask if mask.dim() == 2 else None)
+    if m is None or m.shape[-1] != seq_len:
+        return None
+    keep = m > -1.0  # 0 keeps; masked positions hold -10000 / finfo.min
+    lens = keep.sum(-1, dtype=torch.int32)
+    prefix = torch.arange(seq_len, device=m.device)[None, :] < lens[:, None]
+    if not bool(torch.equal(keep, prefix)) or bool((m[keep] != 0).any()):
+        return None
+    return lens
 
 
 def merge_attn_out(o, lse, o_blk, lse_blk):

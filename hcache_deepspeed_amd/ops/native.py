@@ -36,14 +36,15 @@ _KERNEL_SIGS = {
     "hds_sumsq": "iplpps",
     "hds_clip_coef": "pffpps",
     "hds_xent": "i" + "pppp" + "l" + "i" + "l" + "i" + "f" + "i" + "f" + "s",
-    "hds_attn_fwd": "p" * 7 + "i" * 7 + "f" + "ii" + "s",
-    "hds_attn_bwd": "p" * 12 + "i" * 7 + "f" + "ii" + "s",
+    "hds_attn_fwd": "p" * 8 + "i" * 7 + "f" + "ii" + "s",
+    "hds_attn_bwd": "p" * 13 + "i" * 7 + "f" + "ii" + "s",
+    "hds_attn_head_dim_supported": "i",
     "hds_attn_config": "iii",
     "hds_attn_fwd_variant": "i",
     "hds_attn_bwd_prio": "i",
     "hds_bsattn_fwd": "p" * 8 + "i" * 7 + "f" + "i" + "s",
     "hds_bsattn_bwd": "p" * 15 + "i" * 7 + "f" + "i" + "s",
-    "hds_kv_rope_scatter": "i" + "p" + "l" + "pppp" + "i" + "pp" + "i" * 7 + "s",
+    "hds_kv_rope_scatter": "i" + "p" + "l" + "pppp" + "i" + "pp" + "i" * 8 + "s",
     "hds_paged_attn": "p" + "l" + "ppp" + "i" + "pp" + "i" * 5 + "f" + "i" + "s",
     "hds_paged_rows_per_atom": "",
     "hds_moe_dispatch": "i" + "pppp" + "iiii" + "s",

@@ -11,7 +11,10 @@ from . import native
 ROWS_PER_ATOM = 128
 
 
-KERNEL_HEAD_DIM = 128  # head size the HIP serving kernels are built for; other sizes take the torch path
+def kernel_head_dim_ok(D):
+    """The HIP serving kernels are instantiated for the same head dims as the training FlashAttention."""
+    from .attention import head_dim_supported
+    return head_dim_supported(D)
 
 
 def kv_rope_scatter(qkv, cache, tok_seq, tok_pos, block_tables, cos, sin, n_q, n_kv, rotate_q=True, do_rope=True,
@@ -25,12 +28,15 @@ def kv_rope_scatter(qkv, cache, tok_seq, tok_pos, block_tables, cos, sin, n_q, n
     T, NH, D = qkv.shape
     bs = cache.shape[1]
     partial = do_rope and 0 < rotary_dim < D
-    if native.use_native(qkv) and D == KERNEL_HEAD_DIM and not partial:
+    if native.use_native(qkv):
+        rd = rotary_dim if partial else D
+        if D % 4 or rd % 8:
+            raise NotImplementedError(f"kv_rope_scatter: head_dim {D} / rotary_dim {rd} not supported on the GPU")
         native.check(
             native.kernels().hds_kv_rope_scatter(native.dt(qkv), qkv.data_ptr(), qkv.stride(0), cache.data_ptr(),
                                                  tok_seq.data_ptr(), tok_pos.data_ptr(), block_tables.data_ptr(),
                                                  block_tables.shape[1], cos.data_ptr() if do_rope else None,
-                                                 sin.data_ptr() if do_rope else None, T, n_q, n_kv, D, bs,
+                                                 sin.data_ptr() if do_rope else None, T, n_q, n_kv, D, rd, bs,
                                                  int(rotate_q), int(do_rope), native.stream()), "kv_rope_scatter")
         return
     pos = tok_pos.long()
@@ -74,7 +80,9 @@ def paged_attention(q, cache, atoms, n_atoms, seq_meta, block_tables, n_q, n_kv,
     """q: [T, n_q, D] (token-strided view ok). Returns o [T, n_q, D]."""
     T, _, D = q.shape
     o = torch.empty(T, n_q, D, device=q.device, dtype=q.dtype)
-    if native.use_native(q) and D == KERNEL_HEAD_DIM:
+    if native.use_native(q):
+        if not kernel_head_dim_ok(D) or q.dtype != torch.bfloat16:
+            raise NotImplementedError(f"paged_attention: head_dim {D} / {q.dtype} has no HIP kernel")
         native.check(
             native.kernels().hds_paged_attn(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(),
                                             atoms.data_ptr(), n_atoms, seq_meta.data_ptr(), block_tables.data_ptr(),

@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..activations import bias_act
-from ..attention import flash_attn
+from ..attention import flash_attn, native_supported, padding_mask_lengths
 from ..norm import layer_norm
 
 
@@ -136,8 +136,12 @@ class DeepSpeedTransformerLayer(nn.Module):
         d = c.hidden_size // nh
         p_drop = c.attn_dropout_ratio if (self.training and c.attn_dropout_ratio > 0) else 0.0
         q, k, v = qkv.view(B, S, 3, nh, d).unbind(2)
-        if mask is None and p_drop == 0.0 and qkv.is_cuda and qkv.dtype == torch.bfloat16 and d == 128:
-            return flash_attn(q.contiguous(), k.contiguous(), v.contiguous(), causal=False).reshape(B * S, -1)
+        if p_drop == 0.0 and native_supported(q):
+            # a right-padding key mask (the BERT case) runs the HIP kernel with per-sequence lengths
+            lens = None if mask is None else self._mask_lengths(mask, S)
+            if mask is None or lens is not None:
+                return flash_attn(q.contiguous(), k.contiguous(), v.contiguous(), causal=False,
+                                  seq_lens=lens).reshape(B * S, -1)
         qh, kh, vh = (t.transpose(1, 2) for t in (q, k, v))
         s = torch.matmul(qh, kh.transpose(-1, -2)).float() / math.sqrt(d)
         if mask is not None:
@@ -146,6 +150,17 @@ class DeepSpeedTransformerLayer(nn.Module):
         if p_drop > 0:
             p = F.dropout(p, p_drop, True)
         return torch.matmul(p.to(vh.dtype), vh).transpose(1, 2).reshape(B * S, -1)
+
+    _mask_cache = (None, None, None)
+
+    @classmethod
+    def _mask_lengths(cls, mask, S):
+        """Per-sequence lengths of a padding mask, computed once per mask tensor (every layer of a forward shares
+        it) so the host sync of the prefix check is paid once per step, not once per layer."""
+        key = (mask.data_ptr(), mask._version, tuple(mask.shape))
+        if cls._mask_cache[0] != key:
+            cls._mask_cache = (key, padding_mask_lengths(mask, S), None)
+        return cls._mask_cache[1]
 
     def _dropout(self, x):
         r = self.config.hidden_dropout_ratio

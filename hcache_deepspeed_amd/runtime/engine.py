@@ -192,10 +192,16 @@ class DeepSpeedEngine(nn.Module):
     # configuration
     # ------------------------------------------------------------------------------------
     def _configure_distributed_model(self, model):
-        # meta (zero.Init) parameters stay meta: ZeRO-3 materialises them unit by unit
+        # zero.Init-partitioned parameters stay partitioned for ZeRO-3 (the optimizer moves the per-parameter
+        # partitions into its flat units); other stages need the full values back
+        from .zero.partition_parameters import is_init_partitioned, unpartition_init_param
+        if self.zero_optimization_stage() != 3:
+            for p in model.parameters():
+                if is_init_partitioned(p):
+                    unpartition_init_param(p, device=self.device)
         with torch.no_grad():
             for p in model.parameters():
-                if p.is_meta:
+                if p.is_meta or is_init_partitioned(p):
                     continue
                 if p.is_floating_point() and p.dtype != self.compute_dtype:
                     p.data = p.data.to(self.compute_dtype)
@@ -210,8 +216,8 @@ class DeepSpeedEngine(nn.Module):
             src = dist.get_global_rank(self.dp_group, 0) if self.dp_group is not None else 0
             with torch.no_grad():
                 for p in model.parameters():
-                    if p.is_meta:
-                        continue
+                    if p.is_meta or is_init_partitioned(p):
+                        continue  # Init partitions were built from rank 0's broadcast values
                     eg = groups.expert_data_group_of(p)
                     if eg is not False:
                         # expert params: replicas live in the expert-data-parallel group only

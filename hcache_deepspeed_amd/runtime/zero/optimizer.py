@@ -95,9 +95,20 @@ class _PreBackward(torch.autograd.Function):
         return (None, None) + grads
 
 
-def discover_stage3_units(module, leaf_modules=()):
-    """ZeRO-3 fetch units: each element of top-level ModuleLists (transformer blocks) and any module
-    whose class is in ``leaf_modules``; everything else -> one root unit kept gathered for the step."""
+def _numel(p):
+    return int(getattr(p, "ds_numel", p.numel()))
+
+
+def discover_stage3_units(module, leaf_modules=(), persistence_threshold=0, bucket_numel=0):
+    """ZeRO-3 fetch units as (name, [modules], params-or-None).
+
+    * each element of a ModuleList (transformer blocks) and every module whose class is in ``leaf_modules``;
+    * models without any ModuleList (``nn.Sequential`` stacks, custom nets) fall back to per-submodule units:
+      modules that own parameters, in registration order, bucketed up to ``bucket_numel`` elements so a fetch
+      is one all-gather of a few tens of MB (reference parameter_offload.py:281-460 fetches per submodule).
+      Parameters below ``persistence_threshold`` elements stay in the persistent root unit
+      (stage3_param_persistence_threshold).
+    Everything else -> one root unit kept gathered for the step."""
     units, claimed = [], set()
     leaf_modules = tuple(leaf_modules)
     for name, m in module.named_modules():
@@ -113,6 +124,24 @@ def discover_stage3_units(module, leaf_modules=()):
                 if any(True for _ in child.parameters()):
                     units.append((cname, child))
                 claimed.add(cname)
+    units = [(n, [m], None) for n, m in units]
+    if units or bucket_numel <= 0:
+        return units
+    seen, cur, size = set(), None, 0
+    for name, m in module.named_modules():
+        own = [p for p in m.parameters(recurse=False)
+               if id(p) not in seen and _numel(p) >= max(1, persistence_threshold)]
+        if not own:
+            continue
+        seen.update(id(p) for p in own)
+        n = sum(_numel(p) for p in own)
+        if cur is None or size + n > bucket_numel:
+            cur = (name or "module", [], [])
+            units.append(cur)
+            size = 0
+        cur[1].append(m)
+        cur[2].extend(own)
+        size += n
     return units
 
 
@@ -199,6 +228,7 @@ class ZeroOptimizer:
         self._rep_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._rep_ranges = self._replicated_ranges() if self.mp_group is not None else []
         self._fwd_trace, self._trace_ok, self._trace_pos = [], False, 0
+        self._last_pre_uid = None
         self._recording = True
         self.prefetch_depth = max(0, int(self.mi.zero3_prefetch_depth))
         # parameter-coordinator policy (reference partitioned_param_coordinator.py:380-441,524-555 and
@@ -371,19 +401,33 @@ class ZeroOptimizer:
                     claimed.update(id(p) for p in ps)
                     u = self._new_unit(units, ps, [group_of[id(p)] for p in ps], name, key)
                     u.module = m
-            cands = discover_stage3_units(self.module, leaf_modules)
+            bucket = int(float(getattr(self.mi, "zero3_unit_bucket_mb", 128)) * 2**20) // \
+                torch.tensor([], dtype=self.dtype).element_size()
+            cands = discover_stage3_units(self.module, leaf_modules, int(self.zcfg.param_persistence_threshold),
+                                          bucket)
+
+            def cand_params(c):
+                return c[2] if c[2] is not None else list(c[1][0].parameters())
+
             count = {}
-            for _, m in cands:
-                for p in m.parameters():
+            for c in cands:
+                for p in cand_params(c):
                     count[id(p)] = count.get(id(p), 0) + 1
-            for name, m in cands:
-                ps = [p for p in m.parameters() if id(p) in group_of and count[id(p)] == 1 and id(p) not in claimed
-                      and self._comm_key(p) is None]
+            # a parameter used by several modules (tied weights) is only safe in the persistent root unit
+            uses = {}
+            for _, p in self.module.named_parameters(remove_duplicate=False):
+                uses[id(p)] = uses.get(id(p), 0) + 1
+            shared = {k for k, v in uses.items() if v > 1}
+            for c in cands:
+                name, mods = c[0], c[1]
+                ps = [p for p in cand_params(c) if id(p) in group_of and count[id(p)] == 1 and id(p) not in claimed
+                      and self._comm_key(p) is None and (c[2] is None or id(p) not in shared)]
                 if not ps:
                     continue
                 claimed.update(id(p) for p in ps)
                 u = self._new_unit(units, ps, [group_of[id(p)] for p in ps], name, None)
-                u.module = m
+                u.module = mods[0]
+                u.modules = mods
             rest = {}
             for p in params_all:
                 if id(p) not in claimed:
@@ -430,17 +474,26 @@ class ZeroOptimizer:
         dev = self.device
         self.store = ShardStore(self.units, self.dtype, dev, self.grad_acc_dtype, lp_host=self.offload_param)
         self.direct_grads = all(u.direct for u in self.units)
-        from .partition_parameters import materialize_unit
+        from .partition_parameters import is_init_partitioned
         with torch.no_grad():
             for u in self.units:
-                seed = int(self.config.seed or 1234) + 7919 * u.uid
-                if u.expert_key is not None:
-                    seed += 1000003 * (1 + self._ep_rank(u.expert_key))  # distinct experts per EP rank
-                repl = materialize_unit(u, dev, self.dtype, seed=seed)
-                if repl:
-                    self._swap_params(u, repl)
                 lp = self.store.lp_slice(u)
-                if self.offload_param:
+                init_parts = [is_init_partitioned(p) for p in u.params]
+                if any(init_parts):
+                    # zero.Init: per-parameter partitions -> this unit's flat shard (one reduce-scatter)
+                    shard32 = self._shard_from_init_parts(u, init_parts)
+                    lp.copy_(shard32)
+                    u._init_master = shard32
+                    full = None
+                    if u.world == 1 and not self.offload_param:
+                        full = lp
+                    elif u.persistent:
+                        full = torch.empty(u.padded, dtype=self.dtype, device=dev)
+                        dist.all_gather_into_tensor(full, lp.to(dev), group=u.dp_group)
+                    for p in u.params:
+                        for a in ("_hds_part", "_hds_part_group", "_hds_part_world", "_hds_part_rank"):
+                            p.__dict__.pop(a, None)
+                elif self.offload_param:
                     full = torch.empty(u.padded, dtype=self.dtype, device=dev)
                     u.copy_params_into(full)
                     lp.copy_(full[u.rank * u.shard:(u.rank + 1) * u.shard])  # D2H into pinned host shard
@@ -455,6 +508,9 @@ class ZeroOptimizer:
                 for p in u.params:
                     p.ds_tensor = lp
                 if u.persistent or (u.world == 1 and not self.offload_param):
+                    if full is None:  # offloaded world-1 unit built from Init partitions
+                        full = torch.empty(u.padded, dtype=self.dtype, device=dev)
+                        full.copy_(lp)
                     u.full = full
                     u.bind_params(full)
                     u.status = AVAILABLE
@@ -471,11 +527,47 @@ class ZeroOptimizer:
                     if u.status == AVAILABLE:
                         u.bind_grads(u.grad_full)
             self.store.master = self.store.lp.float()
+            for u in self.units:  # Init partitions carry the full-precision initial values
+                m32 = u.__dict__.pop("_init_master", None)
+                if m32 is not None:
+                    self.store.master[u.store_off:u.store_off + u.shard].copy_(m32)
             if not getattr(self, "_defer_states", False):
                 self._init_states()
         for p in (p for u in self.units for p in u.params):
             p.ds_status = self.param_to_unit[id(p)][0].status
             p._hds_zero = self
+
+    def _shard_from_init_parts(self, u, init_parts):
+        """fp32 shard of unit ``u`` assembled from zero.Init per-parameter partitions. Each rank places its slice
+        of every parameter at the parameter's offset in a zero unit buffer; a reduce-scatter over the unit's
+        group sums the disjoint slices. When the Init group differs from the unit's group (MiCS shards, expert
+        or TP groups) the parameters are all-gathered over the Init group instead."""
+        from .partition_parameters import gather_init_param
+        dev = self.device
+        same = all(not f or (p._hds_part_world == u.world and p._hds_part_rank == u.rank and
+                             (u.world == 1 or p._hds_part_group is u.dp_group or
+                              (p._hds_part_group is None and u.dp_group is None)))
+                   for p, f in zip(u.params, init_parts))
+        contrib = torch.zeros(u.padded, dtype=torch.float32, device=dev)
+        for i, (p, f) in enumerate(zip(u.params, init_parts)):
+            off, n = u.offsets[i], u.numels[i]
+            if not f:
+                if u.rank == 0 or not same:  # a regular parameter: counted once in the reduce-scatter sum
+                    contrib[off:off + n].copy_(p.data.reshape(-1))
+                continue
+            if same:
+                part = p._hds_part
+                pn = part.numel()
+                lo, hi = u.rank * pn, min(n, (u.rank + 1) * pn)
+                if hi > lo:
+                    contrib[off + lo:off + hi].copy_(part[:hi - lo])
+            else:
+                contrib[off:off + n].copy_(gather_init_param(p).reshape(-1))
+        if u.world > 1 and same:
+            out = torch.empty(u.shard, dtype=torch.float32, device=dev)
+            dist.reduce_scatter_tensor(out, contrib, group=u.dp_group)
+            return out
+        return contrib[u.rank * u.shard:(u.rank + 1) * u.shard].clone()
 
     def _replicated_ranges(self):
         """Store ranges (of MY shard) holding TP-replicated parameters: counted once in the global norm."""
@@ -489,22 +581,6 @@ class ZeroOptimizer:
                 if a < b:
                     out.append((u.store_off + a - lo, u.store_off + b - lo))
         return out
-
-    def _swap_params(self, u, repl):
-        """Replace materialised meta parameters everywhere this optimizer references them."""
-        for i, p in enumerate(u.params):
-            if id(p) in repl:
-                new = repl[id(p)]
-                for attr in ("ds_shape", "ds_numel"):
-                    setattr(new, attr, getattr(p, attr))
-                new.ds_id = id(new)
-                self.param_to_unit.pop(id(p), None)
-                self.param_to_unit[id(new)] = (u, i)
-                if id(p) in self.param_names:
-                    self.param_names[id(new)] = self.param_names.pop(id(p))
-                u.params[i] = new
-        for group in self.param_groups:
-            group["params"] = [repl.get(id(p), p) for p in group["params"]]
 
     def _init_states(self):
         s = self.store
@@ -543,8 +619,23 @@ class ZeroOptimizer:
             for u in self.units:
                 if u.persistent or u.module is None:
                     continue
-                self._hook_handles.append(u.module.register_forward_pre_hook(self._make_pre_fwd(u)))
-                self._hook_handles.append(u.module.register_forward_hook(self._make_post_fwd(u)))
+                mods = getattr(u, "modules", None) or [u.module]
+                for j, m in enumerate(mods):
+                    self._hook_handles.append(m.register_forward_pre_hook(self._make_pre_fwd(u)))
+                    # a bucket unit spanning several modules is released after its LAST module's forward
+                    self._hook_handles.append(m.register_forward_hook(self._make_post_fwd(u, release=j == len(mods) - 1)))
+            # register_external_parameter: a module whose forward uses another unit's parameter gathers that unit
+            for m in self.module.modules():
+                ext = getattr(m, "_external_params", None)
+                if not ext:
+                    continue
+                ext_units = []
+                for p in ext.values():
+                    hit = self.param_to_unit.get(id(p))
+                    if hit is not None and not hit[0].persistent and hit[0] not in ext_units:
+                        ext_units.append(hit[0])
+                for u in ext_units:
+                    self._hook_handles.append(m.register_forward_pre_hook(self._make_ext_pre(u)))
 
     def _make_grad_hook(self, u):
 
@@ -558,18 +649,27 @@ class ZeroOptimizer:
     def _make_pre_fwd(self, u):
 
         def pre(module, args):
-            self._record_and_prefetch(u)
+            if self._last_pre_uid != u.uid:  # a bucket unit's later modules do not re-enter the trace
+                self._last_pre_uid = u.uid
+                self._record_and_prefetch(u)
             self._gather(u, wait=True)
 
         return pre
 
-    def _make_post_fwd(self, u):
+    def _make_ext_pre(self, u):
+
+        def pre(module, args):
+            self._gather(u, wait=True)  # external parameter: kept until its own unit's release
+
+        return pre
+
+    def _make_post_fwd(self, u, release=True):
 
         def post(module, args, output):
             grad_on = torch.is_grad_enabled()
             if grad_on and not self.in_backward:
                 output = self._wrap_outputs(u, output)
-            if self._partitioned(u) and not self.in_backward and not self._is_last_in_trace(u) and \
+            if release and self._partitioned(u) and not self.in_backward and not self._is_last_in_trace(u) and \
                     u.uid not in self._reuse_keep:
                 self._release(u)
             return output
@@ -958,6 +1058,7 @@ class ZeroOptimizer:
     # forward bracket (called by the engine around module.forward)
     # ------------------------------------------------------------------------------------
     def pre_forward(self):
+        self._last_pre_uid = None
         self._trace_pos = 0
         self._trace_ok = bool(self._fwd_trace) and not self._recording
         for u in self.root_units:

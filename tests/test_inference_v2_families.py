@@ -112,12 +112,25 @@ def test_hf_checkpoint_dir_and_serialize_roundtrip(family, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("family", ["llama", "mixtral", "qwen2_moe", "phi3", "phi", "falcon_new", "opt"])
-def test_family_parity_gpu(family):
-    """HIP paged attention / fused RoPE+KV-scatter path (head_dim 128) on every block structure."""
+@pytest.mark.parametrize("family,H", [("llama", 512), ("mixtral", 512), ("qwen2_moe", 512), ("phi3", 512),
+                                      ("phi", 512), ("falcon_new", 512), ("opt", 512),
+                                      # the families' real head dims: Phi 80 (partial rotary 32), Phi-3 96,
+                                      # Falcon / OPT 64, and a 256-wide head
+                                      ("phi", 320), ("phi3", 384), ("falcon", 256), ("opt", 256), ("llama", 1024)])
+def test_family_parity_gpu(family, H, monkeypatch):
+    """HIP paged attention / fused RoPE+KV-scatter path (head_dim H/4) on every block structure; the torch
+    reference serving path is disabled so a silent fallback fails the test."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    m = _families(H=512)[family]()
+    from hcache_deepspeed_amd.ops import paged as P
+    real = P.paged_attention
+
+    def hip_only(q, *a, **k):
+        assert q.is_cuda
+        return real(q, *a, **k)
+
+    monkeypatch.setattr(P, "paged_attention", hip_only)
+    m = _families(H=H)[family]()
     torch.manual_seed(0)
     m = _randomize(m.float().eval())
     eng = build_engine_from_hf_model(m, {"dtype": "bf16", "latent_mode": "kv",

@@ -236,6 +236,68 @@ def test_flash_attn_fwd_bwd(S, Hq, Hkv, causal, window):
     assert _rel(v.grad.reshape(B * S, Hkv, D), vr.grad) < 2e-2
 
 
+@pytest.fixture
+def no_attn_fallback(monkeypatch):
+    """Fail the test if the fp32 torch reference attention runs instead of the HIP kernels."""
+    from hcache_deepspeed_amd.ops import attention as A
+
+    def boom(*a, **k):
+        raise AssertionError("torch reference attention ran on the GPU path")
+
+    monkeypatch.setattr(A, "_ref_attention", boom)
+    monkeypatch.setattr(A, "_padded_ref", boom)
+    monkeypatch.setattr(A, "_ref_bwd", boom)
+
+
+@pytest.mark.parametrize("D", [32, 48, 64, 80, 96, 112, 160, 192, 256])
+@pytest.mark.parametrize("causal,window", [(True, 0), (False, 0), (True, 97)])
+def test_flash_attn_head_dims(D, causal, window, no_attn_fallback):
+    """Every instantiated head dim (GPT-2/BERT/Falcon/OPT 64, Phi 80, Phi-3 96, Gemma 256, ...) on the HIP path
+    against the fp32 reference, forward and backward, GQA, ragged tile edges."""
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    B, S, Hq, Hkv = 2, 333, 4, 2
+    torch.manual_seed(D)
+    q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn(q, k, v, causal=causal, window=window)
+    qr, kr, vr = (t.detach().float().reshape(B * S, t.shape[2], D).requires_grad_(True) for t in (q, k, v))
+    orf = _attn_ref(qr, kr, vr, causal, window, None, S)
+    assert _rel(o.reshape(B * S, Hq, D), orf) < 1e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float().reshape(B * S, Hq, D))
+    assert _rel(q.grad.reshape(B * S, Hq, D), qr.grad) < 2e-2
+    assert _rel(k.grad.reshape(B * S, Hkv, D), kr.grad) < 2e-2
+    assert _rel(v.grad.reshape(B * S, Hkv, D), vr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_flash_attn_padding_seq_lens(D, no_attn_fallback):
+    """Right-padded batch + key-padding lengths (the BERT mask case) on the HIP kernels: valid rows match the
+    per-sequence reference, padded rows and their gradients are zero."""
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    B, S, H = 3, 200, 4
+    lens = torch.tensor([200, 77, 1], dtype=torch.int32)
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn(q, k, v, causal=False, seq_lens=lens.cuda())
+    do = torch.randn_like(o)
+    o.backward(do)
+    for b, L in enumerate(lens.tolist()):
+        qr, kr, vr = (t.detach()[b, :L].float().requires_grad_(True) for t in (q, k, v))
+        orf = _attn_ref(qr, kr, vr, False, 0, None, L)
+        assert _rel(o[b, :L], orf) < 1e-2
+        orf.backward(do[b, :L].float())
+        for got, want in ((q.grad[b, :L], qr.grad), (k.grad[b, :L], kr.grad), (v.grad[b, :L], vr.grad)):
+            # L == 1: softmax is exactly 1, so dq / dk are 0 up to rounding -- compare absolutely there
+            err = (got.float() - want).norm().item()
+            assert err < 2e-2 * want.norm().item() + 1e-4 * math.sqrt(want.numel())
+        assert o[b, L:].abs().max().item() == 0 if L < S else True
+        assert k.grad[b, L:].abs().max().item() == 0 if L < S else True
+
+
 def test_flash_attn_varlen():
     from hcache_deepspeed_amd.ops.attention import flash_attn
     lens = [17, 300, 1, 129, 64]
@@ -288,7 +350,7 @@ def test_qkv_attention_matches_unfused():
     assert _rel(qkv.grad, x1.grad) < 2e-2
 
 
-def _paged_setup(lens, seen, Hq=8, Hkv=2, D=128, bs=64, nblocks=64):
+def _paged_setup(lens, seen, Hq=8, Hkv=2, D=128, bs=64, nblocks=64, rot=None):
     from hcache_deepspeed_amd.ops.rope import rope_tables
     torch.manual_seed(3)
     cache = torch.randn(nblocks, bs, 2, Hkv, D, device="cuda", dtype=torch.bfloat16)
@@ -304,29 +366,32 @@ def _paged_setup(lens, seen, Hq=8, Hkv=2, D=128, bs=64, nblocks=64):
     tab = torch.zeros(len(lens), maxb, dtype=torch.int32)
     for i, t in enumerate(tables):
         tab[i, :len(t)] = torch.tensor(t)
-    return cache, tab, metas, off, rope_tables(4096, D, 10000.0, device="cuda")
+    return cache, tab, metas, off, rope_tables(4096, rot or D, 10000.0, device="cuda")
 
 
-def test_kv_rope_scatter_matches_reference():
+@pytest.mark.parametrize("D,rot", [(128, 0), (64, 0), (80, 32), (80, 40), (96, 0), (256, 64)])
+def test_kv_rope_scatter_matches_reference(D, rot):
+    """Fused RoPE + paged KV scatter for every serving head dim, incl. partial rotary (Phi: 80 / 32)."""
     from hcache_deepspeed_amd.ops.paged import kv_rope_scatter
     lens, seen = [5, 70, 1], [0, 10, 200]
-    Hq, Hkv, D = 8, 2, 128
-    cache, tab, metas, T, (cos, sin) = _paged_setup(lens, seen)
+    Hq, Hkv = 8, 2
+    cache, tab, metas, T, (cos, sin) = _paged_setup(lens, seen, D=D, rot=rot)
     tok_seq = torch.cat([torch.full((n, ), i, dtype=torch.int32) for i, n in enumerate(lens)])
     tok_pos = torch.cat([torch.arange(s, s + n, dtype=torch.int32) for n, s in zip(lens, seen)])
     qkv = torch.randn(T, Hq + 2 * Hkv, D, device="cuda", dtype=torch.bfloat16)
     q2, c2 = qkv.clone().cpu().float(), cache.clone().cpu().float()
-    kv_rope_scatter(qkv, cache, tok_seq.cuda(), tok_pos.cuda(), tab.cuda(), cos, sin, Hq, Hkv)
-    kv_rope_scatter(q2, c2, tok_seq, tok_pos, tab, cos.cpu(), sin.cpu(), Hq, Hkv)
+    kv_rope_scatter(qkv, cache, tok_seq.cuda(), tok_pos.cuda(), tab.cuda(), cos, sin, Hq, Hkv, rotary_dim=rot)
+    kv_rope_scatter(q2, c2, tok_seq, tok_pos, tab, cos.cpu(), sin.cpu(), Hq, Hkv, rotary_dim=rot)
     assert _rel(qkv.cpu(), q2) < 1e-2
     assert _rel(cache.cpu(), c2) < 1e-2
 
 
+@pytest.mark.parametrize("D", [128, 64, 80, 96, 256])
 @pytest.mark.parametrize("lens,seen", [([1, 1, 1], [100, 5, 700]), ([130, 64, 3], [0, 0, 0]), ([37, 1], [90, 333])])
-def test_paged_attention_matches_reference(lens, seen):
+def test_paged_attention_matches_reference(lens, seen, D):
     from hcache_deepspeed_amd.ops.paged import build_atoms, paged_attention
-    Hq, Hkv, D = 8, 2, 128
-    cache, tab, metas, T, _ = _paged_setup(lens, seen)
+    Hq, Hkv = 8, 2
+    cache, tab, metas, T, _ = _paged_setup(lens, seen, D=D)
     q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16)
     atoms, n = build_atoms(metas, Hq, Hkv)
     meta = torch.tensor(metas, dtype=torch.int32)

@@ -84,3 +84,35 @@ def test_transformer_layer_gpu_flash_path():
     assert rel(out, ref) < 2e-2
     for a, b in zip(ga, gb):
         assert rel(a, b) < 3e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,heads", [(768, 12), (512, 4)])
+def test_transformer_layer_gpu_padding_mask(H, heads, monkeypatch):
+    """BERT-base shape (head_dim 64) with a right-padding attention mask: the HIP FlashAttention runs with
+    per-sequence lengths (the torch attention is disabled), valid rows match the fp32 masked reference."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hcache_deepspeed_amd.ops.transformer import transformer as TL
+    calls = []
+    real = TL.flash_attn
+
+    def spy(*a, **k):
+        calls.append(k.get("seq_lens"))
+        return real(*a, **k)
+
+    monkeypatch.setattr(TL, "flash_attn", spy)
+    torch.manual_seed(2)
+    layer = DeepSpeedTransformerLayer(_cfg(False, H=H, heads=heads)).cuda().bfloat16()
+    B, S = 3, 128
+    lens = [128, 50, 7]
+    mask = torch.zeros(B, 1, 1, S, device="cuda")
+    for b, L in enumerate(lens):
+        mask[b, ..., L:] = -10000.0
+    x = torch.randn(B, S, H, device="cuda").bfloat16().requires_grad_(True)
+    out = layer(x, mask.bfloat16())
+    assert calls and calls[0] is not None and calls[0].tolist() == lens  # HIP kernel with per-sequence lengths
+    ref = _ref(layer, x, mask)
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    for b, L in enumerate(lens):
+        assert rel(out[b, :L], ref[b, :L]) < 2e-2
