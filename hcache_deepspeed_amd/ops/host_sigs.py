@@ -37,6 +37,9 @@ SIGS = {
     "hds_aio_pread": (I, [P, P, L, ctypes.c_char_p, L, I]),
     "hds_aio_pwrite": (I, [P, P, L, ctypes.c_char_p, L, I]),
     "hds_aio_wait": (L, [P]),
+    "hds_aio_submit": (L, [P, I, P, L, ctypes.c_char_p, L]),
+    "hds_aio_wait_req": (I, [P, L]),
+    "hds_aio_engine": (I, [P]),
     "hds_aio_file_size": (L, [ctypes.c_char_p]),
     # rccl_comm.cpp
     "hds_rccl_load": (I, [ctypes.c_char_p]),

@@ -24,6 +24,9 @@ int hds_aio_destroy(void* h);
 int hds_aio_pread(void* h, void* buf, int64_t bytes, const char* path, int64_t off, int async_op);
 int hds_aio_pwrite(void* h, const void* buf, int64_t bytes, const char* path, int64_t off, int async_op);
 int64_t hds_aio_wait(void* h);
+int64_t hds_aio_submit(void* h, int write, void* buf, int64_t bytes, const char* path, int64_t off);
+int hds_aio_wait_req(void* h, int64_t id);
+int hds_aio_engine(void* h);
 void* hds_shm_open(const char* name, int rank, int world, int64_t slot_bytes, int create);
 int hds_shm_close(void* h, int unlink);
 int hds_shm_allreduce(void* h, void* buf, int64_t n, int dtype);
@@ -90,7 +93,7 @@ static void test_adam() {
     }
 }
 
-static void test_aio(const char* dir) {
+static void test_aio_engine(const char* dir) {
   const int64_t bytes = (3 << 20) + 12345;
   std::vector<unsigned char> src(bytes), dst(bytes, 0);
   for (int64_t i = 0; i < bytes; ++i) src[i] = (unsigned char)(i * 131 + 7);
@@ -101,8 +104,36 @@ static void test_aio(const char* dir) {
   CHECK(hds_aio_wait(h) >= 1, "aio wait write");
   CHECK(hds_aio_pread(h, dst.data(), bytes, path.c_str(), 0, 0) == 0, "aio pread");
   CHECK(memcmp(src.data(), dst.data(), bytes) == 0, "aio round trip mismatch");
+  // many tracked requests in flight (more chunks than queue slots), waited out of order
+  const int nreq = 12;
+  const int64_t rb = (1 << 20) + 4096 * 3;
+  std::vector<std::vector<unsigned char>> bufs(nreq, std::vector<unsigned char>(rb));
+  std::vector<int64_t> ids;
+  for (int r = 0; r < nreq; ++r) {
+    for (int64_t i = 0; i < rb; ++i) bufs[r][i] = (unsigned char)(i * 7 + r);
+    ids.push_back(hds_aio_submit(h, 1, bufs[r].data(), rb, path.c_str(), r * rb));
+    CHECK(ids.back() > 0, "aio submit write");
+  }
+  for (int r = nreq - 1; r >= 0; --r) CHECK(hds_aio_wait_req(h, ids[r]) == 0, "aio wait_req write %d", r);
+  std::vector<unsigned char> back(rb);
+  for (int r = 0; r < nreq; ++r) {
+    const int64_t id = hds_aio_submit(h, 0, back.data(), rb, path.c_str(), r * rb);
+    CHECK(hds_aio_wait_req(h, id) == 0, "aio wait_req read");
+    CHECK(memcmp(back.data(), bufs[r].data(), rb) == 0, "aio request %d mismatch", r);
+  }
+  CHECK(hds_aio_wait_req(h, 999999) != 0, "unknown request id must fail");
   hds_aio_destroy(h);
   unlink(path.c_str());
+}
+
+static void test_aio(const char* dir) {
+  test_aio_engine(dir);  // io_uring when the kernel allows it
+  setenv("HDS_AIO_ENGINE", "threads", 1);
+  void* h = hds_aio_create(1 << 20, 8, 0, 1, 4);
+  CHECK(hds_aio_engine(h) == 0, "HDS_AIO_ENGINE=threads must select the thread pool");
+  hds_aio_destroy(h);
+  test_aio_engine(dir);
+  unsetenv("HDS_AIO_ENGINE");
 }
 
 static void test_shm() {
