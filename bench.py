@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--offload", choices=["none", "cpu", "nvme"], default="none",
                     help="ZeRO-Offload/Infinity of optimizer states (+ params with --offload-param)")
     ap.add_argument("--offload-param", action="store_true")
+    ap.add_argument("--nvme-path", default="/tmp/hds_nvme", help="swap folder of the NVMe tier (--offload nvme)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
     args = ap.parse_args()
     tuned = _use_tuned_gemms()
@@ -113,6 +114,11 @@ def main():
         ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True}
         if args.offload_param:
             ds_config["zero_optimization"]["offload_param"] = {"device": args.offload, "pin_memory": True}
+        if args.offload == "nvme":
+            for k in ("offload_optimizer", "offload_param"):
+                if k in ds_config["zero_optimization"]:
+                    ds_config["zero_optimization"][k]["nvme_path"] = args.nvme_path
+            ds_config["aio"] = {"block_size": 1 << 20, "queue_depth": 64, "intra_op_parallelism": 8}
     t_init = time.time()
     with hds.zero.Init(enabled=args.zero == 3):
         model = build(cfg_model)
@@ -184,6 +190,17 @@ def main():
                       "init_s": round(t_init, 1), "valid": on_gpu and not bool(args.layers),
                       "tuned_gemm_table": tuned, "device": "mi355x" if on_gpu else "cpu-dry-run"},
         }
+        zo = engine.optimizer
+        sw = getattr(zo, "opt_swapper", None)
+        if sw is not None:  # ZeRO-Infinity NVMe tier: how much of the optimizer's swap I/O hid behind CPU Adam
+            out["extra"]["nvme_opt"] = {"read_gib": round(sw.bytes_read / 2**30, 2),
+                                        "written_gib": round(sw.bytes_written / 2**30, 2),
+                                        "step_io_wait_s": round(sw.wait_s, 2), "step_pipeline_s": round(sw.step_s, 2),
+                                        "engine": zo.nvme.engine}
+        ps = getattr(zo, "param_swapper", None)
+        if ps is not None:
+            out["extra"]["nvme_param"] = {"read_gib": round(ps.bytes_read / 2**30, 2),
+                                          "written_gib": round(ps.bytes_written / 2**30, 2)}
         print(json.dumps(out), flush=True)
     tdist.barrier()
     tdist.destroy_process_group()

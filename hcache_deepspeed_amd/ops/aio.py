@@ -1,12 +1,32 @@
 """Async tensor file I/O handle (reference: ``AsyncIOBuilder().load().aio_handle`` -- csrc/aio/py_lib/py_ds_aio.cpp
-:19-115, and the GDS handle ``GDSBuilder().load().gds_handle``). Backed by csrc/host/aio.cpp (thread pool,
-O_DIRECT for 4 KiB aligned pinned buffers).
+:19-115, and the GDS handle ``GDSBuilder().load().gds_handle``). Backed by csrc/host/aio.cpp: io_uring (raw
+syscalls, block_size chunks, queue_depth in flight) or a pread/pwrite thread pool; O_DIRECT for 4 KiB aligned
+pinned buffers. Beyond the reference API, :meth:`aio_handle.submit_read` / :meth:`aio_handle.submit_write` return an
+:class:`AioRequest` whose ``wait()`` blocks on that request only (what a read-ahead / write-behind pipeline needs).
 """
 import os
 
 import torch
 
 from . import native
+
+
+class AioRequest:
+    """One in-flight tracked transfer; keeps its buffer alive until waited."""
+
+    __slots__ = ("handle", "rid", "buffer", "done")
+
+    def __init__(self, handle, rid, buffer):
+        self.handle, self.rid, self.buffer, self.done = handle, rid, buffer, False
+
+    def wait(self):
+        if not self.done:
+            rc = self.handle._lib.hds_aio_wait_req(self.handle.h, self.rid)
+            self.done = True
+            self.buffer = None
+            if rc != 0:
+                raise IOError(f"aio request {self.rid} failed ({rc})")
+        return True
 
 
 class aio_handle:
@@ -36,6 +56,24 @@ class aio_handle:
 
     def get_intra_op_parallelism(self):
         return self.intra_op_parallelism
+
+    @property
+    def engine(self):
+        """"io_uring" or "threads"."""
+        return "io_uring" if self._lib.hds_aio_engine(self.h) == 1 else "threads"
+
+    def _submit(self, write, buffer, filename, file_offset):
+        p, n = self._buf(buffer)
+        rid = self._lib.hds_aio_submit(self.h, int(write), p, n, filename.encode(), int(file_offset))
+        if rid <= 0:
+            raise IOError(f"aio {'write' if write else 'read'} of {filename} failed to submit ({rid})")
+        return AioRequest(self, rid, buffer)
+
+    def submit_read(self, buffer, filename, file_offset=0):
+        return self._submit(False, buffer, filename, file_offset)
+
+    def submit_write(self, buffer, filename, file_offset=0):
+        return self._submit(True, buffer, filename, file_offset)
 
     def _buf(self, t):
         assert not t.is_cuda, "aio buffers must be host tensors (pinned preferred)"

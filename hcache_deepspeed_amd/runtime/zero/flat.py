@@ -132,7 +132,10 @@ class ShardStore:
             total += u.shard
         self.numel = total
         self.device = device
-        if lp_host:
+        if lp_host == "nvme":
+            # ZeRO-Infinity NVMe tier: the shard lives in the parameter swap file (runtime/swap_tensor)
+            self.lp = torch.empty(0, dtype=dtype)
+        elif lp_host:
             # ZeRO-Infinity parameter offload: the compute-dtype shard lives in pinned host memory
             pin = torch.cuda.is_available()
             self.lp = torch.zeros(total, dtype=dtype, device="cpu", pin_memory=pin)

@@ -60,12 +60,29 @@ class OffloadZeroOptimizer(ZeroOptimizer):
         self.lp_on_host = s.lp.device.type == "cpu" and self.device.type == "cuda"
         assert not (self.lp_on_host and self.n_off < n), "offload_param requires offload_optimizer.ratio == 1"
         self.sub = max(1 << 20, min(int(self.zcfg.sub_group_size), self.n_off or 1))
-        # host copies of the offloaded range
-        self.h_master = _host_empty(self.n_off, torch.float32, False)
-        self.h_master.copy_(s.master[:self.n_off].cpu())
-        if self.n_off == n:
-            s.master = None  # free before the host state buffers are allocated
-        self.h_states = {k: torch.zeros(self.n_off, dtype=torch.float32) for k in s.states}
+        self.nvme = None
+        if self.offload_device == "nvme":
+            # fp32 master + moments of the offloaded range on NVMe, streamed by the step in chunks of at most
+            # 64M elements (3 pinned staging slots per state: read-ahead / in use / write-behind)
+            from ..swap_tensor import PipelinedOptimizerSwapper
+            from ..swap_tensor.aio_config import make_aio_handle
+            self.sub = min(self.sub, 64 << 20)
+            folder = os.path.join(oc.nvme_path or "/tmp/hds_nvme", "zero_stage_3", "optimizer", f"rank{dist.get_rank()}")
+            self.nvme = make_aio_handle(self.config.aio_config)
+            keys = ["fp32"] + list(self._STATE_KEYS[self.kind])
+            self.opt_swapper = PipelinedOptimizerSwapper(self.nvme, folder, keys, self.n_off, self.sub)
+            self.opt_swapper.write_full("fp32", s.master[:self.n_off].cpu())
+            for k in keys[1:]:
+                self.opt_swapper.write_full(k, None)
+            self.h_master = None
+            self.h_states = {k: None for k in keys[1:]}
+        else:
+            # host copies of the offloaded range
+            self.h_master = _host_empty(self.n_off, torch.float32, False)
+            self.h_master.copy_(s.master[:self.n_off].cpu())
+            if self.n_off == n:
+                s.master = None  # free before the host state buffers are allocated
+            self.h_states = {k: torch.zeros(self.n_off, dtype=torch.float32) for k in s.states}
         # double-buffered pinned staging: grads D2H (chunk k+1) / bf16 params H2D (chunk k-1)
         self.h_grad = [_host_empty(self.sub, s.grad.dtype, self.pin) for _ in range(2)]
         self.h_lp = [_host_empty(self.sub, self.dtype, self.pin) for _ in range(2)]
@@ -75,35 +92,9 @@ class OffloadZeroOptimizer(ZeroOptimizer):
             s.states = {k: None for k in s.states}
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None  # D2H
         self.h2d_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None  # H2D
-        self.nvme = None
-        if self.offload_device == "nvme":
-            from ...ops.aio import aio_handle
-            path = oc.nvme_path or "/tmp/hds_nvme"
-            os.makedirs(path, exist_ok=True)
-            self.nvme_dir = path
-            aio = self.config.aio_config
-            self.nvme = aio_handle(aio.get("block_size", 1 << 20), aio.get("queue_depth", 8),
-                                   aio.get("single_submit", False), aio.get("overlap_events", True),
-                                   aio.get("intra_op_parallelism", 4))
-            for k, v in self.h_states.items():
-                self.nvme.sync_pwrite(v, self._nvme_file(k))
-            self.h_states = {k: None for k in self.h_states}
         log_dist(f"ZeRO-Offload: {self.n_off / 1e6:.1f}M of {n / 1e6:.1f}M elements on {self.offload_device} "
-                 f"(sub-group {self.sub / 1e6:.1f}M)", ranks=[0])
-
-    def _nvme_file(self, k):
-        return os.path.join(self.nvme_dir, f"rank{dist.get_rank()}_{k}.bin")
-
-    def _state_chunk(self, k, lo, hi, buf_cache):
-        if self.nvme is None:
-            return self.h_states[k][lo:hi]
-        t = buf_cache.get(k)
-        if t is None or t.numel() < hi - lo:
-            t = torch.empty(hi - lo, dtype=torch.float32)
-            buf_cache[k] = t
-        t = t[:hi - lo]
-        self.nvme.sync_pread(t, self._nvme_file(k), file_offset=lo * 4)
-        return t
+                 f"(sub-group {self.sub / 1e6:.1f}M)" + (", parameters on NVMe" if self.nvme_param else ""),
+                 ranks=[0])
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -139,10 +130,11 @@ class OffloadZeroOptimizer(ZeroOptimizer):
                 e = min(hi, lo + self.sub)
                 bounds.append((lo, e, seg.group))
                 lo = e
-        cache = {}
         dev_grad = s.grad
         gpu = self.copy_stream is not None
         d2h_ev, h2d_ev = [None, None], [None, None]
+        lp_writes = [None, None]  # NVMe parameter tier: pending swap-file write of each bf16 staging buffer
+        swap = self.opt_swapper.pipeline(bounds) if self.nvme is not None else None
 
         def issue_d2h(i):
             lo, hi, _ = bounds[i]
@@ -171,29 +163,37 @@ class OffloadZeroOptimizer(ZeroOptimizer):
                     h2d_ev[b].synchronize()  # staging buffer b is free again
             hg = self.h_grad[b][:n]
             g = self.param_groups[gi]
-            p32 = self.h_master[lo:hi]
-            # parameters offloaded too: the CPU optimizer writes bf16 straight into the pinned lp shard
-            out = s.lp[lo:hi] if self.lp_on_host else self.h_lp[b][:n]
-            if self.kind in ("adam", "generic"):
-                m = self._state_chunk("exp_avg", lo, hi, cache)
-                v = self._state_chunk("exp_avg_sq", lo, hi, cache)
-                cpu_adam_flat(p32, hg, m, v, g["step"], g["lr"], tuple(g.get("betas", (0.9, 0.999))),
-                              g.get("eps", 1e-8), g.get("weight_decay", 0.0), self.adamw,
-                              g.get("bias_correction", True), bf16_out=out if self.dtype == torch.bfloat16 else None,
-                              grad_scale=coef)
-                if self.nvme is not None:
-                    self.nvme.sync_pwrite(m, self._nvme_file("exp_avg"), file_offset=lo * 4)
-                    self.nvme.sync_pwrite(v, self._nvme_file("exp_avg_sq"), file_offset=lo * 4)
-            elif self.kind == "lion":
-                m = self._state_chunk("exp_avg", lo, hi, cache)
-                cpu_lion_flat(p32, hg, m, g["lr"], tuple(g.get("betas", (0.9, 0.99))), g.get("weight_decay", 0.0),
-                              bf16_out=out if self.dtype == torch.bfloat16 else None, grad_scale=coef)
+            if swap is not None:  # NVMe: this chunk's master / moments, read ahead by the swapper
+                _, st = next(swap)
+                p32 = st["fp32"]
             else:
-                st = self._state_chunk("sum", lo, hi, cache)
-                cpu_adagrad_flat(p32, hg, st, g["lr"], g.get("eps", 1e-10), g.get("weight_decay", 0.0),
+                st = {k: v[lo:hi] for k, v in self.h_states.items()}
+                p32 = self.h_master[lo:hi]
+            if self.nvme_param:
+                if lp_writes[b] is not None:
+                    lp_writes[b].wait()  # staging buffer b's previous swap-file write has landed
+                    lp_writes[b] = None
+                out = self.h_lp[b][:n]
+            else:
+                # parameters offloaded too: the CPU optimizer writes bf16 straight into the pinned lp shard
+                out = s.lp[lo:hi] if self.lp_on_host else self.h_lp[b][:n]
+            if self.kind in ("adam", "generic"):
+                cpu_adam_flat(p32, hg, st["exp_avg"], st["exp_avg_sq"], g["step"], g["lr"],
+                              tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8), g.get("weight_decay", 0.0),
+                              self.adamw, g.get("bias_correction", True),
+                              bf16_out=out if self.dtype == torch.bfloat16 else None, grad_scale=coef)
+            elif self.kind == "lion":
+                cpu_lion_flat(p32, hg, st["exp_avg"], g["lr"], tuple(g.get("betas", (0.9, 0.99))),
+                              g.get("weight_decay", 0.0), bf16_out=out if self.dtype == torch.bfloat16 else None,
+                              grad_scale=coef)
+            else:
+                cpu_adagrad_flat(p32, hg, st["sum"], g["lr"], g.get("eps", 1e-10), g.get("weight_decay", 0.0),
                                  bf16_out=out if self.dtype == torch.bfloat16 else None, grad_scale=coef)
             if self.dtype != torch.bfloat16:
                 out.copy_(p32)
+            if self.nvme_param:
+                lp_writes[b] = self.param_swapper.swap_out(lo, out)
+                continue
             if self.lp_on_host:
                 continue
             if gpu:
@@ -203,6 +203,11 @@ class OffloadZeroOptimizer(ZeroOptimizer):
                     h2d_ev[b].record(self.h2d_stream)
             else:
                 s.lp[lo:hi].copy_(out)
+        if swap is not None:
+            next(swap, None)  # write back the last chunk; the generator waits for every outstanding transfer
+        for w in lp_writes:
+            if w is not None:
+                w.wait()
         if gpu:
             torch.cuda.current_stream().wait_stream(self.h2d_stream)
         self._post_step_gather()
@@ -222,57 +227,70 @@ class OffloadZeroOptimizer(ZeroOptimizer):
                             g.get("eps", 1e-8), g.get("weight_decay", 0.0), self.adamw, True, lp_out=s.lp[lo:hi],
                             dev_scale=coef)
 
-    # checkpoint hooks: the fp32 master / moments of the offloaded range live in host DRAM (or NVMe)
+    # checkpoint hooks: the fp32 master / moments of the offloaded range live in host DRAM or on NVMe
+    def _host_range(self, key):
+        """Full offloaded range of ``key`` ("fp32" or a moment) as a CPU fp32 tensor (read from NVMe if needed)."""
+        if self.nvme is not None:
+            return self.opt_swapper.read_full(key)
+        return self.h_master if key == "fp32" else self.h_states[key]
+
+    def _set_host_range(self, key, t):
+        if self.nvme is not None:
+            self.opt_swapper.write_full(key, t)
+        elif key == "fp32":
+            self.h_master.copy_(t)
+        else:
+            self.h_states[key].copy_(t)
+
     def _ckpt_flats(self):
         s, n, k0 = self.store, self.store.numel, self.n_off
         out = OrderedDict()
-        m = torch.empty(n, dtype=torch.float32)
-        m[:k0].copy_(self.h_master)
-        if k0 < n:
-            m[k0:].copy_(s.master[k0:])
-        out["fp32"] = m
-        for k in self._STATE_KEYS[self.kind]:
+        for key in ["fp32"] + list(self._STATE_KEYS[self.kind]):
             t = torch.empty(n, dtype=torch.float32)
-            if self.nvme is None:
-                t[:k0].copy_(self.h_states[k])
-            elif k0:
-                self.nvme.sync_pread(t[:k0], self._nvme_file(k))
+            if k0:
+                t[:k0].copy_(self._host_range(key))
             if k0 < n:
-                t[k0:].copy_(s.states[k][k0:])
-            out[k] = t
+                t[k0:].copy_((s.master if key == "fp32" else s.states[key])[k0:])
+            out[key] = t
         return out
 
     def _ckpt_commit(self, flats):
         s, n, k0 = self.store, self.store.numel, self.n_off
-        self.h_master.copy_(flats["fp32"][:k0])
-        if k0 < n:
-            s.master[k0:].copy_(flats["fp32"][k0:])
-        for k, t in flats.items():
-            if k == "fp32":
-                continue
-            if self.nvme is None:
-                self.h_states[k].copy_(t[:k0])
-            elif k0:
-                self.nvme.sync_pwrite(t[:k0].contiguous(), self._nvme_file(k))
+        for key, t in flats.items():
+            if k0:
+                self._set_host_range(key, t[:k0])
             if k0 < n:
-                s.states[k][k0:].copy_(t[k0:])
+                (s.master if key == "fp32" else s.states[key])[k0:].copy_(t[k0:])
+
+    def _lp_host(self):
+        """This rank's compute-dtype shard as a host tensor (the NVMe tier reads the parameter swap file)."""
+        if self.nvme_param:
+            return self.param_swapper.read_sync(0, torch.empty(self.store.numel, dtype=self.dtype))
+        return self.store.lp
 
     def _lp_to_master(self):
         s, n, k0 = self.store, self.store.numel, self.n_off
-        self.h_master.copy_(s.lp[:k0])
+        lp = self._lp_host()
+        if k0:
+            self._set_host_range("fp32", lp[:k0].float().cpu())
         if k0 < n:
-            s.master[k0:].copy_(s.lp[k0:])
+            s.master[k0:].copy_(lp[k0:])
 
     def _master_to_lp(self):
         s, n, k0 = self.store, self.store.numel, self.n_off
-        s.lp[:k0].copy_(self.h_master)
+        m = self._host_range("fp32") if k0 else None
+        if self.nvme_param:
+            self.param_swapper.write_sync(0, m.to(self.dtype))
+            return
+        if k0:
+            s.lp[:k0].copy_(m)
         if k0 < n:
             s.lp[k0:].copy_(s.master[k0:])
 
     def full_fp32_state_dict(self, names):
         s = self.store
         saved = s.master
-        m = self.h_master.to(self.device)
+        m = self._host_range("fp32").to(self.device)
         if self.n_off < s.numel:
             m = torch.cat([m, saved[self.n_off:]])
         s.master = m

@@ -81,6 +81,21 @@ class _EventWork:
         return True
 
 
+class _NvmeFetch:
+    """In-flight NVMe parameter fetch of one unit: swap-file read -> pinned staging -> H2D (+ all-gather)."""
+
+    def __init__(self, zopt, u, full, slot, view, req):
+        self.zopt, self.u, self.full, self.slot, self.view, self.req = zopt, u, full, slot, view, req
+        self.work = None
+
+    def wait(self):
+        if self.work is None:
+            self.req.wait()
+            self.work, ev = self.zopt._h2d_from(self.u, self.full, self.view)
+            self.zopt.param_swapper.release(self.slot, ev)  # staging buffer reusable once the H2D copy lands
+        self.work.wait()
+
+
 class _PreBackward(torch.autograd.Function):
     """Identity on a unit's outputs whose backward fires right before that unit's backward."""
 
@@ -202,6 +217,9 @@ class ZeroOptimizer:
 
         op = self.zcfg.offload_param
         self.offload_param = bool(op.enabled) and self.stage == 3
+        # ZeRO-Infinity: the parameter shard on NVMe, fetched through pinned staging buffers (swap_tensor/)
+        self.nvme_param = self.offload_param and op.device == "nvme"
+        self.param_swapper = None
         if self.offload_param and self.device.type == "cuda":
             self.param_h2d_stream = torch.cuda.Stream(self.device)
         else:
@@ -472,12 +490,27 @@ class ZeroOptimizer:
 
     def _build_store(self):
         dev = self.device
-        self.store = ShardStore(self.units, self.dtype, dev, self.grad_acc_dtype, lp_host=self.offload_param)
+        self.store = ShardStore(self.units, self.dtype, dev, self.grad_acc_dtype,
+                                lp_host="nvme" if self.nvme_param else self.offload_param)
+        if self.nvme_param:
+            if not self.zcfg.offload_optimizer.enabled:
+                raise ValueError("offload_param.device='nvme' needs offload_optimizer (cpu or nvme): the fp32 master "
+                                 "of NVMe-resident parameters lives with the host optimizer")
+            from ..swap_tensor import AsyncPartitionedParameterSwapper
+            from ..swap_tensor.aio_config import make_aio_handle
+            op = self.zcfg.offload_param
+            folder = os.path.join(op.nvme_path or "/tmp/hds_nvme", "zero_stage_3", "params", f"rank{dist.get_rank()}")
+            self.param_aio = make_aio_handle(self.config.aio_config)
+            self.param_swapper = AsyncPartitionedParameterSwapper(
+                self.param_aio, folder, self.store.numel, self.dtype, max(u.shard for u in self.units),
+                op.buffer_count)
+            master_host = torch.empty(self.store.numel, dtype=torch.float32)
         self.direct_grads = all(u.direct for u in self.units)
         from .partition_parameters import is_init_partitioned
         with torch.no_grad():
             for u in self.units:
-                lp = self.store.lp_slice(u)
+                # NVMe parameter tier: the shard is staged in a temporary host buffer on its way to the swap file
+                lp = torch.empty(u.shard, dtype=self.dtype) if self.nvme_param else self.store.lp_slice(u)
                 init_parts = [is_init_partitioned(p) for p in u.params]
                 if any(init_parts):
                     # zero.Init: per-parameter partitions -> this unit's flat shard (one reduce-scatter)
@@ -504,6 +537,12 @@ class ZeroOptimizer:
                     full = torch.empty(u.padded, dtype=self.dtype, device=dev)
                     u.copy_params_into(full)
                     lp.copy_(full[u.rank * u.shard:(u.rank + 1) * u.shard])
+                if self.nvme_param:
+                    # the shard goes to NVMe; only the fp32 copy (for the optimizer) stays on the host
+                    m32 = u.__dict__.pop("_init_master", None)
+                    master_host[u.store_off:u.store_off + u.shard].copy_(m32 if m32 is not None else lp.float())
+                    self.param_swapper.write_sync(u.store_off, lp)
+                    lp = None
                 u.shard_tensor = lp
                 for p in u.params:
                     p.ds_tensor = lp
@@ -526,7 +565,7 @@ class ZeroOptimizer:
                         u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=dev)
                     if u.status == AVAILABLE:
                         u.bind_grads(u.grad_full)
-            self.store.master = self.store.lp.float()
+            self.store.master = master_host if self.nvme_param else self.store.lp.float()
             for u in self.units:  # Init partitions carry the full-precision initial values
                 m32 = u.__dict__.pop("_init_master", None)
                 if m32 is not None:
@@ -717,27 +756,39 @@ class ZeroOptimizer:
         return self.layout_world > 1 or self.offload_param
 
     def _h2d_gather(self, u, full):
-        """ZeRO-Infinity fetch: pinned host shard -> device (side stream), then all-gather when sharded."""
+        """ZeRO-Infinity fetch: pinned host shard -> device (side stream), then all-gather when sharded. With the
+        NVMe tier the shard is first read from the swap file into a pinned staging buffer (async; the read of a
+        prefetched unit overlaps the compute of the units before it)."""
+        if self.nvme_param:
+            slot, view, req = self.param_swapper.swap_in(u.store_off, u.shard)
+            return _NvmeFetch(self, u, full, slot, view, req)
+        work, _ = self._h2d_from(u, full, u.shard_tensor)
+        return work
+
+    def _h2d_from(self, u, full, src):
+        """Copy host shard ``src`` into the device and all-gather into ``full``; returns (work, H2D-done event)."""
         s = self.param_h2d_stream
         if s is None:  # CPU runs: synchronous copies, same semantics
             if u.world == 1:
-                full.copy_(u.shard_tensor)
-                return _DoneWork()
-            tmp = u.shard_tensor.to(self.device)
-            return dist.all_gather_into_tensor(full, tmp, group=u.ag_group, async_op=True)
+                full.copy_(src)
+                return _DoneWork(), None
+            tmp = src.to(self.device)
+            return dist.all_gather_into_tensor(full, tmp, group=u.ag_group, async_op=True), None
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             if u.world == 1:
-                full.copy_(u.shard_tensor, non_blocking=True)
+                full.copy_(src, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(s)
                 work = _EventWork(ev)
             else:
                 tmp = torch.empty(u.shard, dtype=self.dtype, device=self.device)
-                tmp.copy_(u.shard_tensor, non_blocking=True)
+                tmp.copy_(src, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s)
                 work = dist.all_gather_into_tensor(full, tmp, group=u.ag_group, async_op=True)
         full.record_stream(s)
-        return work
+        return work, ev
 
     # ------------------------------------------------------------------------------------
     # collectives: torch.distributed (RCCL via c10d) or the native C++ RCCL executor
@@ -1177,7 +1228,9 @@ class ZeroOptimizer:
         works = []
         for u in self.units:
             if self.offload_param and u.persistent and u.full is not None:
-                if u.world == 1:
+                if self.nvme_param:
+                    works.append(self._h2d_gather(u, u.full))
+                elif u.world == 1:
                     u.full.copy_(u.shard_tensor)
                 else:
                     works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor.to(self.device), group=u.ag_group,
@@ -1318,7 +1371,11 @@ class ZeroOptimizer:
         with torch.no_grad():
             for u in self.units:
                 if u.full is not None and self._partitioned(u) and u.status == AVAILABLE:
-                    self.store.lp_slice(u).copy_(u.full[u.rank * u.shard:(u.rank + 1) * u.shard])
+                    shard = u.full[u.rank * u.shard:(u.rank + 1) * u.shard]
+                    if self.nvme_param:
+                        self.param_swapper.write_sync(u.store_off, shard)
+                    else:
+                        self.store.lp_slice(u).copy_(shard)
             self._lp_to_master()
 
     def _lp_to_master(self):
