@@ -146,6 +146,7 @@ class _FusedLinearCEFn(torch.autograd.Function):
             del logits
         ctx.save_for_backward(dh, dw)
         ctx.wdtype = weight.dtype
+        ctx.weight = weight  # the Parameter object: its gradient may be written in place (ZeRO)
         ctx.mark_non_differentiable(losses)
         return losses.sum(), losses
 
@@ -155,7 +156,16 @@ class _FusedLinearCEFn(torch.autograd.Function):
         # the eagerly computed d(hidden) and d(W)
         dh, dw = ctx.saved_tensors
         gh = (dh * dsum.to(dh.dtype)) if dh is not None else None
-        gw = (dw * dsum.float()).to(ctx.wdtype) if dw is not None else None
+        gw = None
+        if dw is not None:
+            dw.mul_(dsum.float())
+            from ..runtime.zero.linear import write_weight_grad
+
+            def put(out, accumulate):  # fp32 accumulator -> the bf16 gradient buffer (one pass)
+                out.add_(dw) if accumulate else out.copy_(dw)
+
+            if not write_weight_grad(ctx.weight, put):
+                gw = dw.to(ctx.wdtype)
         return gh, gw, None, None, None, None
 
 

@@ -177,6 +177,7 @@ class MI355XConfig:
     zero3_prefetch_depth: int = 2
     zero3_max_reduce_inflight: int = 2
     zero3_unit_bucket_mb: float = 128  # per-submodule ZeRO-3 units of ModuleList-free models are bucketed to this
+    direct_wgrad: bool = True  # weight-gradient GEMMs write into the flat gradient buffer (runtime/zero/linear.py)
     fused_lm_head_ce: bool = True
     host_act_cache: HostActCacheConfig = field(default_factory=HostActCacheConfig)
 
@@ -296,6 +297,7 @@ class DeepSpeedConfig:
             xgmi_bucket_mb=int(m.get("xgmi_bucket_mb", 256)), zero3_prefetch_depth=int(m.get("zero3_prefetch_depth", 2)),
             zero3_max_reduce_inflight=int(m.get("zero3_max_reduce_inflight", 2)),
             zero3_unit_bucket_mb=float(m.get("zero3_unit_bucket_mb", 128)),
+            direct_wgrad=bool(m.get("direct_wgrad", True)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
             host_act_cache=HostActCacheConfig(**{f.name: hac[f.name]
                                                  for f in fields(HostActCacheConfig) if f.name in hac}))

@@ -1,4 +1,14 @@
-"""Memory-efficient linear for ZeRO-3 (reference runtime/zero/linear.py ``LinearFunctionForZeroStage3`` :50).
+"""ZeRO linear Functions (reference runtime/zero/linear.py ``LinearFunctionForZeroStage3`` :50).
+
+Two jobs:
+
+* memory efficiency (ZeRO-3): save the input and the Parameter OBJECT, not the weight tensor (below);
+* in-place weight gradients (every stage, ``mi355x.direct_wgrad``): the weight gradient GEMM writes straight
+  into the parameter's slice of the flat ZeRO gradient buffer -- ``mm(out=grad)`` on the first micro-step of
+  a window, ``addmm_(beta=1)`` after -- so neither the per-step zero fill of the gradient buffer nor autograd's
+  AccumulateGrad add (``grad += dW``: a full read-modify-write of every weight gradient) runs. Readiness
+  bookkeeping stays with the parameter's post-accumulate hook, which autograd still fires (with no gradient).
+
 
 A plain ``F.linear`` saves the weight TENSOR for backward, which pins the gathered full buffer of the whole
 unit until the backward pass -- a partitioned model would keep every layer's gathered weights alive. This
@@ -11,6 +21,19 @@ import types
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+
+def write_weight_grad(w, compute):
+    """If ZeRO owns ``w``'s gradient buffer and allows in-place writes, call ``compute(out, accumulate)`` to
+    produce the weight gradient straight into it and return True; otherwise return False."""
+    z = getattr(w, "_hds_zero", None)
+    tgt = z.wgrad_target(w) if z is not None else None
+    if tgt is None:
+        return False
+    g, fresh = tgt
+    compute(g, not fresh)
+    z.wgrad_written(w)
+    return True
 
 
 class LinearFunctionForZeroStage3(torch.autograd.Function):
@@ -30,7 +53,17 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = dy.matmul(w.to(dy.dtype))
         if ctx.needs_input_grad[1]:
-            dw = dy.reshape(-1, dy.shape[-1]).t().matmul(x.reshape(-1, x.shape[-1]).to(dy.dtype))
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            x2 = x.reshape(-1, x.shape[-1]).to(dy.dtype)
+
+            def gemm(out, accumulate):
+                if accumulate:
+                    out.addmm_(dy2.t(), x2)
+                else:
+                    torch.mm(dy2.t(), x2, out=out)
+
+            if not write_weight_grad(w, gemm):
+                dw = dy2.t().matmul(x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0)
         return dx, dw, db
@@ -44,11 +77,13 @@ def _mel_forward(self, x):
     return zero3_linear(x, self.weight, self.bias)
 
 
-def wrap_memory_efficient_linears(module):
-    """Route every nn.Linear under ``module`` through the memory-efficient Function (instance-level)."""
+def wrap_memory_efficient_linears(module, only=None):
+    """Route every nn.Linear under ``module`` (or those whose weight id is in ``only``) through the Function
+    (instance-level forward override)."""
     n = 0
     for m in module.modules():
-        if isinstance(m, nn.Linear) and not getattr(m, "_hds_mel", False):
+        if isinstance(m, nn.Linear) and not getattr(m, "_hds_mel", False) and \
+                (only is None or id(m.weight) in only):
             m.forward = types.MethodType(_mel_forward, m)
             m._hds_mel = True
             n += 1

@@ -233,6 +233,7 @@ class ZeroOptimizer:
             for u in self.units:
                 if not u.persistent and u.module is not None:
                     wrap_memory_efficient_linears(u.module)
+        self._setup_direct_wgrad()
         self.micro_in_window = 0
         self.boundary = True
         self.in_backward = False
@@ -679,7 +680,7 @@ class ZeroOptimizer:
     def _make_grad_hook(self, u):
 
         def hook(p):
-            u.pending -= 1
+            u.pending -= 1  # fires once per backward, also for weights written in place (their AccumulateGrad gets None)
             if u.pending == 0 and not u.grads_reduced:
                 self._unit_grads_ready(u)
 
@@ -850,7 +851,8 @@ class ZeroOptimizer:
             u.status = AVAILABLE
         if wait and self.in_backward and u.grad_full is None and u.requires_grad_count:
             # the unsharded gradient is allocated on demand, not for prefetched units
-            u.grad_full = torch.zeros(u.padded, dtype=self.dtype, device=self.device)
+            u.grad_full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
+            self._reset_grad_buffer(u)
             u.bind_grads(u.grad_full)
             self._note_live()
         elif self.in_backward and u.direct and self.offload_param and u.requires_grad_count:
@@ -957,6 +959,7 @@ class ZeroOptimizer:
     # ------------------------------------------------------------------------------------
     def _unit_grads_ready(self, u):
         u.grads_reduced = True
+        self._zero_unwritten_wgrads(u)
         if self.hold_reduction and self.boundary:
             if not self._held:
                 self._held_micro = self.micro_in_window
@@ -974,7 +977,7 @@ class ZeroOptimizer:
         if self.stage in (2, 3):
             for u in held:
                 if u.grad_full is not None and not u.direct:
-                    u.grad_full.zero_()
+                    self._reset_grad_buffer(u)
 
     @staticmethod
     def _retire(queue, limit):
@@ -1093,13 +1096,14 @@ class ZeroOptimizer:
             held = {id(h) for h in self._held}
             for u in self.units:
                 if u.grad_full is not None and not u.direct and id(u) not in held:
-                    u.grad_full.zero_()
+                    self._reset_grad_buffer(u)
         if self.stage == 3:
             for u in self.units:
                 if not u.persistent:
                     self._release(u)
         self.in_backward = False
         self.micro_in_window += 1
+
         if self._recording and self._fwd_trace:
             self._recording = False
             self._trace_ok = True
@@ -1134,11 +1138,109 @@ class ZeroOptimizer:
         return self.loss_scaler.loss_scale
 
     def zero_grad(self, set_to_none=True):
-        self.store.grad.zero_()
+        if self._store_zero_idx is not None:
+            # in-place weight gradients overwrite their ranges: zero only the rest, mark the weights fresh
+            self.store.grad.index_fill_(0, self._store_zero_idx, 0)
+            for u in self.units:
+                if u.direct:
+                    self._mark_fresh(u)
+        else:
+            self.store.grad.zero_()
         for u in self.units:
             if u.grad_full is not None and not u.direct:
-                u.grad_full.zero_()
+                self._reset_grad_buffer(u)
         self.micro_in_window = 0
+
+    # ------------------------------------------------------------------------------------
+    # in-place weight gradients (runtime/zero/linear.py write_weight_grad)
+    # ------------------------------------------------------------------------------------
+    def _setup_direct_wgrad(self):
+        """Weights of nn.Linear modules whose gradient buffer is in the compute dtype get their weight-gradient
+        GEMM written in place; the remaining positions of each unit buffer are zeroed by one index_fill."""
+        self._wgrad_ok = set()
+        self._store_zero_idx = None
+        if not getattr(self.mi, "direct_wgrad", True) or self.grad_acc_dtype != self.dtype:
+            return
+        from .linear import wrap_memory_efficient_linears
+        cand = {id(m.weight) for m in self.module.modules()
+                if isinstance(m, nn.Linear) and id(m.weight) in self.param_to_unit and m.weight.requires_grad}
+        # the fused LM-head cross entropy writes its weight gradient the same way (ops/cross_entropy.py)
+        for m in self.module.modules():
+            w = getattr(getattr(m, "lm_head", None), "weight", None)
+            if w is not None and id(w) in self.param_to_unit and w.requires_grad:
+                cand.add(id(w))
+        if not cand:
+            return
+        self._wgrad_ok = cand
+        wrap_memory_efficient_linears(self.module, only=cand)
+        # A candidate may ALSO receive gradient through plain autograd (used outside its module's forward, tied
+        # weights). That contribution reaches AccumulateGrad after the in-place GEMM (the engine sums every
+        # contribution first), so it simply adds on top; if the in-place GEMM did not run this window the buffer
+        # still holds last window's values, which this tensor hook (it runs before AccumulateGrad) clears.
+        for u in self.units:
+            for p in u.params:
+                if id(p) in cand:
+                    self._hook_handles.append(p.register_hook(self._make_stale_guard(p)))
+        dev = self.device
+        store_idx = []
+        for u in self.units:
+            keep = torch.ones(u.padded, dtype=torch.bool)
+            for i, p in enumerate(u.params):
+                if id(p) in cand:
+                    keep[u.offsets[i]:u.offsets[i] + u.numels[i]] = False
+            u.zero_idx = keep.nonzero().flatten().to(dev)
+            u.wgrad_params = [p for p in u.params if id(p) in cand] or None
+            if u.direct:
+                store_idx.append(u.zero_idx + u.store_off)
+        if store_idx:
+            self._store_zero_idx = torch.cat(store_idx + [
+                torch.arange(u.store_off, u.store_off + u.shard, device=dev) for u in self.units if not u.direct])
+        for u in self.units:
+            if u.direct:
+                self._mark_fresh(u)
+
+    @staticmethod
+    def _make_stale_guard(p):
+
+        def guard(grad):
+            if getattr(p, "_hds_gfresh", False) and p.grad is not None:
+                p.grad.zero_()
+                p._hds_gfresh = False
+            return grad
+
+        return guard
+
+    def _mark_fresh(self, u):
+        for p in getattr(u, "wgrad_params", None) or ():
+            p._hds_gfresh = True
+
+    def _reset_grad_buffer(self, u, buf=None):
+        """Make ``u``'s (non-direct) gradient buffer ready for a new accumulation window."""
+        buf = u.grad_full if buf is None else buf
+        if getattr(u, "wgrad_params", None):
+            buf.index_fill_(0, u.zero_idx, 0)
+            self._mark_fresh(u)
+        else:
+            buf.zero_()
+
+    def wgrad_target(self, p):
+        """(gradient view, fresh) when ``p``'s weight gradient may be written in place, else None."""
+        if id(p) not in self._wgrad_ok:
+            return None
+        g = p.grad
+        if g is None or g.dtype != p.dtype or not g.is_contiguous():
+            return None
+        return g, getattr(p, "_hds_gfresh", False)
+
+    def wgrad_written(self, p):
+        # readiness is signalled by the parameter's post-accumulate hook, which still fires (with no gradient)
+        p._hds_gfresh = False
+
+    def _zero_unwritten_wgrads(self, u):
+        """Weights that got no gradient this window still hold last window's values: zero them."""
+        for p in getattr(u, "wgrad_params", None) or ():
+            if getattr(p, "_hds_gfresh", False) and p.grad is not None:
+                p.grad.zero_()
 
     def _seg_group(self, seg):
         return self.param_groups[seg.group]

@@ -229,3 +229,63 @@ def test_zero_world3_4(world, stage, zinit):
     """More ranks than the default harness (uneven shard padding at world 3, 4-way reduce-scatter / all-gather):
     the flat-shard collectives used at 8 GPUs, rehearsed on gloo."""
     run_distributed(_zero_vs_torch, world, stage, 1, zinit)
+
+
+class _WgradToy(torch.nn.Module):
+    """Linears used normally, one also used through F.linear outside its forward, one skipped on odd steps."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 32)
+        self.b = torch.nn.Linear(32, 32, bias=False)
+        self.skip = torch.nn.Linear(32, 32)
+        self.out = torch.nn.Linear(32, 4)
+        self.odd = False
+
+    def forward(self, x, y):
+        h = torch.tanh(self.a(x))
+        h = torch.tanh(self.b(h)) + 0.5 * torch.nn.functional.linear(h, self.b.weight)  # shared use
+        if not self.odd:
+            h = h + self.skip(h)
+        return torch.nn.functional.mse_loss(self.out(h), y)
+
+
+def _direct_wgrad_equiv(rank, world, stage, gas):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.runtime.zero import linear as zl
+    finals, writes = [], []
+    for direct in (True, False):
+        torch.manual_seed(0)
+        m = _WgradToy()
+        cfg = {"train_micro_batch_size_per_gpu": 4, "gradient_accumulation_steps": gas,
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}},
+               "zero_optimization": {"stage": stage}, "mi355x": {"direct_wgrad": direct}}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        n = [0]
+        orig = zl.write_weight_grad
+
+        def counting(w, compute):
+            ok = orig(w, compute)
+            n[0] += ok
+            return ok
+
+        zl.write_weight_grad = counting
+        try:
+            g = torch.Generator().manual_seed(7 + rank)
+            for it in range(4 * gas):
+                m.odd = bool((it // gas) % 2)
+                x, y = torch.randn(4, 16, generator=g), torch.randn(4, 4, generator=g)
+                eng.backward(eng(x, y))
+                eng.step()
+        finally:
+            zl.write_weight_grad = orig
+        finals.append(eng.optimizer.full_fp32_state_dict(eng._param_names))
+        writes.append(n[0])
+    assert writes[0] > 0 and writes[1] == 0, writes
+    for k in finals[0]:
+        assert torch.allclose(finals[0][k], finals[1][k], atol=1e-6, rtol=1e-5), (stage, k)
+
+
+@pytest.mark.parametrize("stage,gas", [(1, 2), (2, 1), (2, 2), (3, 1), (3, 2)])
+def test_direct_wgrad_matches_autograd_world2(stage, gas):
+    run_distributed(_direct_wgrad_equiv, 2, stage, gas)
