@@ -118,6 +118,37 @@ __global__ __launch_bounds__(256) void nhwc_bias_add_kernel(const T* __restrict_
   }
 }
 
+// Embedding weight gradient, accumulated in place: grad[id, :] += sum of dy[t, :] over tokens t with ids[t] == id.
+// ``sorted``/``perm`` come from a stable sort of the ids, so every id's tokens are one contiguous run and the
+// first position of each run owns the row: one read-modify-write per touched row, fp32 sums in a fixed
+// (token) order -- deterministic, no atomics, and no dense [V, D] temporary (the sort-based framework path
+// materialises and then adds one). One workgroup per sorted position; non-leading positions exit at once.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const T* __restrict__ dy, const int64_t* __restrict__ sorted,
+                                                        const int64_t* __restrict__ perm, T* __restrict__ grad,
+                                                        int64_t n, int D, int64_t V, int64_t pad_idx) {
+  const int64_t i = blockIdx.x;
+  const int64_t id = sorted[i];
+  if ((i > 0 && sorted[i - 1] == id) || id == pad_idx || id < 0 || id >= V) return;
+  int64_t end = i + 1;
+  while (end < n && sorted[end] == id) ++end;
+  T* g = grad + id * (int64_t)D;
+  for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int64_t j = i; j < end; ++j) {
+      float v[8];
+      Vec8<T>::load(dy + perm[j] * (int64_t)D + c, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+    float old[8];
+    Vec8<T>::load(g + c, old);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) old[e] += acc[e];
+    Vec8<T>::store(g + c, old);
+  }
+}
+
 #define HDS_TOK_DISPATCH(dtype, ...)                  \
   switch (dtype) {                                    \
     case kF32: { typedef float T; __VA_ARGS__; break; }    \
@@ -170,5 +201,14 @@ HDS_EXPORT int hds_nhwc_bias_add(int dtype, const void* a, const void* bias, con
   HDS_TOK_DISPATCH(dtype, hipLaunchKernelGGL(nhwc_bias_add_kernel<T>, dim3(grid), dim3(256), 0, st, (const T*)a,
                                              (const T*)bias, (const T*)other, (const T*)other_bias, (T*)out, n_vec,
                                              C, mode));
+  return (int)hipGetLastError();
+}
+
+HDS_EXPORT int hds_embed_bwd(int dtype, const void* dy, const int64_t* sorted, const int64_t* perm, void* grad,
+                             int64_t n, int D, int64_t V, int64_t pad_idx, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (D % 8 || n > 0x7fffffff) return (int)hipErrorInvalidValue;
+  HDS_TOK_DISPATCH(dtype, hipLaunchKernelGGL(embed_bwd_kernel<T>, dim3((unsigned)n), dim3(256), 0, st, (const T*)dy,
+                                             sorted, perm, (T*)grad, n, D, V, pad_idx));
   return (int)hipGetLastError();
 }

@@ -63,6 +63,7 @@ _KERNEL_SIGS = {
     "hds_token_gather": "i" + "ppp" + "iiii" + "s",
     "hds_token_scatter": "i" + "ppp" + "iiii" + "s",
     "hds_token_sort": "p" + "ii" + "s",
+    "hds_embed_bwd": "i" + "pppp" + "l" + "i" + "ll" + "s",
     "hds_slice_mask": "i" + "ppp" + "iiiii" + "s",
     "hds_grouped_gemm_max_tiles": "ii",
     "hds_grouped_gemm": "ppppp" + "iiiiii" + "s",

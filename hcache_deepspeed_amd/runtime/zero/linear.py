@@ -36,6 +36,20 @@ def write_weight_grad(w, compute):
     return True
 
 
+def grad_accumulator(w, dtype):
+    """The ZeRO-owned gradient buffer of ``w`` to ADD a gradient contribution into directly (returning None to
+    autograd instead of a dense tensor), or None. A buffer still marked fresh (an in-place GEMM target that has
+    not been written this window) holds last window's values and is cleared first."""
+    z = getattr(w, "_hds_zero", None)
+    g = w.grad if z is not None else None
+    if g is None or g.dtype != dtype or not g.is_contiguous() or not z.accumulate_ok(w):
+        return None
+    if getattr(w, "_hds_gfresh", False):
+        g.zero_()
+        w._hds_gfresh = False
+    return g
+
+
 class LinearFunctionForZeroStage3(torch.autograd.Function):
 
     @staticmethod

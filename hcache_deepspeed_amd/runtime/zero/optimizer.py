@@ -64,6 +64,29 @@ def _optimizer_kind(opt):
     return "generic", False
 
 
+
+class _ZeroPlan:
+    """Zero a set of [lo, hi) ranges of a flat buffer: long ranges as slice fills, the short ones (norm weights,
+    biases) with ONE index_fill -- an index tensor over every position would cost 8 bytes per element."""
+    SLICE_MIN = 1 << 16
+
+    def __init__(self, ranges, device):
+        merged = []
+        for lo, hi in sorted(r for r in ranges if r[1] > r[0]):
+            if merged and lo <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], hi)
+            else:
+                merged.append([lo, hi])
+        self.slices = [(lo, hi) for lo, hi in merged if hi - lo >= self.SLICE_MIN]
+        small = [torch.arange(lo, hi) for lo, hi in merged if hi - lo < self.SLICE_MIN]
+        self.idx = torch.cat(small).to(device) if small else None
+
+    def apply(self, buf):
+        for lo, hi in self.slices:
+            buf[lo:hi].zero_()
+        if self.idx is not None:
+            buf.index_fill_(0, self.idx, 0)
+
 class _DoneWork:
 
     def wait(self):
@@ -1138,9 +1161,9 @@ class ZeroOptimizer:
         return self.loss_scaler.loss_scale
 
     def zero_grad(self, set_to_none=True):
-        if self._store_zero_idx is not None:
+        if self._store_zero_plan is not None:
             # in-place weight gradients overwrite their ranges: zero only the rest, mark the weights fresh
-            self.store.grad.index_fill_(0, self._store_zero_idx, 0)
+            self._store_zero_plan.apply(self.store.grad)
             for u in self.units:
                 if u.direct:
                     self._mark_fresh(u)
@@ -1158,7 +1181,8 @@ class ZeroOptimizer:
         """Weights of nn.Linear modules whose gradient buffer is in the compute dtype get their weight-gradient
         GEMM written in place; the remaining positions of each unit buffer are zeroed by one index_fill."""
         self._wgrad_ok = set()
-        self._store_zero_idx = None
+        self._accum_ok = set()
+        self._store_zero_plan = None
         if not getattr(self.mi, "direct_wgrad", True) or self.grad_acc_dtype != self.dtype:
             return
         from .linear import wrap_memory_efficient_linears
@@ -1169,6 +1193,12 @@ class ZeroOptimizer:
             w = getattr(getattr(m, "lm_head", None), "weight", None)
             if w is not None and id(w) in self.param_to_unit and w.requires_grad:
                 cand.add(id(w))
+        # token embeddings scatter-add their weight gradient into the buffer (ops/embedding.py)
+        self._accum_ok = {id(m.weight) for m in self.module.modules()
+                          if isinstance(m, nn.Embedding) and id(m.weight) in self.param_to_unit and m.weight.requires_grad}
+        if self._accum_ok:
+            from ...ops.embedding import wrap_embeddings
+            wrap_embeddings(self.module, only=self._accum_ok)
         if not cand:
             return
         self._wgrad_ok = cand
@@ -1182,19 +1212,24 @@ class ZeroOptimizer:
                 if id(p) in cand:
                     self._hook_handles.append(p.register_hook(self._make_stale_guard(p)))
         dev = self.device
-        store_idx = []
+        store_ranges = []
         for u in self.units:
-            keep = torch.ones(u.padded, dtype=torch.bool)
-            for i, p in enumerate(u.params):
-                if id(p) in cand:
-                    keep[u.offsets[i]:u.offsets[i] + u.numels[i]] = False
-            u.zero_idx = keep.nonzero().flatten().to(dev)
+            covered = sorted((u.offsets[i], u.offsets[i] + u.numels[i]) for i, p in enumerate(u.params) if id(p) in cand)
+            gaps, pos = [], 0
+            for lo, hi in covered:
+                if lo > pos:
+                    gaps.append((pos, lo))
+                pos = max(pos, hi)
+            if pos < u.padded:
+                gaps.append((pos, u.padded))
+            u.zero_plan = _ZeroPlan(gaps, dev)
             u.wgrad_params = [p for p in u.params if id(p) in cand] or None
             if u.direct:
-                store_idx.append(u.zero_idx + u.store_off)
-        if store_idx:
-            self._store_zero_idx = torch.cat(store_idx + [
-                torch.arange(u.store_off, u.store_off + u.shard, device=dev) for u in self.units if not u.direct])
+                store_ranges += [(lo + u.store_off, hi + u.store_off) for lo, hi in gaps]
+            else:
+                store_ranges.append((u.store_off, u.store_off + u.shard))
+        if any(u.direct for u in self.units):
+            self._store_zero_plan = _ZeroPlan(store_ranges, dev)
         for u in self.units:
             if u.direct:
                 self._mark_fresh(u)
@@ -1218,7 +1253,7 @@ class ZeroOptimizer:
         """Make ``u``'s (non-direct) gradient buffer ready for a new accumulation window."""
         buf = u.grad_full if buf is None else buf
         if getattr(u, "wgrad_params", None):
-            buf.index_fill_(0, u.zero_idx, 0)
+            u.zero_plan.apply(buf)
             self._mark_fresh(u)
         else:
             buf.zero_()
@@ -1231,6 +1266,9 @@ class ZeroOptimizer:
         if g is None or g.dtype != p.dtype or not g.is_contiguous():
             return None
         return g, getattr(p, "_hds_gfresh", False)
+
+    def accumulate_ok(self, p):
+        return id(p) in self._accum_ok or id(p) in self._wgrad_ok
 
     def wgrad_written(self, p):
         # readiness is signalled by the parameter's post-accumulate hook, which still fires (with no gradient)

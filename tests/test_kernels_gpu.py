@@ -486,3 +486,29 @@ def test_dequant_reduce(bits):
     acc = torch.ones(n, device="cuda")
     Q.dequant_reduce(q, s, W, n, 512, bits, out=acc, accumulate=True)
     assert torch.allclose(acc.cpu(), ref + 1, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("pad", [None, 3])
+def test_embedding_grad_scatter_add_gpu(dtype, pad):
+    from hcache_deepspeed_amd.ops.embedding import embedding_grad_add_
+    torch.manual_seed(0)
+    V, D, N = 1000, 4096 + 8 * 3, 5000
+    ids = torch.randint(0, V, (N, ), device="cuda")
+    ids[:600] = 7  # a long run of one id
+    ids[600:700] = 3
+    dy = torch.randn(N, D, device="cuda", dtype=dtype)
+    grad = torch.randn(V, D, device="cuda", dtype=dtype)
+    ref = grad.float().clone()
+    keep = ids != (pad if pad is not None else -1)
+    ref.index_add_(0, ids[keep], dy[keep].float())
+    out = embedding_grad_add_(grad, ids, dy, pad)
+    assert out.data_ptr() == grad.data_ptr()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(grad.float(), ref, atol=tol * 8, rtol=tol)
+    again = torch.randn(V, D, device="cuda", dtype=dtype)
+    a2 = again.clone()
+    embedding_grad_add_(again, ids, dy, pad)
+    embedding_grad_add_(a2, ids, dy, pad)
+    assert torch.equal(again, a2)  # deterministic
