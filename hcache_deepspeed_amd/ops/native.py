@@ -63,6 +63,11 @@ _KERNEL_SIGS = {
     "hds_token_gather": "i" + "ppp" + "iiii" + "s",
     "hds_token_scatter": "i" + "ppp" + "iiii" + "s",
     "hds_token_sort": "p" + "ii" + "s",
+    "hds_gemm_nt_supported": "iiiiii",
+    "hds_gemm_nt": "ppp" + "iiiiii" + "f" + "ii" + "s",
+    "hds_gemm_mxfp8_supported": "iiiiii",
+    "hds_gemm_mxfp8": "ppppp" + "iiiiii" + "f" + "i" + "s",
+    "hds_mx_quant": "ppp" + "l" + "i" + "l" + "s",
     "hds_embed_bwd": "i" + "pppp" + "l" + "i" + "ll" + "s",
     "hds_slice_mask": "i" + "ppp" + "iiiii" + "s",
     "hds_grouped_gemm_max_tiles": "ii",

@@ -512,3 +512,61 @@ def test_embedding_grad_scatter_add_gpu(dtype, pad):
     embedding_grad_add_(again, ids, dy, pad)
     embedding_grad_add_(a2, ids, dy, pad)
     assert torch.equal(again, a2)  # deterministic
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1280, 512, 1024), (2304, 2560, 256)])
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gemm_nt_matches_fp32_gpu(M, N, K, accumulate, variant):
+    from hcache_deepspeed_amd.ops import native
+    from hcache_deepspeed_amd.ops.gemm import gemm_nt
+    assert native.kernels().hds_gemm_nt_supported(M, N, K, K, K, N)
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    # asymmetric structure: a row/column pattern that a transposed or mis-indexed store cannot reproduce
+    a[:, 0] = torch.arange(M, device="cuda", dtype=torch.float32).to(torch.bfloat16) / M
+    b[:, 1] = torch.arange(N, device="cuda", dtype=torch.float32).to(torch.bfloat16) / N
+    c0 = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    out = c0.clone()
+    gemm_nt(a, b, out=out, alpha=0.5, accumulate=accumulate, variant=variant)
+    ref = 0.5 * (a.float() @ b.float().t()) + (c0.float() if accumulate else 0)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.gpu
+def test_mx_quantize_matches_reference_gpu():
+    from hcache_deepspeed_amd.ops.fp8_gemm import mx_quantize, mx_quantize_ref
+    torch.manual_seed(0)
+    x = (torch.randn(512, 1024, device="cuda") * torch.logspace(-3, 3, 1024, device="cuda")).to(torch.bfloat16)
+    x[3, :32] = 0  # all-zero block
+    q, s = mx_quantize(x)
+    qr, sr = mx_quantize_ref(x.cpu())
+    assert torch.equal(s.cpu(), sr)
+    mism = (q.cpu() != qr).float().mean().item()
+    assert mism < 1e-3, mism  # rounding ties may differ in the last bit only
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 512), (1280, 512, 2048)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_mx_gemm_matches_dequant_reference_gpu(M, N, K, variant):
+    from hcache_deepspeed_amd.ops.fp8_gemm import mx_dequantize, mx_gemm, mx_quantize
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    a[:, :128] *= 50  # blocks with very different scales along K
+    b[:, 256:] *= 1e-2 if K > 256 else 1
+    a[:, 0] = torch.arange(M, device="cuda", dtype=torch.float32).to(torch.bfloat16) / M
+    qa, sa = mx_quantize(a)
+    qb, sb = mx_quantize(b)
+    out = mx_gemm(qa, sa, qb, sb, alpha=0.5, variant=variant)
+    ref = 0.5 * (mx_dequantize(qa, sa) @ mx_dequantize(qb, sb).t())
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
+    # and the quantized product tracks the bf16 one
+    full = 0.5 * (a.float() @ b.float().t())
+    rel = ((out.float() - full).norm() / full.norm()).item()
+    assert rel < 0.08, rel
