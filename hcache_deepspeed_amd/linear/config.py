@@ -23,3 +23,7 @@ class QuantizationConfig:
     mantissa_bits: int = 3
     group_size: int = 512
     q_dtype: torch.dtype = torch.uint8
+    # MI355X: 8-bit e4m3 weights of 2-D linears also keep an MX-FP8 copy (e8m0 scale per 32 elements) and run
+    # prefill/training-sized inputs on the block-scaled FP8 matrix cores, with the activations MX-quantized on
+    # the fly (ops/fp8_gemm.py). False keeps the reference's weight-only path (dequantize + bf16 GEMM).
+    mx_fp8: bool = True

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from .. import comm as dist
 from .config import LoRAConfig, QuantizationConfig
-from .quantization import QuantizedLinear, QuantizedParameter
+from .quantization import QuantizedLinear, QuantizedParameter, _mx_eligible, mx_linear
 
 
 class OptimizedLinear(nn.Module):
@@ -52,6 +52,8 @@ class LoRAOptimizedLinear(nn.Module):
         shard = flat[rank * self.sharded_weight_size:(rank + 1) * self.sharded_weight_size].clone()
         if quantization_config is not None:
             self.weight = QuantizedParameter(shard, quantization_config=quantization_config, dtype=dtype)
+            if self.zero_shards == 1 and _mx_eligible(self.weight.quantization_config, output_dim, input_dim):
+                self.weight.enable_mx((output_dim, input_dim), w)
         else:
             self.weight = nn.Parameter(shard, requires_grad=False)
         self.weight.ds_optim_param = False
@@ -99,7 +101,10 @@ class LoRAOptimizedLinear(nn.Module):
         self.fused = False
 
     def forward(self, x):
-        base = F.linear(x, self.full_weight().to(x.dtype))
+        if isinstance(self.weight, QuantizedParameter) and self.weight.mx_ok() and not self.fused:
+            base = mx_linear(x, self.weight)
+        else:
+            base = F.linear(x, self.full_weight().to(x.dtype))
         if self.fused:
             return base
         return base + self.lora_scaling_factor * self.lora_weight_2(self.lora_weight_1(x))

@@ -50,6 +50,18 @@ def grad_accumulator(w, dtype):
     return g
 
 
+_FWD_GEMM = __import__("os").environ.get("HDS_GEMM_FWD", "0") == "1"  # experiment: hand-written MFMA fwd GEMM
+
+
+def _linear_fwd(x, weight, bias):
+    if _FWD_GEMM and bias is None and x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16:
+        from ...ops.gemm import gemm_nt, gemm_nt_supported
+        x2 = x.reshape(-1, x.shape[-1])
+        if gemm_nt_supported(x2.shape[0], weight.shape[0], x2.shape[1]) and x2.is_contiguous():
+            return gemm_nt(x2, weight).view(*x.shape[:-1], weight.shape[0])
+    return F.linear(x, weight, bias)
+
+
 class LinearFunctionForZeroStage3(torch.autograd.Function):
 
     @staticmethod
@@ -57,7 +69,7 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.weight = weight
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        return _linear_fwd(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):

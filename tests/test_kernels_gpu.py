@@ -570,3 +570,32 @@ def test_mx_gemm_matches_dequant_reference_gpu(M, N, K, variant):
     full = 0.5 * (a.float() @ b.float().t())
     rel = ((out.float() - full).norm() / full.norm()).item()
     assert rel < 0.08, rel
+
+
+@pytest.mark.gpu
+def test_quantized_lora_linear_mx_fp8_gpu():
+    """LoRA over an MX-FP8 frozen base: forward and input gradient on the FP8 matrix cores match the
+    dequantized-weight computation."""
+    from hcache_deepspeed_amd.linear import LoRAConfig, OptimizedLinear, QuantizationConfig
+    from hcache_deepspeed_amd.ops.fp8_gemm import mx_dequantize, mx_quantize
+    torch.manual_seed(0)
+    lin = OptimizedLinear(1024, 512, lora_config=LoRAConfig(lora_r=8, lora_alpha=16),
+                          quantization_config=QuantizationConfig(q_bits=8, group_size=256), dtype=torch.bfloat16,
+                          device="cuda")
+    lin.weight.to("cuda")
+    assert lin.weight.mx_ok()
+    x = torch.randn(2, 256, 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    y = lin(x)
+    w = mx_dequantize(*lin.weight.mx_w)
+    xq = mx_dequantize(*mx_quantize(x.detach().reshape(-1, 1024)))
+    ref = (xq @ w.t()).reshape(2, 256, 512)
+    base = y - lin.lora_scaling_factor * lin.lora_weight_2(lin.lora_weight_1(x))
+    err = (base.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
+    g = torch.randn_like(y)
+    y.backward(g)
+    dx_ref = g.float().reshape(-1, 512) @ w + lin.lora_scaling_factor * (
+        g.float().reshape(-1, 512) @ lin.lora_weight_2.weight.float() @ lin.lora_weight_1.weight.float())
+    rel = ((x.grad.float().reshape(-1, 1024) - dx_ref).norm() / dx_ref.norm()).item()
+    assert rel < 0.08, rel
+    assert lin.lora_weight_1.weight.grad is not None

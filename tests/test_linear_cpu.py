@@ -48,3 +48,20 @@ def _sharded(rank, world):
 
 def test_base_weight_sharding_world2():
     run_distributed(_sharded, 2)
+
+
+def test_quantized_linear_mx_fp8_cpu_reference():
+    """8-bit e4m3 QuantizedLinear keeps an MX-FP8 copy; off-GPU it runs the dequantized MX weight."""
+    from hcache_deepspeed_amd.linear import QuantizationConfig
+    from hcache_deepspeed_amd.linear.quantization import QuantizedLinear
+    from hcache_deepspeed_amd.ops.fp8_gemm import mx_dequantize
+    torch.manual_seed(0)
+    ql = QuantizedLinear(512, 256, quantization_config=QuantizationConfig(q_bits=8, group_size=128),
+                         dtype=torch.float32)
+    assert ql.weight.mx_ok() and ql.weight.mx_shape == (256, 512)
+    x = torch.randn(4, 512)
+    w = mx_dequantize(*ql.weight.mx_w)
+    torch.testing.assert_close(ql(x), x @ w.t())
+    off = QuantizedLinear(512, 256, quantization_config=QuantizationConfig(q_bits=8, group_size=128, mx_fp8=False),
+                          dtype=torch.float32)
+    assert not off.weight.mx_ok()
