@@ -141,15 +141,27 @@ def main():
             engine.step()
         return loss
 
+    progress = os.environ.get("HDS_BENCH_PROGRESS") == "1"  # long-context sweeps: a line per step on stderr
+
+    def step_progress(tag, i, t_start):
+        if progress and rank == 0:
+            sync()
+            print(f"[bench] {tag} step {i} done at {time.perf_counter() - t_start:.1f}s "
+                  f"peak {torch.cuda.max_memory_allocated(dev) / 2**30 if on_gpu else 0:.1f} GiB", file=sys.stderr,
+                  flush=True)
+
     loss = None
+    tw = time.perf_counter()
     for i in range(args.warmup):
         loss = train_step(i)
+        step_progress("warmup", i, tw)
     sync()
     tdist.barrier()
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = train_step(args.warmup + i)
+        step_progress("timed", i, t0)
     sync()
     tdist.barrier()
     sync()

@@ -30,6 +30,13 @@ class DeepSpeedDataSampler:
         self.drop_last = drop_last
         self._order = np.argsort(self.metric, kind="stable")
 
+    @classmethod
+    def from_analyzer(cls, save_path, metric_name, global_batch_size, micro_batch_size, **kw):
+        """Sampler over the per-sample metric written by the data analyzer (data_sampling/data_analyzer.py; the
+        reference's ``<metric>_sample_to_metric`` index files are read the same way)."""
+        from .data_sampling.data_analyzer import load_sample_to_metric
+        return cls(load_sample_to_metric(save_path, metric_name), global_batch_size, micro_batch_size, **kw)
+
     def _eligible(self):
         if self.scheduler is None:
             return np.arange(self.n)
