@@ -8,6 +8,11 @@ micro-batch search ``run_tuning_micro_batch_sizes`` :741 with plateau early-stop
 package's per-node launcher) with ``autotuning.enabled`` in its config; the engine measures steps
 [start_profile_step, end_profile_step], writes ``{throughput, latency}`` to ``metric_path`` and exits.
 Experiments whose model states cannot fit the GPU (mem_estimators) are skipped without being launched.
+
+After the stage x micro-batch sweep, the best stage's ZeRO knobs (bucket sizes, overlap, ZeRO-3 prefetch /
+persistence / MI355X prefetch depth -- ``DEFAULT_TUNING_SPACES`` or the user's ``autotuning.tuning_space``) are
+searched at the chosen micro-batch by a tuner (reference autotuning/tuner/: ``gridsearch``, ``random``,
+``model_based``) under ``tuner_num_trials`` / ``tuner_early_stopping``.
 """
 import copy
 import json
@@ -20,6 +25,18 @@ from ..runtime.zero.mem_estimators import estimate
 from ..utils.logging import logger
 
 DEFAULT_STAGES = (0, 1, 2, 3)
+
+# knobs per ZeRO stage searched after the micro-batch sweep (sizes tuned for xGMI: bigger buckets, fewer calls)
+DEFAULT_TUNING_SPACES = {
+    1: {"zero_optimization": {"reduce_bucket_size": [int(5e7), int(2.5e8), int(5e8)],
+                              "allgather_bucket_size": [int(5e7), int(5e8)]}},
+    2: {"zero_optimization": {"reduce_bucket_size": [int(5e7), int(2.5e8), int(5e8)],
+                              "allgather_bucket_size": [int(5e7), int(5e8)], "overlap_comm": [True, False]}},
+    3: {"zero_optimization": {"reduce_bucket_size": [int(5e7), int(5e8)],
+                              "stage3_prefetch_bucket_size": [int(5e7), int(2e8)],
+                              "stage3_param_persistence_threshold": [int(1e4), int(1e6)]},
+        "mi355x": {"zero3_prefetch_depth": [1, 2, 3]}},
+}
 
 
 class Autotuner:
@@ -121,6 +138,42 @@ class Autotuner:
         return m
 
     def tune(self):
+        best = self._tune_stage_mbs()
+        if best is not None and self.at.get("tuner_type", "gridsearch") != "none":
+            self._tune_space(best)
+        return self.optimal
+
+    def _tune_space(self, best):
+        from .tuner import GridSearchTuner, ModelBasedTuner, RandomTuner
+        from .tuner.utils import gen_combinations, merge_dicts
+        base_cfg = best[2]
+        stage = base_cfg.get("zero_optimization", {}).get("stage", 0)
+        space = self.at.get("tuning_space", DEFAULT_TUNING_SPACES.get(stage))
+        if not space:
+            return
+        exps = []
+        for i, knobs in enumerate(gen_combinations(space)):
+            cfg = merge_dicts(copy.deepcopy(base_cfg), knobs)
+            name = f"{best[1]}_t{i}"
+            cfg["autotuning"] = dict(base_cfg["autotuning"],
+                                     metric_path=os.path.abspath(os.path.join(self.exps_dir, name + ".metric.json")))
+            exps.append({"name": name, "ds_config": cfg, "knobs": knobs})
+        kind = self.at.get("tuner_type", "gridsearch")
+        cls = {"gridsearch": GridSearchTuner, "random": RandomTuner, "model_based": ModelBasedTuner}[kind]
+
+        def run(exp):
+            m = self.run_ds_config(exp["ds_config"], exp["name"])
+            self.records[exp["name"]] = {"knobs": exp["knobs"], "metric": m}
+            return m
+
+        kw = {"tuning_space": space} if kind == "model_based" else {}
+        tuner = cls(exps, run, self.metric_name, **kw)
+        tuner.tune(sample_size=1, n_trials=int(self.at.get("tuner_num_trials", 50)),
+                   early_stopping=self.at.get("tuner_early_stopping", 5))
+        if tuner.best_exp is not None and tuner.best_metric_val > self.optimal[0]:
+            self.optimal = (tuner.best_metric_val, tuner.best_exp["name"], tuner.best_exp["ds_config"])
+
+    def _tune_stage_mbs(self):
         best = None
         for name, stage, mbs, cfg in self._generate_experiments():
             m = self.run_ds_config(cfg, name)

@@ -47,7 +47,9 @@ def test_autotuner_end_to_end_cpu(tmp_path, monkeypatch):
     cfg = {"train_micro_batch_size_per_gpu": 1, "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}},
            "autotuning": {"zero_stages": [0, 3], "min_train_micro_batch_size_per_gpu": 1,
                           "num_tuning_micro_batch_sizes": 2, "start_profile_step": 2, "end_profile_step": 4,
-                          "results_dir": str(tmp_path / "res"), "exps_dir": str(tmp_path / "exps")}}
+                          "results_dir": str(tmp_path / "res"), "exps_dir": str(tmp_path / "exps"),
+                          "tuner_type": "model_based", "tuner_num_trials": 2,
+                          "tuning_space": {"zero_optimization": {"reduce_bucket_size": [1000000, 10000000]}}}}
     cpath = tmp_path / "ds.json"
     cpath.write_text(json.dumps(cfg))
     monkeypatch.chdir(tmp_path)
@@ -60,6 +62,71 @@ def test_autotuner_end_to_end_cpu(tmp_path, monkeypatch):
     assert [e[0] for e in exps] == ["z0_mbs1", "z0_mbs2", "z3_mbs1", "z3_mbs2"]
     best = tuner.tune()
     assert best is not None and all(r["metric"] is not None for r in tuner.records.values())
+    assert sum(1 for k in tuner.records if "_t" in k) == 2  # the knob search ran after the stage x mbs sweep
     path = tuner.write_optimal_config()
     opt = json.load(open(path))
     assert "autotuning" not in opt and opt["zero_optimization"]["stage"] in (0, 3)
+
+
+def _fake_exps():
+    from hcache_deepspeed_amd.autotuning.tuner.utils import gen_combinations
+    space = {"zero_optimization": {"reduce_bucket_size": [1, 2, 4, 8, 16], "overlap_comm": [True, False]},
+             "mi355x": {"zero3_prefetch_depth": [1, 2, 3]}}
+    exps = [{"name": f"e{i}", "ds_config": c} for i, c in enumerate(gen_combinations(space))]
+    return space, exps
+
+
+def _fake_metric(exp):
+    z = exp["ds_config"]["zero_optimization"]
+    d = exp["ds_config"]["mi355x"]["zero3_prefetch_depth"]
+    if z["reduce_bucket_size"] == 16 and d == 3:
+        return None  # "OOM": a failed experiment
+    return {"throughput": 100 - (z["reduce_bucket_size"] - 4) ** 2 - 10 * (d - 2) ** 2 + 5 * z["overlap_comm"],
+            "latency": 1.0}
+
+
+@pytest.mark.parametrize("kind", ["gridsearch", "random", "model_based"])
+def test_tuners_find_best_config(kind):
+    from hcache_deepspeed_amd.autotuning.tuner import GridSearchTuner, ModelBasedTuner, RandomTuner
+    space, exps = _fake_exps()
+    assert len(exps) == 30
+    calls = []
+
+    def run(exp):
+        calls.append(exp["name"])
+        return _fake_metric(exp)
+
+    if kind == "gridsearch":
+        t = GridSearchTuner(exps, run, "throughput")
+    elif kind == "random":
+        t = RandomTuner(exps, run, "throughput", seed=1)
+    else:
+        t = ModelBasedTuner(exps, run, "throughput", tuning_space=space, seed=0)
+    n = t.tune(sample_size=1, n_trials=30)
+    assert n == 30 and len(set(calls)) == 30  # every config exactly once
+    best = t.best_exp["ds_config"]
+    assert best["zero_optimization"]["reduce_bucket_size"] == 4 and best["mi355x"]["zero3_prefetch_depth"] == 2
+    assert best["zero_optimization"]["overlap_comm"] is True
+
+
+def test_model_based_tuner_beats_random_order_on_budget():
+    from hcache_deepspeed_amd.autotuning.tuner import ModelBasedTuner
+    space, exps = _fake_exps()
+    hits = 0
+    for seed in range(5):
+        t = ModelBasedTuner(exps, _fake_metric, "throughput", tuning_space=space, seed=seed)
+        t.tune(sample_size=1, n_trials=12)
+        hits += t.best_metric_val == 105
+    assert hits >= 3  # finds the optimum within 12 of 30 trials most of the time
+
+
+def test_tuner_early_stopping_and_latency_metric():
+    from hcache_deepspeed_amd.autotuning.tuner import GridSearchTuner
+    space, exps = _fake_exps()
+    t = GridSearchTuner(exps, _fake_metric, "throughput")
+    n = t.tune(n_trials=100, early_stopping=3)
+    assert n < 30 and n >= t.best_iter + 3
+    lt = GridSearchTuner(exps, lambda e: {"latency": e["ds_config"]["zero_optimization"]["reduce_bucket_size"]},
+                         "latency")
+    lt.tune(n_trials=100)
+    assert lt.best_exp["ds_config"]["zero_optimization"]["reduce_bucket_size"] == 1
