@@ -176,12 +176,18 @@ def _hds_attention(module, query, key, value, attention_mask, scaling, dropout=0
         o = flash_attn(query.transpose(1, 2), key.transpose(1, 2).contiguous(), value.transpose(1, 2).contiguous(),
                        causal=True, softmax_scale=scaling)
         return o, None
-    rep = H // key.shape[1]
-    k = key.repeat_interleave(rep, 1) if rep > 1 else key
-    v = value.repeat_interleave(rep, 1) if rep > 1 else value
+    from ..ops.decode_attention import decode_attention, decode_supported, sdpa_gqa
     mask = attention_mask[:, :, :, :Skv] if attention_mask is not None and attention_mask.dim() == 4 else None
-    o = F.scaled_dot_product_attention(query, k, v, attn_mask=mask, is_causal=causal and mask is None and Sq > 1 and Sq == Skv,
-                                       scale=scaling)
+    if Sq == 1 and dropout == 0.0 and decode_supported(query[:, :, 0], key):
+        # generation step: one query row against the cache, GQA served from the kv heads directly
+        bias = None
+        if mask is not None:
+            m = mask[:, 0, -1, :]
+            bias = m if m.is_floating_point() else torch.zeros(m.shape, device=m.device).masked_fill(~m, float("-inf"))
+        o = decode_attention(query[:, :, 0], key, value, scaling, bias=bias)
+        return o[:, None], None
+    o = sdpa_gqa(query, key, value, mask=mask, is_causal=causal and mask is None and Sq > 1 and Sq == Skv,
+                 scale=scaling)
     return o.transpose(1, 2).contiguous(), None
 
 
@@ -197,6 +203,11 @@ def register_attention():
     try:
         from transformers import AttentionInterface
         AttentionInterface.register("hds_fused_attn", _hds_attention)
+        try:  # masks for our implementation: the SDPA form (None when plain causal -> the flash path)
+            from transformers.masking_utils import AttentionMaskInterface, sdpa_mask
+            AttentionMaskInterface.register("hds_fused_attn", sdpa_mask)
+        except ImportError:
+            pass
         return True
     except Exception:  # noqa: BLE001
         return False
@@ -239,6 +250,9 @@ def inject(model, quant=None, trainable=False, fuse_mlp=True):
             n += 1
         except Exception:  # noqa: BLE001
             pass
+    elif not trainable:
+        from .containers import inject_attention_containers
+        n += inject_attention_containers(model)  # GPT-J / GPT-Neo / BLOOM: family attention containers
     if quant is not None and quant.enabled:
         for parent in list(model.modules()):
             for cname, child in list(parent.named_children()):

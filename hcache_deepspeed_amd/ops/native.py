@@ -68,6 +68,9 @@ _KERNEL_SIGS = {
     "hds_gemm_mxfp8_supported": "iiiiii",
     "hds_gemm_mxfp8": "ppppp" + "iiiiii" + "f" + "i" + "s",
     "hds_mx_quant": "ppp" + "l" + "i" + "l" + "s",
+    "hds_decode_attn_supported": "ii",
+    "hds_decode_attn_splits": "iii",
+    "hds_decode_attn": "p" + "ll" + "p" + "lll" + "p" + "lll" + "p" + "l" + "p" + "ppp" + "iiiiii" + "f" + "s",
     "hds_embed_bwd": "i" + "pppp" + "l" + "i" + "ll" + "s",
     "hds_slice_mask": "i" + "ppp" + "iiiii" + "s",
     "hds_grouped_gemm_max_tiles": "ii",
