@@ -55,7 +55,29 @@ struct AttnParams {
   float scale;
   int causal;
   int window;  // >0: sliding window (keys in (q - window, q])
+  // Evoformer (EVO kernels only): additive biases and their gradients, batch = B * evo_n sequences of seq_len
+  const void* b1;  // [B*N][L]        (bf16 or fp32, bias_f32)
+  const void* b2;  // [B][H][L][L]
+  int bias_f32;
+  float* db1;      // [B*N][L]  fp32, accumulated
+  float* db2;      // [B][H][L][L] fp32, accumulated
+  int evo_n;
 };
+
+__device__ __forceinline__ float ld_bias(const AttnParams& p, const void* base, int64_t i) {
+  return p.bias_f32 ? reinterpret_cast<const float*>(base)[i] : (float)reinterpret_cast<const bf16*>(base)[i];
+}
+
+// Evoformer pair / mask bias of (sequence bn, head h, query q, key) (indices clamped; masked() zeroes padding)
+__device__ __forceinline__ float evo_bias(const AttnParams& p, int bn, int h, int q, int key) {
+  const int L = p.seq_len;
+  q = q < L ? q : L - 1;
+  key = key < L ? key : L - 1;
+  float x = 0.f;
+  if (p.b1) x += ld_bias(p, p.b1, (int64_t)bn * L + key);
+  if (p.b2) x += ld_bias(p, p.b2, ((int64_t)((bn / p.evo_n) * p.hq + h) * L + q) * L + key);
+  return x;
+}
 
 __device__ __forceinline__ void seq_bounds(const AttnParams& p, int b, int& start, int& len) {
   if (p.cu_seqlens) {
@@ -428,7 +450,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
 // (128 regs) + one 32x32 S/dP pair, which fits 256 registers -> 2 waves per SIMD, so one wave's
 // softmax/VALU section overlaps the other wave's MFMAs. The two query halves' partial dK/dV are
 // summed through LDS once at the end.
-template <int D, int PRIO>
+template <int D, int PRIO, bool EVO = false>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) {
   constexpr int BK = 128;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT;
@@ -539,8 +561,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * r4 + j;
-          float pr = fast_exp2(sacc[r] * c - l4[j] * kLog2e);
-          if (need_mask && masked(p, qt * BN + qr0 + j, myk, len)) pr = 0.f;
+          float x = sacc[r] * c - l4[j] * kLog2e;
+          if constexpr (EVO) x += evo_bias(p, b, hk, qt * BN + qr0 + j, myk) * kLog2e;
+          float pr = fast_exp2(x);
+          if ((EVO || need_mask) && masked(p, qt * BN + qr0 + j, myk, len)) pr = 0.f;
           sacc[r] = pr;
           dpacc[r] = pr * (dpacc[r] - d4[j]);
         }
@@ -589,7 +613,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
 // =====================================================================================
 // backward dQ
 // =====================================================================================
-template <int D, int NW, int PRIO>
+template <int D, int NW, int PRIO, bool EVO = false>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
@@ -686,10 +710,33 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float pr = fast_exp2(s[t][r] * c - lse2);
-          if (need_mask && masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) pr = 0.f;
+          const int key = k0 + 32 * t + acc_row(r, h);
+          float x = s[t][r] * c - lse2;
+          if constexpr (EVO) x += evo_bias(p, b, hq, myq, key) * kLog2e;
+          float pr = fast_exp2(x);
+          const bool off = masked(p, myq, key, len);
+          if ((EVO || need_mask) && off) pr = 0.f;
           s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
+          if constexpr (EVO) {
+            // pair-bias gradient, summed over the N rows of the MSA (float atomics into [B][H][L][L])
+            if (p.db2 && !off)
+              atomicAdd(p.db2 + ((int64_t)((b / p.evo_n) * p.hq + hq) * len + myq) * len + key, s[t][r]);
+          }
         }
+      if constexpr (EVO) {
+        if (p.db1) {  // mask-bias gradient: sum over this wave's 32 queries, then over heads by atomics
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              float v = s[t][r];
+#pragma unroll
+              for (int off = 1; off < 32; off <<= 1) v += __shfl_xor(v, off, 64);
+              const int key = k0 + 32 * t + acc_row(r, h);
+              if ((lane & 31) == 0 && key < len) atomicAdd(p.db1 + (int64_t)b * len + key, v);
+            }
+        }
+      }
       const bf16x8 sb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
@@ -738,6 +785,10 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
   p.scale = scale;
   p.causal = causal;
   p.window = window;
+  p.b1 = p.b2 = nullptr;
+  p.bias_f32 = 0;
+  p.db1 = p.db2 = nullptr;
+  p.evo_n = 1;
   return p;
 }
 
@@ -881,4 +932,42 @@ HDS_EXPORT int hds_attn_bwd(const void* q, const void* k, const void* v, const v
   HDS_ATTN_DIMS(HDS_CASE)
 #undef HDS_CASE
   return hipErrorInvalidValue;
+}
+
+// Evoformer attention backward (DS4Sci_EvoformerAttention): q/k/v/o/dout/dq/dk/dv [B, N, L, H, D] contiguous,
+// lse / delta in this file's [H][B*N*L] layout, biases b1 [B, N, 1, 1, L] and b2 [B, 1, H, L, L] (bf16 or fp32,
+// either may be null), fp32 gradient accumulators db1 [B*N, L] / db2 [B, H, L, L] (zeroed by the caller; null
+// when not wanted). Runs the FlashAttention backward kernels with the biases folded into P.
+HDS_EXPORT int hds_evoformer_bwd(const void* q, const void* k, const void* v, const void* o, const float* lse,
+                                 const void* dout, void* dq, void* dk, void* dv, float* delta, const void* b1,
+                                 const void* b2, int bias_f32, float* db1, float* db2, int B, int N, int L, int H,
+                                 int D, float scale, hipStream_t st) {
+  if (!(D == 32 || D == 64 || D == 128) || B <= 0 || N <= 0 || L <= 0 || H <= 0) return hipErrorInvalidValue;
+  int64_t strides[8];
+  for (int i = 0; i < 8; ++i) strides[i] = (int64_t)H * D;
+  const int batch = B * N, total = B * N * L;
+  AttnParams p = make_params(q, k, v, (void*)o, (float*)lse, dout, dq, dk, dv, delta, strides, nullptr, nullptr,
+                             batch, L, total, H, H, scale, 0, 0);
+  p.b1 = b1;
+  p.b2 = b2;
+  p.bias_f32 = bias_f32;
+  p.db1 = db1;
+  p.db2 = db2;
+  p.evo_n = N;
+  const int64_t rows = (int64_t)total * H;
+  switch (D) {
+#define HDS_EVO(d)                                                                                              \
+  case d:                                                                                                       \
+    hipLaunchKernelGGL(attn_bwd_delta_kernel<d>, dim3((rows + 15) / 16), dim3(256), 0, st, p);                 \
+    hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<d, 1, true>), dim3((L + 127) / 128, H, batch), dim3(512), 0, \
+                       st, p);                                                                                  \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<d, 8, 1, true>), dim3((L + 255) / 256, H, batch), dim3(512), 0, st, \
+                       p);                                                                                      \
+    break;
+    HDS_EVO(32)
+    HDS_EVO(64)
+    HDS_EVO(128)
+#undef HDS_EVO
+  }
+  return hipGetLastError();
 }

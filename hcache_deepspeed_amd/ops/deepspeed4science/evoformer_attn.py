@@ -8,7 +8,9 @@ Shapes: Q/K/V ``[B, N, L, H, D]``; ``bias1 = [B, N, 1, 1, L]`` (MSA mask, broadc
 ``bias2 = [B, 1, H, L, L]`` (pair bias, broadcast over the N rows). Output ``[B, N, L, H, D]``.
 
 Forward on the GPU (bf16, head_dim 32/64/128): the HIP kernel csrc/kernels/evoformer.hip (MFMA 32x32x16 flash
-attention with both biases fused, emits the LSE). Elsewhere, and for the backward: a memory-efficient flash-style
+attention with both biases fused, emits the LSE). Backward on the GPU: the FlashAttention dK/dV and dQ kernels
+(csrc/kernels/flash_attn.hip, ``EVO`` instantiations) with the biases folded into the recomputed P and the bias
+gradients reduced by fp32 atomics. Elsewhere: a memory-efficient flash-style
 decomposition -- the forward keeps only the fp32 log-sum-exp per
 query, the backward recomputes the probabilities one query chunk at a time, so peak memory is O(chunk x L)
 instead of O(L^2) per (B, N, H). The per-chunk products run as batched GEMMs on the matrix cores; head_dim is
@@ -60,6 +62,32 @@ def _hip_forward(q, k, v, b1, b2, scale):
     return o, lse
 
 
+def _hip_backward(ctx, do, qh, kh, vh, oh, lse, bias1, bias2, scale):
+    """HIP backward: the FlashAttention dK/dV and dQ kernels with both biases folded into P (flash_attn.hip
+    ``hds_evoformer_bwd``); dB2 is summed over the N rows and dB1 over heads/queries by fp32 atomics."""
+    from .. import native
+    B, N, H, L, D = qh.shape
+    q, k, v, o = (x.transpose(-2, -3) for x in (qh, kh, vh, oh))  # back to the contiguous [B, N, L, H, D]
+    do = do.contiguous()
+    lse_t = lse.permute(2, 0, 1, 3).reshape(H, B * N * L).contiguous()  # [H][tokens]
+    delta = torch.empty(H, B * N * L, dtype=torch.float32, device=q.device)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    want_b1 = bias1 is not None and ctx.needs_input_grad[3]
+    want_b2 = bias2 is not None and ctx.needs_input_grad[4]
+    db1 = torch.zeros(B * N, L, dtype=torch.float32, device=q.device) if want_b1 else None
+    db2 = torch.zeros(B, H, L, L, dtype=torch.float32, device=q.device) if want_b2 else None
+    bias_f32 = int((bias1 if bias1 is not None else bias2) is not None and
+                   (bias1 if bias1 is not None else bias2).dtype == torch.float32)
+    native.check(native.kernels().hds_evoformer_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                                    lse_t.data_ptr(), do.data_ptr(), dq.data_ptr(), dk.data_ptr(),
+                                                    dv.data_ptr(), delta.data_ptr(), native.ptr(bias1),
+                                                    native.ptr(bias2), bias_f32, native.ptr(db1), native.ptr(db2), B,
+                                                    N, L, H, D, float(scale), native.stream()), "evoformer_bwd")
+    g1 = db1.view(B, N, 1, 1, L).to(bias1.dtype) if want_b1 else None
+    g2 = db2.view(B, 1, H, L, L).to(bias2.dtype) if want_b2 else None
+    return dq, dk, dv, g1, g2
+
+
 class EvoformerFusedAttention(torch.autograd.Function):
 
     @staticmethod
@@ -72,6 +100,7 @@ class EvoformerFusedAttention(torch.autograd.Function):
             o, lse = _hip_forward(q, k, v, bias1, bias2, scale)
             ctx.save_for_backward(qh, kh, vh, o.transpose(-2, -3), lse, bias1, bias2)
             ctx.scale = scale
+            ctx.hip = True
             return o
         o = torch.empty(qh.shape, dtype=q.dtype, device=q.device)
         lse = torch.empty(B, N, H, L, dtype=torch.float32, device=q.device)
@@ -92,6 +121,8 @@ class EvoformerFusedAttention(torch.autograd.Function):
         qh, kh, vh, o, lse, bias1, bias2 = ctx.saved_tensors
         scale = ctx.scale
         B, N, H, L, D = qh.shape
+        if getattr(ctx, "hip", False):
+            return _hip_backward(ctx, do, qh, kh, vh, o, lse, bias1, bias2, scale)
         doh = do.transpose(-2, -3)
         delta = (doh.float() * o.float()).sum(-1)  # [B, N, H, L]
         dq = torch.empty(qh.shape, dtype=torch.float32, device=qh.device)
