@@ -66,10 +66,34 @@ __device__ __forceinline__ bf16x8 read_tr(const char* lds_tile, int s, int dt) {
   const char* a1 = lds_tile + tile_off(row + 8, ch) + 8 * (p & 1);
   bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(a0));
   bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(a1));
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// read_tr issued as inline asm: hipcc puts an `s_waitcnt vmcnt(0)` in front of every ds_read_b64_tr_b16 builtin
+// that follows an LDS-DMA (it cannot tell the DMA's destination from the tile being read), which stalls a wave on
+// its own prefetch of the NEXT tile. The asm form is invisible to that analysis; the caller retires it with
+// lds_wait<N>() (lgkmcnt counts in issue order, so a count that also covers compiler-issued reads stays safe).
+__device__ __forceinline__ bf16x4 ds_tr_asm(const char* a) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)a) : "memory");
   return r;
+}
+__device__ __forceinline__ bf16x8 read_tr_asm(const char* lds_tile, int s, int dt) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = 16 * s + 4 * (g >> 1) + q;
+  const int ch = 4 * dt + 2 * (g & 1) + (p >> 1);
+  const bf16x4 lo = ds_tr_asm(lds_tile + tile_off(row, ch) + 8 * (p & 1));
+  const bf16x4 hi = ds_tr_asm(lds_tile + tile_off(row + 8, ch) + 8 * (p & 1));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 tr_d_asm(const char* tile, int s, int dt) {
+  return read_tr_asm(tile + (dt >> 2) * 16384, s, dt & 3);
+}
+template <int N>
+__device__ __forceinline__ void lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs that consume the asm reads behind the wait (guide rule 18)
 }
 
 // B-operand fragment for k-step (s & 1) of a 32-row accumulator tile: registers 8*(s&1) .. +7.
@@ -86,6 +110,14 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
 }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// max of three without the NaN-canonicalising v_max_f32 x,x that hipcc puts in front of every fmaxf on an MFMA
+// result (two instructions per score); the scores are finite or -inf, so IEEE NaN handling is moot here
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 
 // ---- head-dim generic tiles -------------------------------------------------------------------
 // A D-wide 64-row tile is ceil(D/128) 128-column sub-tiles in the layout above; only the first D/8 16-byte
@@ -120,6 +152,27 @@ __device__ __forceinline__ void stage_tile_d(char* tile, RowPtr row_ptr) {
 #pragma unroll
     for (int i = 0; i < 16 / NW; ++i) {
       const int n = w * (16 / NW) + i;
+      const int row = 4 * n + (lane >> 4);
+      const int ch = (lane & 15) ^ swz(row);
+      if (nch == kFull || ch < nch) {
+        const char* src = (const char*)(row_ptr(row) + 128 * c) + ch * 16;
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(tile + c * 16384 + n * 1024), 16, 0, 0);
+      }
+    }
+  }
+}
+
+// Same as stage_tile_d, but staged by a GROUP of NWG waves: wi = this wave's index inside the group.
+template <int NWG, int D, typename RowPtr>
+__device__ __forceinline__ void stage_tile_dw(char* tile, RowPtr row_ptr, int wi) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < Dim<D>::NT; ++c) {
+    constexpr int kFull = 16;
+    const int nch = (D - 128 * c) >= 128 ? kFull : (D - 128 * c) / 8;
+#pragma unroll
+    for (int i = 0; i < 16 / NWG; ++i) {
+      const int n = wi * (16 / NWG) + i;
       const int row = 4 * n + (lane >> 4);
       const int ch = (lane & 15) ^ swz(row);
       if (nch == kFull || ch < nch) {

@@ -207,17 +207,20 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       }
       const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
                              (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
+      // the max runs on the raw scores and the scale is folded into the exponent's FMA (c > 0), which saves a
+      // multiply per score: the softmax VALU, not the MFMA pipe, bounds this loop
       float tmax = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t) {
+        if (need_mask) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float x = s[t][r] * c;
-          if (need_mask && masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) x = -INFINITY;
-          s[t][r] = x;
-          tmax = fmaxf(tmax, x);
+          for (int r = 0; r < 16; ++r)
+            if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) s[t][r] = -INFINITY;
         }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) tmax = max3_raw(tmax, s[t][r], s[t][r + 1]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
       float alpha = 1.f, muse;
       if constexpr ((VAR & 2) != 0) {
         if (!__all(tmax <= m + kDeferThr)) {  // some row outgrew the stale max: move every row's max now
@@ -243,22 +246,209 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = fast_exp2(s[t][r] - muse);
+          const float e = fast_exp2(__builtin_fmaf(s[t][r], c, -muse));
           s[t][r] = e;
           rs += e;
         }
       rs += __shfl_xor(rs, 32, 64);
       l = l * alpha + rs;
       bf16x8 pb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
+      if constexpr ((VAR & 2) != 0) {
+        // V^T fragments by asm transposed reads (no compiler vmcnt(0) on the next tile's DMA in flight),
+        // one 32-column block ahead of its MFMAs
+        bf16x8 vf[2][4];
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
+        for (int st = 0; st < 4; ++st) vf[0][st] = tr_d_asm(Vt, st, 0);
 #pragma unroll
-        for (int st = 0; st < 4; ++st) o[dt] = mfma(tr_d(Vt, st, dt), pb[st], o[dt]);
+        for (int dt = 0; dt < DT; ++dt) {
+          if (dt + 1 < DT) {
+#pragma unroll
+            for (int st = 0; st < 4; ++st) vf[(dt + 1) & 1][st] = tr_d_asm(Vt, st, dt + 1);
+            lds_wait<8>();
+          } else {
+            lds_wait<0>();
+          }
+#pragma unroll
+          for (int st = 0; st < 4; ++st) o[dt] = mfma(vf[dt & 1][st], pb[st], o[dt]);
+        }
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int st = 0; st < 4; ++st) o[dt] = mfma(tr_d(Vt, st, dt), pb[st], o[dt]);
+      }
     }
     __syncthreads();
   }
 
   // epilogue: O[myq][d] = o^T / l ; lse
+  if (myq < len) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* op = p.o + (int64_t)(start + myq) * p.so + (int64_t)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) store_row_block<D>(op, o[dt], dt, h, inv);
+    if (h == 0 && p.lse) {
+      const float lse = (l > 0.f) ? (m + __log2f(l)) / kLog2e : -INFINITY;
+      p.lse[(int64_t)hq * p.total_tokens + start + myq] = lse;
+    }
+  }
+}
+
+// =====================================================================================
+// forward, staggered wave groups (D <= 128, 8 waves)
+// =====================================================================================
+// Every key tile is two SECTIONS separated by a raw barrier: S (S^T = K.Q^T, online softmax, O rescale) and P
+// (O^T += V^T.P^T). Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's P-section MFMAs run
+// beside its partner's S-section MFMAs + softmax VALU instead of both waves doing the same phase at once
+// (MI355X_MICROARCH "Two waves per SIMD" item 9). The K/V ring stays two tiles deep; waves 0-3 stage K and
+// waves 4-7 stage V, each during its S section, for the tile after next -- a buffer is restaged only after the
+// lagging group's last read of it -- and each group retires its own DMA (vmcnt(0)) before the barrier that closes
+// its P section, one section before the leading group first reads the tile.
+template <int D>
+__global__ __launch_bounds__(512) void attn_fwd_stg_kernel(AttnParams p) {
+  constexpr int NW = 8, BM = 32 * NW;
+  constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
+  static_assert(D <= 128, "staggered forward: head_dim <= 128");
+  __shared__ __attribute__((aligned(16))) char smem[4 * TL];  // K[2], V[2]
+  int blk, hq, b;
+  lpt_ids(blk, hq, b);
+  int start, len;
+  seq_bounds(p, b, start, len);
+  const int nqb = (len + BM - 1) / BM;
+  const int qb = p.causal ? (gridDim.x - 1 - blk) : blk;
+  if (qb >= nqb || len == 0) return;
+  const int hk = hq / (p.hq / p.hkv);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = w >> 2;  // 0: leading group (stages K), 1: lagging group (stages V)
+  const int q0 = qb * BM;
+  const int myq = q0 + 32 * w + (lane & 31);
+  const float c = p.scale * kLog2e;
+
+  bf16x8 qf[KS];
+  {
+    const int qr = myq < len ? myq : len - 1;
+    const bf16* qp = p.q + (int64_t)(start + qr) * p.sq + (int64_t)hq * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+  }
+  int kt_end = (len + BN - 1) / BN;
+  if (p.causal) {
+    const int last = q0 + BM - 1 < len - 1 ? q0 + BM - 1 : len - 1;
+    kt_end = last / BN + 1;
+  }
+  int kt_begin = 0;
+  if (p.window > 0) {
+    const int first = q0 - p.window + 1;
+    kt_begin = first > 0 ? first / BN : 0;
+  }
+  auto rowp = [&](const bf16* base, int64_t stride, int kt) {
+    return [=](int row) {
+      int r = kt * BN + row;
+      r = r < len ? r : len - 1;
+      return base + (int64_t)(start + r) * stride + (int64_t)hk * D;
+    };
+  };
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+  const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
+
+  // prologue: the first tile's K and V by every wave
+  stage_tile_d<NW, D>(smem + 0, rowp(p.k, p.sk, kt_begin));
+  stage_tile_d<NW, D>(smem + 2 * TL, rowp(p.v, p.sv, kt_begin));
+  __syncthreads();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // waves 4-7 start one section behind
+
+  bf16x8 pb[4];
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
+    const char* Kt = smem + buf * TL;
+    const char* Vt = smem + 2 * TL + buf * TL;
+    const int k0 = kt * BN;
+    bool skip = (k0 >= len) || (wq_lo >= len);
+    if (p.causal && k0 > wq_hi) skip = true;
+    if (p.window > 0 && k0 + BN - 1 <= wq_lo - p.window) skip = true;
+    // ---- S section: stage the next tile's K (group 0) / V (group 1), S = K.Q^T, softmax ----
+    if (kt + 1 < kt_end) {
+      if (grp == 0)
+        stage_tile_dw<4, D>(smem + (buf ^ 1) * TL, rowp(p.k, p.sk, kt + 1), w & 3);
+      else
+        stage_tile_dw<4, D>(smem + 2 * TL + (buf ^ 1) * TL, rowp(p.v, p.sv, kt + 1), w & 3);
+    }
+    if (!skip) {
+      f32x16 s[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[t] = mfma(rows_d(Kt, 32 * t, ks), qf[ks], s[t]);
+      }
+      const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
+                             (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (need_mask) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) s[t][r] = -INFINITY;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) tmax = max3_raw(tmax, s[t][r], s[t][r + 1]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
+      float alpha = 1.f;
+      if (!__all(tmax <= m + kDeferThr)) {  // deferred running max (guide T13)
+        const float mnew = fmaxf(m, tmax);
+        alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
+        m = mnew;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      }
+      const float muse = (m == -INFINITY) ? 0.f : m;
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = fast_exp2(__builtin_fmaf(s[t][r], c, -muse));
+          s[t][r] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      pb[0] = acc_to_b<0>(s[0]);
+      pb[1] = acc_to_b<1>(s[0]);
+      pb[2] = acc_to_b<0>(s[1]);
+      pb[3] = acc_to_b<1>(s[1]);
+    }
+    __builtin_amdgcn_s_barrier();
+    // ---- P section: O^T += V^T.P^T (V^T fragments one 32-column block ahead of the MFMAs) ----
+    if (!skip) {
+      bf16x8 vf[2][4];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) vf[0][st] = read_tr_asm(Vt, st, 0);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        if (dt + 1 < DT) {
+#pragma unroll
+          for (int st = 0; st < 4; ++st) vf[(dt + 1) & 1][st] = read_tr_asm(Vt, st, dt + 1);
+          lds_wait<8>();  // block dt's 8 reads are done, block dt+1's may still fly
+        } else {
+          lds_wait<0>();
+        }
+#pragma unroll
+        for (int st = 0; st < 4; ++st) o[dt] = mfma(vf[dt & 1][st], pb[st], o[dt]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the next tile has landed
+    __builtin_amdgcn_s_barrier();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // rejoin
+
   if (myq < len) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     bf16* op = p.o + (int64_t)(start + myq) * p.so + (int64_t)hq * D;
@@ -796,9 +986,10 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1;
 
-// forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both
+// forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
+// 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 3) return hipErrorInvalidValue;
+  if (var < 0 || var > 4) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -826,6 +1017,7 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
       const dim3 grid((max_len + 255) / 256, hq, batch);
       if constexpr (D == 128) {  // the A/B variants exist for the training head dim only
         switch (g_fwd_var) {
+          case 4: hipLaunchKernelGGL((attn_fwd_stg_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;

@@ -623,3 +623,43 @@ def test_decode_attention_matches_reference_gpu(D, H, Hkv, S):
         out = decode_attention(q, k, v, 0.1, **kw)
         ref = decode_attention_ref(q.float(), k.float(), v.float(), 0.1, kw.get("bias"), kw.get("alibi"))
         torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["causal", "full", "window", "varlen"])
+def test_flash_fwd_staggered_variant_gpu(case):
+    """Forward variant 4 (staggered wave groups, asm transposed reads) against the fp32 reference."""
+    from hcache_deepspeed_amd.ops import native
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    lib = native.kernels()
+    torch.manual_seed(7)
+    B, S, Hq, Hkv, D = 2, 700, 8, 2, 128
+    q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    kw = dict(causal=case != "full", window=100 if case == "window" else 0)
+    try:
+        outs = {}
+        for var in (2, 4):
+            assert lib.hds_attn_fwd_variant(var) == 0
+            if case == "varlen":
+                cu = torch.tensor([0, 333, 2 * S], device="cuda", dtype=torch.int32)
+                outs[var] = flash_attn(q.reshape(-1, Hq, D), k.reshape(-1, Hkv, D), v.reshape(-1, Hkv, D),
+                                       causal=True, cu_seqlens=cu)
+            else:
+                outs[var] = flash_attn(q, k, v, **kw)
+    finally:
+        lib.hds_attn_fwd_variant(2)
+    d = (outs[4].float() - outs[2].float()).abs().max().item()
+    assert d < 3e-2, d  # both within bf16 rounding of each other (same math, different schedule)
+    if case != "varlen":
+        qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k.repeat_interleave(4, 2), v.repeat_interleave(4, 2)))
+        s = qf @ kf.transpose(-1, -2) / D**0.5
+        i = torch.arange(S, device="cuda")
+        mask = torch.zeros(S, S, dtype=torch.bool, device="cuda")
+        if kw["causal"]:
+            mask |= i[None, :] > i[:, None]
+        if kw["window"]:
+            mask |= i[None, :] <= i[:, None] - kw["window"]
+        ref = (torch.softmax(s.masked_fill(mask, float("-inf")), -1) @ vf).transpose(1, 2)
+        torch.testing.assert_close(outs[4].float(), ref, atol=2e-2, rtol=2e-2)

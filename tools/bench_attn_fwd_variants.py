@@ -1,5 +1,5 @@
 """Sweep the FlashAttention forward variants (static priority / deferred max) at the bench shape
-(Llama-3-8B heads, B=6, S=4096, causal) and report TF/s plus the max deviation from variant 0 and from an fp32
+(Llama-3-8B heads, B=7, S=4096, causal) and report TF/s plus the max deviation from variant 0 and from an fp32
 reference on a slice."""
 import sys
 import time
@@ -22,7 +22,7 @@ def timeit(fn, iters=20):
 
 
 def main():
-    B, S, Hq, Hkv, D = 6, 4096, 32, 8, 128
+    B, S, Hq, Hkv, D = 7, 4096, 32, 8, 128
     torch.manual_seed(0)
     q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
     k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
@@ -35,7 +35,7 @@ def main():
     s = s.masked_fill(torch.triu(torch.ones(S, S, device="cuda", dtype=torch.bool), 1), float("-inf"))
     ref = (torch.softmax(s, -1) @ vf).transpose(0, 1)
     base = None
-    for var in (0, 1, 2, 3):
+    for var in (2, 4, 2, 4):
         lib.hds_attn_fwd_variant(var)
         o = flash_attn(q, k, v, causal=True)
         t = timeit(lambda: flash_attn(q, k, v, causal=True))
@@ -45,11 +45,11 @@ def main():
         dr = (o[0, :, :4].float() - ref).abs().max().item()
         print(f"fwd variant {var}: {t*1e3:.3f} ms {fl/t/1e12:.0f} TF/s | max|o-o_v0| {d0:.3e} | max|o-ref32| {dr:.3e}",
               flush=True)
-    lib.hds_attn_fwd_variant(3)
+    lib.hds_attn_fwd_variant(2)
     do = torch.randn_like(q)
     qg, kg, vg = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
     grads0 = None
-    for prio in (0, 1):
+    for prio in (1,):
         lib.hds_attn_bwd_prio(prio)
 
         def fb():
