@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--layers", type=int, default=0, help="debug only: override layer count (result is marked invalid)")
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
+    ap.add_argument("--act-cache-budget-gib", type=float, default=0.0,
+                    help="host activation cache: HBM budget the planner keeps activations under (0: 92%% of HBM)")
     ap.add_argument("--host-act-cache", action="store_true",
                     help="HCache host activation cache (saved activations spill to pinned host memory)")
     ap.add_argument("--offload", choices=["none", "cpu", "nvme"], default="none",
@@ -107,7 +109,8 @@ def main():
                                                    "weight_decay": 0.1}},
         "gradient_clipping": 1.0,
         "zero_optimization": {"stage": args.zero},
-        "mi355x": {"zero3_prefetch_depth": args.prefetch, "host_act_cache": {"enabled": bool(args.host_act_cache)}},
+        "mi355x": {"zero3_prefetch_depth": args.prefetch, "host_act_cache": {"enabled": bool(args.host_act_cache),
+                                                                        "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }
     if args.offload != "none":

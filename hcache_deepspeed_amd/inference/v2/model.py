@@ -70,7 +70,7 @@ class RaggedTransformer:
             self.cos = self.sin = None
         self.scale = 1.0 / math.sqrt(D)
         self.kv_cache = None
-        self.copy_stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self.copy_stream = torch.cuda.Stream(device, priority=-1) if device.type == "cuda" else None
 
     # ------------------------------------------------------------------------------------------
     # weights: canonical dict (arch.convert_*) -> this rank's shards

@@ -11,9 +11,12 @@ Mechanism (``torch.autograd.graph.saved_tensors_hooks``):
   ``min_layers_resident`` blocks is copied D2H on a dedicated HIP copy stream into a pinned host buffer
   from a reuse pool (``offload/pinned.py``, hipHostMalloc). The GPU tensor is released immediately with
   ``record_stream`` so the caching allocator recycles it once the DMA has drained -- forward never waits.
-* backward/unpack: when block i's tensors are first needed, block i-1's tensors are prefetched H2D on the
-  copy stream (reverse layer order), so the PCIe transfer overlaps block i's backward; the compute stream
-  only waits on the per-tensor HIP event.
+* backward/unpack: when backward first touches ANY saved tensor of block i (spilled or resident -- resident
+  tensors of tracked blocks carry a small layer tag for exactly this), the spilled tensors of blocks
+  i-1 .. i-prefetch_layers are prefetched H2D on the copy stream (reverse layer order), so the PCIe transfer
+  overlaps the backward of the blocks after them; the compute stream only waits on the per-tensor HIP event.
+  (Tagging resident tensors matters under the budget policy: the spilled blocks are the EARLIEST ones, whose
+  successors are all resident -- without the tag nothing would start their prefetch before they are needed.)
 Parameters (autograd leaves) and small tensors are never offloaded.
 
 Budget policy (``gpu_budget_bytes``): spilling everything is PCIe-bound (at 32k tokens a Llama-3-8B layer saves
@@ -25,6 +28,9 @@ D2H has the whole remaining forward to drain and their H2D the whole remaining b
 guard still spills any tensor that would push the allocation past the budget.
 """
 import contextlib
+import os
+import sys
+import time
 
 import torch
 import torch.nn as nn
@@ -41,6 +47,14 @@ class _Spilled:
         self.h2d_done = None
 
 
+class _Tagged:
+    """A resident saved tensor of a tracked block: unpacking it tells the cache where backward is."""
+    __slots__ = ("t", "layer")
+
+    def __init__(self, t, layer):
+        self.t, self.layer = t, layer
+
+
 class HostActivationCache:
 
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
@@ -54,7 +68,9 @@ class HostActivationCache:
         self.keep = int(min_layers_resident)
         self.prefetch_layers = int(prefetch_layers)
         self.pool = PinnedPool()
-        self.stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+        # high priority: HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues round-robin, and a copy that
+        # lands in the compute stream's queue cannot start before every kernel queued ahead of it has finished
+        self.stream = torch.cuda.Stream(device, priority=-1) if device.type == "cuda" else None
         self.cur_layer = -1
         self.n_layers = 0
         self.by_layer = {}
@@ -115,7 +131,7 @@ class HostActivationCache:
         self.layer_bytes[self.cur_layer] = self.layer_bytes.get(self.cur_layer, 0) + nbytes
         if (self.plan is not None and self.cur_layer not in self.plan
                 and torch.cuda.memory_allocated(self.device) + nbytes <= self.budget):
-            return t
+            return _Tagged(t, self.cur_layer) if self.by_layer else t  # tag only when something was spilled
         s = _Spilled()
         s.shape, s.dtype, s.device, s.layer = t.shape, t.dtype, t.device, self.cur_layer
         src = t if t.is_contiguous() else t.contiguous()
@@ -135,23 +151,46 @@ class HostActivationCache:
     def _prefetch(self, s):
         if s.dev is not None:
             return
+        # Allocate on the COMPUTE stream: its caching-allocator pool holds the blocks backward just freed, while
+        # an allocation on the copy stream finds an empty per-stream pool and, with HBM nearly full, makes the
+        # allocator free cached blocks -- a device-wide synchronize that serialises every copy with compute.
+        cur = torch.cuda.current_stream()
+        s.dev = torch.empty(s.shape, dtype=s.dtype, device=s.device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(s.d2h_done)
-            s.dev = torch.empty(s.shape, dtype=s.dtype, device=s.device)
+            self.stream.wait_event(ready)
             s.dev.view(-1).copy_(s.host, non_blocking=True)
+            s.dev.record_stream(self.stream)
             s.h2d_done = torch.cuda.Event()
             s.h2d_done.record(self.stream)
 
+    _DEBUG = os.environ.get("HDS_ACT_CACHE_DEBUG") == "1"
+
+    def _prefetch_before(self, layer):
+        for j in range(1, self.prefetch_layers + 1):
+            lst = self.by_layer.get(layer - j, ())
+            if self._DEBUG and lst and lst[0].dev is None:
+                print(f"[act-cache] t={time.perf_counter():.3f} backward at layer {layer}: prefetch layer {layer - j} "
+                      f"({len(lst)} tensors), allocated {torch.cuda.memory_allocated(self.device) / 2**30:.1f} GiB",
+                      file=sys.stderr, flush=True)
+            for o in lst:
+                self._prefetch(o)
+
     def _unpack(self, s):
+        if isinstance(s, _Tagged):
+            self._prefetch_before(s.layer)
+            return s.t
         if not isinstance(s, _Spilled):
             return s
+        if self._DEBUG and s.dev is None:
+            print(f"[act-cache] t={time.perf_counter():.3f} layer {s.layer} needed before its prefetch", file=sys.stderr,
+                  flush=True)
         self._prefetch(s)
-        for j in range(1, self.prefetch_layers + 1):
-            for o in self.by_layer.get(s.layer - j, ()):
-                self._prefetch(o)
+        self._prefetch_before(s.layer)
         torch.cuda.current_stream().wait_event(s.h2d_done)
         out = s.dev
-        out.record_stream(torch.cuda.current_stream())
         s.dev = None
         self.pool.put(s.host)
         s.host = None

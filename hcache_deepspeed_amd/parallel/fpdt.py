@@ -72,7 +72,7 @@ class _HostChunks:
 
     def __init__(self, offload, device):
         self.offload = bool(offload) and device.type == "cuda"
-        self.stream = torch.cuda.Stream(device) if self.offload else None
+        self.stream = torch.cuda.Stream(device, priority=-1) if self.offload else None
         self.host, self.ready, self.dev = {}, {}, {}
 
     def put(self, key, t):

@@ -168,7 +168,7 @@ class HostActCacheConfig:
     min_layers_resident: int = 2
     policy: str = "budget"  # "budget": spill only what exceeds gpu_budget_gib; "all": spill every eligible layer
     gpu_budget_gib: float = 0.0  # 0: 92% of device memory
-    prefetch_layers: int = 2
+    prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block
 
 
 @dataclass

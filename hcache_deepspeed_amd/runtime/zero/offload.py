@@ -90,8 +90,10 @@ class OffloadZeroOptimizer(ZeroOptimizer):
         if self.n_off == n:
             s.master = None
             s.states = {k: None for k in s.states}
-        self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None  # D2H
-        self.h2d_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None  # H2D
+        # copy streams at high priority: a stream that shares a hardware queue with the compute stream (HIP
+        # spreads streams over GPU_MAX_HW_QUEUES=4 queues) cannot start a copy before the kernels queued ahead
+        self.copy_stream = torch.cuda.Stream(self.device, priority=-1) if self.device.type == "cuda" else None  # D2H
+        self.h2d_stream = torch.cuda.Stream(self.device, priority=-1) if self.device.type == "cuda" else None  # H2D
         log_dist(f"ZeRO-Offload: {self.n_off / 1e6:.1f}M of {n / 1e6:.1f}M elements on {self.offload_device} "
                  f"(sub-group {self.sub / 1e6:.1f}M)" + (", parameters on NVMe" if self.nvme_param else ""),
                  ranks=[0])

@@ -244,7 +244,7 @@ class ZeroOptimizer:
         self.nvme_param = self.offload_param and op.device == "nvme"
         self.param_swapper = None
         if self.offload_param and self.device.type == "cuda":
-            self.param_h2d_stream = torch.cuda.Stream(self.device)
+            self.param_h2d_stream = torch.cuda.Stream(self.device, priority=-1)
         else:
             self.param_h2d_stream = None
         self._build_units(leaf_modules)

@@ -1,0 +1,11 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp HDS_BENCH_PROGRESS=1
+mkdir -p gpurun_out/actc
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_host_tier_gpu.py > gpurun_out/actc/test.log 2>&1 || { echo "rc=$?" >> gpurun_out/actc/test.log; exit 1; }
+for B in 0 240; do
+  timeout -k 10 400 python -u bench.py --seq 32768 --micro-batch 1 --host-act-cache --act-cache-budget-gib $B --steps 3 --warmup 2 > gpurun_out/actc/bench3_b$B.log 2>&1 || exit 1
+done
+timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/actc/trace3 -o run -- python3 bench.py --seq 32768 --micro-batch 1 --host-act-cache --steps 1 --warmup 2 > gpurun_out/actc/trace3.log 2>&1 || exit 1
+python3 tools/overlap_report.py gpurun_out/actc/trace3 > gpurun_out/actc/overlap3.txt 2>&1 || true
+find gpurun_out/actc/trace3 -name "*.csv" -size +30M -delete
