@@ -58,8 +58,12 @@ class _Tagged:
 class HostActivationCache:
 
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
-                 gpu_budget_bytes=None):
+                 gpu_budget_bytes=None, host_budget_bytes=None):
         self.device = device
+        # pinned host bytes the cache may hold at once (the calibration step spills every eligible layer; at long
+        # context that alone can exceed the host's memory): beyond it tensors stay on the GPU
+        self.host_budget = host_budget_bytes
+        self.host_in_use = 0
         self.budget = gpu_budget_bytes  # None: spill every eligible layer (no planning)
         self.plan = None  # set of layer indices to spill once calibrated
         self.layer_bytes = {}
@@ -84,8 +88,13 @@ class HostActivationCache:
             gib = float(getattr(cfg, "gpu_budget_gib", 0.0) or 0.0)
             total = torch.cuda.get_device_properties(device).total_memory
             budget = int(gib * 2**30) if gib > 0 else int(0.92 * total)
+        hgib = float(getattr(cfg, "host_budget_gib", 0.0) or 0.0)
+        if hgib <= 0:
+            import psutil
+            hgib = min(0.4 * psutil.virtual_memory().total / 2**30, 160.0)
         return cls(device, min_bytes=1 << 20, min_layers_resident=cfg.min_layers_resident,
-                   prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget)
+                   prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget,
+                   host_budget_bytes=int(hgib * 2**30))
 
     # ---------------------------------------------------------------------------------------
     def attach(self, model):
@@ -116,6 +125,12 @@ class HostActivationCache:
                 self._calibrating = True
                 torch.cuda.reset_peak_memory_stats(self.device)
         self.cur_layer = -1
+        for lst in self.by_layer.values():  # a forward whose backward never ran: return its host buffers
+            for o in lst:
+                if o.host is not None:
+                    self.pool.put(o.host)
+                    self.host_in_use -= o.host.numel() * o.host.element_size()
+                    o.host = None
         self.by_layer = {}
         self.layer_bytes = {}
         with torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack):
@@ -132,6 +147,8 @@ class HostActivationCache:
         if (self.plan is not None and self.cur_layer not in self.plan
                 and torch.cuda.memory_allocated(self.device) + nbytes <= self.budget):
             return _Tagged(t, self.cur_layer) if self.by_layer else t  # tag only when something was spilled
+        if self.host_budget is not None and self.host_in_use + nbytes > self.host_budget:
+            return _Tagged(t, self.cur_layer) if self.by_layer else t
         s = _Spilled()
         s.shape, s.dtype, s.device, s.layer = t.shape, t.dtype, t.device, self.cur_layer
         src = t if t.is_contiguous() else t.contiguous()
@@ -145,6 +162,7 @@ class HostActivationCache:
             s.d2h_done = torch.cuda.Event()
             s.d2h_done.record(self.stream)
         self.bytes_offloaded += src.numel() * src.element_size()
+        self.host_in_use += src.numel() * src.element_size()
         self.by_layer.setdefault(s.layer, []).append(s)
         return s
 
@@ -193,6 +211,7 @@ class HostActivationCache:
         out = s.dev
         s.dev = None
         self.pool.put(s.host)
+        self.host_in_use -= s.host.numel() * s.host.element_size()
         s.host = None
         return out
 

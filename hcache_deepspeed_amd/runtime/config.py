@@ -169,6 +169,7 @@ class HostActCacheConfig:
     policy: str = "budget"  # "budget": spill only what exceeds gpu_budget_gib; "all": spill every eligible layer
     gpu_budget_gib: float = 0.0  # 0: 92% of device memory
     prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block
+    host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: min(40% of host RAM, 160 GiB))
 
 
 @dataclass
