@@ -41,6 +41,11 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
         self._training_latency = 0.0
         self._total_latency = 0.0
         self._iters = 0
+        self._gather_latency = 0.0
+        self._total_batch_size = None
+        self._e2e_start = None
+        self._eval_iters = 0
+        self.last_latency_report = None
         self._training_start_time = None
         self._t_start = time.time()
         self._in_generate = False
@@ -60,11 +65,53 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
             m.unfuse_lora_weight()
 
     # ---- generation --------------------------------------------------------------------------
+    def _mp_group(self):
+        """Model-parallel group for ``inference_tp_size > 1``: consecutive ranks (reference
+        create_inference_module :315-338), created once."""
+        if self.inference_tp_size <= 1:
+            return None
+        if getattr(self, "_he_mp_group", None) is None:
+            from .. import comm as dist
+            tp, world, rank = self.inference_tp_size, dist.get_world_size(), dist.get_rank()
+            assert world % tp == 0, f"inference_tp_size={tp} must divide world size {world}"
+            for g in range(world // tp):
+                ranks = list(range(g * tp, (g + 1) * tp))
+                grp = dist.new_group(ranks)
+                if rank in ranks:
+                    self._he_mp_group = grp
+        return self._he_mp_group
+
+    def _kv_generate(self, input_ids, **kwargs):
+        """KV-cached (optionally tensor-parallel) generation for this framework's Llama-family models."""
+        from .. import comm as dist
+        from ..models.generation import KVCacheGenerator
+        grp = self._mp_group()
+        am = kwargs.pop("attention_mask", None)
+        if grp is not None:  # batch the group's prompts, generate once with sliced layers, keep own rows
+            tp = self.inference_tp_size
+            B = input_ids.shape[0]
+            allx = torch.empty((B * tp, ) + tuple(input_ids.shape[1:]), dtype=input_ids.dtype,
+                               device=input_ids.device)
+            dist.all_gather_into_tensor(allx, input_ids.contiguous(), group=grp)
+            if am is not None:
+                alla = torch.empty((B * tp, ) + tuple(am.shape[1:]), dtype=am.dtype, device=am.device)
+                dist.all_gather_into_tensor(alla, am.contiguous(), group=grp)
+                am = alla
+            out = KVCacheGenerator(self.module, grp).generate(allx, attention_mask=am, **kwargs)
+            r = dist.get_rank(grp)
+            return out[B * r:B * (r + 1)]
+        return KVCacheGenerator(self.module).generate(input_ids, attention_mask=am, **kwargs)
+
     @torch.no_grad()
     def generate(self, *args, **kwargs):
+        from ..models.generation import supports_kv_generation
         t0 = time.time()
         if self._training_start_time is not None:
             self._training_latency += t0 - self._training_start_time
+        if self._total_batch_size is None:
+            from .. import comm as dist
+            x = args[0] if args else kwargs.get("input_ids")
+            self._total_batch_size = x.shape[0] * (dist.get_world_size() if dist.is_initialized() else 1)
         zopt = self.optimizer
         gathered = zopt is not None and getattr(zopt, "stage", 0) == 3 and getattr(zopt, "partitioned", False)
         was_training = self.module.training
@@ -73,11 +120,19 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
         try:
             if gathered:
                 zopt.gather_all()
+            self._gather_latency = time.time() - t0
             self.fuse_lora_weight()
             if "max_new_tokens" in kwargs:
                 kwargs["max_new_tokens"] = min(kwargs["max_new_tokens"], self.max_out_tokens)
             gen = getattr(self.module, "generate", None)
-            out = gen(*args, **kwargs) if gen is not None else self._greedy(*args, **kwargs)
+            if gen is not None:
+                out = gen(*args, **kwargs)
+            elif supports_kv_generation(self.module):
+                if args:
+                    kwargs["input_ids"] = args[0]
+                out = self._kv_generate(kwargs.pop("input_ids"), **kwargs)
+            else:
+                out = self._greedy(*args, **kwargs)
             self.unfuse_lora_weight()
         finally:
             if gathered:
@@ -87,13 +142,13 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
             if self.release_inference_cache and torch.cuda.is_available():
                 torch.cuda.empty_cache()
         t1 = time.time()
-        self._generate_latency += t1 - t0
+        self._generate_latency += t1 - t0 - self._gather_latency
         self._iters += 1
         self._training_start_time = t1
         return out
 
     def _greedy(self, input_ids, max_new_tokens=16, **kwargs):
-        """Greedy decoding for models without ``.generate`` (e.g. this framework's LlamaForCausalLM)."""
+        """Greedy full-recompute decoding for models with neither ``.generate`` nor the Llama block layout."""
         ids = input_ids
         for _ in range(int(max_new_tokens)):
             logits = self.module(ids)
@@ -108,16 +163,44 @@ class DeepSpeedHybridEngine(DeepSpeedEngine):
         return super().forward(*inputs, **kwargs)
 
     def eval(self):
+        """Switch to generation mode; logs the RLHF iteration breakdown since the previous ``eval`` (reference
+        hybrid_engine.py :381-403: E2E / gather / generate / training latency and samples per second)."""
+        now = time.time()
+        if self._e2e_start is not None:
+            lat = now - self._e2e_start
+            self._total_latency += lat
+            self._eval_iters += 1
+            others = lat - (self._gather_latency + self._generate_latency + self._training_latency)
+            msg = (f"|E2E latency={lat:.2f}s |Gather latency={self._gather_latency:.2f}s "
+                   f"({100 * self._gather_latency / lat:.2f}%) |Generate time={self._generate_latency:.2f}s "
+                   f"({100 * self._generate_latency / lat:.2f}%) |Training time={self._training_latency:.2f}s "
+                   f"({100 * self._training_latency / lat:.2f}%) |Others={others:.2f} ({100 * others / lat:.2f}%)")
+            if self._total_batch_size is not None:
+                msg += (f"|CurSamplesPerSec={self._total_batch_size / lat:.2f} "
+                        f"|AvgSamplesPerSec={self._total_batch_size * self._eval_iters / self._total_latency:.2f}")
+            self.last_latency_report = msg
+            log_dist(msg, ranks=[0])
+        self._e2e_start = now
+        self._training_start_time = None
+        self._training_latency = self._generate_latency = self._gather_latency = 0.0
         self.module.eval()
         return self
 
     def train(self, mode=True):
         self.module.train(mode)
-        if mode and self._training_start_time is None:
+        if mode:
             self._training_start_time = time.time()
         return self
 
+    def step(self, *args, **kwargs):
+        out = super().step(*args, **kwargs)
+        if self._training_start_time is not None:
+            now = time.time()
+            self._training_latency += now - self._training_start_time
+            self._training_start_time = now
+        return out
+
     def latency_stats(self):
         total = time.time() - self._t_start
-        return {"generate_s": self._generate_latency, "training_s": self._training_latency, "total_s": total,
-                "generate_calls": self._iters}
+        return {"generate_s": self._generate_latency, "gather_s": self._gather_latency,
+                "training_s": self._training_latency, "total_s": total, "generate_calls": self._iters}
