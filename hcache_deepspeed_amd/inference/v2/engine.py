@@ -74,7 +74,7 @@ class InferenceEngineV2:
             model_config = spec_from_llama_config(model_config)
             weights = convert_own_llama(weights, model_config)
         self._model = RaggedTransformer(model_config, weights, device, dtype, tp_group=self._base_mp_group,
-                                        latent_mode=self._config.latent_mode)
+                                        latent_mode=self._config.latent_mode, engine_config=self._config)
         sm = self._config.state_manager
         kvc = self._model.kv_cache_config()
         self._kv = BlockedKVCache(kvc["num_layers"], kvc["n_kv_heads"], kvc["head_dim"], sm.kv_block_size, dtype,
@@ -225,9 +225,14 @@ class InferenceEngineV2:
               "lm_head.w": m.lm_head, "lm_head.b": m.lm_head_b,
               "layers": [{k: v for k, v in L.w.items() if v is not None} for L in m.layers]}
 
+        from .modules.implementations import _PackedWeight
+
         def cpu(x):
             if isinstance(x, torch.Tensor):
                 return x.cpu()
+            if isinstance(x, _PackedWeight):  # weight-only quantized: packed codes + scales + shape
+                return {"q": x.q.cpu(), "scales": x.scales.cpu(),
+                        "meta": torch.tensor([x.out_features, x.in_features, x.group_size])}
             if isinstance(x, dict):
                 return {k: cpu(v) for k, v in x.items() if v is not None}
             if isinstance(x, list):

@@ -27,12 +27,14 @@ import torch
 import torch.nn.functional as F
 
 from ... import comm as dist
-from ...ops.activations import bias_act, glu
-from ...ops.grouped_gemm import moe_ffn_dropless
-from ...ops.moe import moe_combine, moe_dispatch, topk_assign, topk_route
+from ...ops.activations import glu
 from ...ops.norm import layer_norm, rms_norm
-from ...ops.paged import build_atoms, kv_rope_scatter, paged_attention
+from ...ops.paged import build_atoms, kv_rope_scatter
 from ...ops.rope import rope_tables
+from .modules import (DSEmbeddingsConfig, DSLinearConfig, DSMoEConfig, DSNormConfig, DSSelfAttentionConfig,
+                      DSUnembedConfig, instantiate_attention, instantiate_embed, instantiate_linear, instantiate_moe,
+                      instantiate_pre_norm, instantiate_unembed)
+from .modules.implementations import _PackedWeight
 
 
 class _Layer:
@@ -47,7 +49,8 @@ class _Layer:
 class RaggedTransformer:
     """Decoder over a paged KV cache (optionally tensor-parallel), configured by an ArchSpec."""
 
-    def __init__(self, spec, weights, device, dtype=torch.bfloat16, tp_group=None, latent_mode="hidden"):
+    def __init__(self, spec, weights, device, dtype=torch.bfloat16, tp_group=None, latent_mode="hidden",
+                 engine_config=None):
         self.cfg = self.spec = spec
         self.device = device
         self.dtype = dtype
@@ -62,15 +65,52 @@ class RaggedTransformer:
         self.n_kv = spec.num_key_value_heads // self.tp
         self.d = D
         self.rot = spec.rotary_dim if 0 < spec.rotary_dim < D else D
+        self.scale = 1.0 / math.sqrt(D)
+        self._build_modules(engine_config)
         self._load(weights)
         if spec.pos == "rope":
             self.cos, self.sin = rope_tables(max(spec.max_position_embeddings, 8192), self.rot, spec.rope_theta,
                                              spec.rope_scaling, device=device)
         else:
             self.cos = self.sin = None
-        self.scale = 1.0 / math.sqrt(D)
         self.kv_cache = None
         self.copy_stream = torch.cuda.Stream(device, priority=-1) if device.type == "cuda" else None
+
+    def _build_modules(self, ec):
+        """Compute modules chosen by the inference-v2 heuristics (modules/heuristics.py): the engine config's
+        ``quantization.quantization_mode`` switches every projection to the FP6 / INT weight-only kernels."""
+        spec, D, H = self.spec, self.d, self.spec.hidden_size
+        nq, nkv = self.n_q, self.n_kv
+        norm = DSNormConfig(H, "rms" if spec.norm == "rms" else "layer", spec.norm_eps)
+        self.norm_mod = instantiate_pre_norm(norm, ec)
+        self.embed_mod = instantiate_embed(DSEmbeddingsConfig(embedding_dim=H, positional_offset=spec.pos_offset), ec)
+        self.attn_mod = instantiate_attention(
+            DSSelfAttentionConfig(nq, nkv, D, scale_factor=self.scale, rotary_dim=self.rot,
+                                  positional_embedding_type="rotate_half" if spec.pos == "rope" else "none",
+                                  sliding_window=spec.sliding_window or 0), ec)
+        self.qkv_lin = instantiate_linear(DSLinearConfig(H, (nq + 2 * nkv) * D), ec)
+        self.o_lin = instantiate_linear(DSLinearConfig(nq * D, H), ec)
+        act = self._act_name()
+        I = spec.intermediate_size // self.tp
+        if spec.moe is not None:
+            m = spec.moe
+            self.moe_mod = instantiate_moe(DSMoEConfig(H, I, int(m.get("num_experts", 0)), int(m["top_k"]),
+                                                       f"{act}_glu", bool(m["normalize"])), ec)
+        if spec.gated:
+            self.up_lin = instantiate_linear(DSLinearConfig(H, 2 * I, activation=f"{act}_glu"), ec)
+        else:
+            self.up_lin = instantiate_linear(DSLinearConfig(H, I, activation=act), ec)
+        self.down_lin = instantiate_linear(DSLinearConfig(I, H), ec)
+        self.unembed_mod = instantiate_unembed(DSUnembedConfig(model_dim=H, vocab_size=spec.vocab_size,
+                                                               norm_type="rms" if spec.norm == "rms" else "layer"), ec)
+
+    def _transform(self, L):
+        """Per-implementation weight layout (quantization happens here, once, on the device)."""
+        w = L.w
+        for key, mod in (("qkv.w", self.qkv_lin), ("o.w", self.o_lin), ("up.w", self.up_lin),
+                         ("down.w", self.down_lin)):
+            if w.get(key) is not None:
+                w[key] = mod.transform_param(w[key])
 
     # ------------------------------------------------------------------------------------------
     # weights: canonical dict (arch.convert_*) -> this rank's shards
@@ -150,6 +190,7 @@ class RaggedTransformer:
                     w["up.b"] = t(self._gated_rows(ub[:, None])[:, 0] if self.spec.gated else self._rows(ub))
                 w["down.w"] = t(self._cols(Ls["down.w"]))
                 w["down.b"] = t(Ls.get("down.b")) if r == 0 else None
+            self._transform(L)
             self.layers.append(L)
 
     def _load_presharded(self, sd):
@@ -161,7 +202,9 @@ class RaggedTransformer:
         self.layers = []
         for Ls in sd["layers"]:
             L = _Layer()
-            L.w = {k: t(v) for k, v in Ls.items()}
+            L.w = {k: (_PackedWeight(v["q"].to(self.device), v["scales"].to(self.device), *[int(i) for i in v["meta"]])
+                       if isinstance(v, dict) else t(v)) for k, v in Ls.items()}
+            self._transform(L)
             self.layers.append(L)
 
     # ------------------------------------------------------------------------------------------
@@ -177,10 +220,11 @@ class RaggedTransformer:
         return x
 
     def _norm(self, x, w, b, residual=None):
-        eps = self.spec.norm_eps
-        if self.spec.norm == "rms":
-            return rms_norm(x, w, eps, residual) if residual is not None else rms_norm(x, w, eps)
-        return layer_norm(x, w, b, eps, residual) if residual is not None else layer_norm(x, w, b, eps)
+        """norm(x) or the fused (norm(x + residual), x + residual) through the registered pre-norm module."""
+        if residual is None:
+            return self.norm_mod(x, None, w, b)[1]
+        r, y = self.norm_mod(residual, x, w, b)
+        return y, r
 
     def _act_name(self):
         a = self.spec.act
@@ -189,40 +233,15 @@ class RaggedTransformer:
     def _mlp(self, L, x):
         if L["w13"] is not None:
             return self._moe(L, x)
-        if self.spec.gated:
-            h = F.linear(x, L["up.w"], L["up.b"])
-            return F.linear(glu(h, self._act_name()), L["down.w"], L["down.b"])
-        h = bias_act(F.linear(x, L["up.w"]), L["up.b"], self._act_name())
-        return F.linear(h, L["down.w"], L["down.b"])
+        return self.down_lin(self.up_lin(x, L["up.w"], L["up.b"]), L["down.w"], L["down.b"])
 
     def _moe(self, L, x):
-        """Inference top-k MoE (no token dropping). On the GPU: sync-free routing + two grouped GEMMs over the
-        expert-contiguous rows (ops/grouped_gemm.py, HIP kernel). Elsewhere: capacity slots + batched GEMMs."""
-        m = self.spec.moe
-        T, H = x.shape
-        logits = F.linear(x.float(), L["router.w"].float())
-        E = logits.shape[-1]
-        w13, w2 = L["w13"], L["w2"]
-        if x.is_cuda and x.dtype == torch.bfloat16 and H % 128 == 0 and w2.shape[2] % 128 == 0:
-            # dropless grouped-GEMM path: routing stays on the device (no capacity = max(count) sync)
-            expert, pos, w, counts = topk_assign(logits, m["top_k"], normalize=m["normalize"])
-            out = moe_ffn_dropless(x, expert, pos, w, counts, w13, w2, lambda h: glu(h, self._act_name()))
-        else:
-            out = self._moe_bmm(x, logits, m, E, H, w13, w2)
+        out = self.moe_mod(x, L["router.w"], L["w13"], L["w2"])
         if L["shared.w13"] is not None:
             s = F.linear(glu(F.linear(x, L["shared.w13"]), self._act_name()), L["shared.w2"])
             gate = torch.sigmoid(F.linear(x.float(), L["shared_gate.w"].float())).to(s.dtype)
             out = out + gate * s
         return out
-
-    def _moe_bmm(self, x, logits, m, E, H, w13, w2):
-        """Capacity formulation: dispatch into [E, max(count), H] slots and batched expert GEMMs."""
-        expert, pos, w, C, _, _ = topk_route(logits, m["top_k"], 1.0, 1, drop_tokens=False, use_rts=False,
-                                             normalize=m["normalize"], training=False)
-        disp = moe_dispatch(x, expert, pos, E, C).view(E, C, H)
-        h = torch.bmm(disp, w13.transpose(1, 2))
-        y = torch.bmm(glu(h.reshape(E * C, -1), self._act_name()).view(E, C, -1), w2.transpose(1, 2))
-        return moe_combine(y.reshape(E * C, H), expert, pos, w, C)
 
     def _prep(self, batch):
         atoms, n_atoms = build_atoms(batch.seq_meta_host, self.n_q, self.n_kv)
@@ -230,22 +249,15 @@ class RaggedTransformer:
         batch.n_atoms = n_atoms
 
     def _embed(self, batch):
-        h = F.embedding(batch.input_ids, self.embed)
-        if self.pos_embed is not None:
-            h = h + F.embedding(batch.tok_pos.long() + self.spec.pos_offset, self.pos_embed)
-        return h
+        return self.embed_mod(batch, self.embed, self.pos_embed)
 
     def _attn(self, i, L, x, batch, T, capture, lat, events):
         nq, nkv, D = self.n_q, self.n_kv, self.d
-        qkv = F.linear(x, L["qkv.w"], L["qkv.b"]).view(T, nq + 2 * nkv, D)
+        qkv = self.qkv_lin(x, L["qkv.w"], L["qkv.b"]).view(T, nq + 2 * nkv, D)
         if capture and self.latent_mode == "kv":
             self._d2h(qkv[:, nq:].reshape(T, -1).clone(), lat[i], events)  # pre-RoPE K|V
-        cache = self.kv_cache.get_cache(i)
-        kv_rope_scatter(qkv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, nq, nkv,
-                        do_rope=self.cos is not None, rotary_dim=self.rot)
-        o = paged_attention(qkv[:, :nq], cache, batch.atoms, batch.n_atoms, batch.seq_meta, batch.block_tables, nq,
-                            nkv, self.scale, self.spec.sliding_window, batch.seq_meta_host, batch.tables_host)
-        return F.linear(o.reshape(T, nq * D), L["o.w"], L["o.b"])
+        o = self.attn_mod(qkv, self.kv_cache.get_cache(i), batch, self.cos, self.sin)
+        return self.o_lin(o, L["o.w"], L["o.b"])
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -279,16 +291,8 @@ class RaggedTransformer:
             else:
                 x2, residual = self._norm(self._allreduce(a), L["ln2.w"], L["ln2.b"], residual)
                 h = self._allreduce(self._mlp(L, x2))
-        idx = batch.last_token_idx
-        if self.final_w is not None:
-            hl, _ = self._norm(h[idx], self.final_w, self.final_b, residual[idx])
-        else:
-            hl = h[idx] + residual[idx]
-        logits = F.linear(hl, self.lm_head, self.lm_head_b)
-        if self.tp > 1:
-            parts = [torch.empty_like(logits) for _ in range(self.tp)]
-            dist.all_gather(parts, logits, group=self.tp_group)
-            logits = torch.cat(parts, -1)[:, :self.vocab]
+        logits = self.unembed_mod(h, residual, batch, self.lm_head, self.lm_head_b, self.final_w, self.final_b,
+                                  spec.norm_eps, self.tp_group, self.vocab)
         if events:
             events[-1].synchronize()
         return logits, lat
@@ -359,9 +363,12 @@ class RaggedTransformer:
         cache = self.kv_cache.get_cache(i)
         if self.latent_mode == "hidden":
             # only the K|V rows of the projection are needed: GEMM against the k/v slice of W_qkv
-            w = L["qkv.w"][nq * D:]
-            bias = L["qkv.b"][nq * D:] if L["qkv.b"] is not None else None
-            kv = F.linear(x, w, bias).view(T, 2 * nkv, D)
+            if isinstance(L["qkv.w"], _PackedWeight):  # packed rows cannot be sliced: full projection
+                kv = self.qkv_lin(x, L["qkv.w"], L["qkv.b"]).view(T, nq + 2 * nkv, D)[:, nq:].contiguous()
+            else:
+                w = L["qkv.w"][nq * D:]
+                bias = L["qkv.b"][nq * D:] if L["qkv.b"] is not None else None
+                kv = F.linear(x, w, bias).view(T, 2 * nkv, D)
         else:
             kv = x.view(T, 2 * nkv, D).contiguous()  # stored pre-RoPE: rotation happens on the way in
         kv_rope_scatter(kv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, 0, nkv,
