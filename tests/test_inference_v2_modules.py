@@ -121,10 +121,10 @@ def test_quantized_engine_gpu(mode, tol):
     if mode:
         cfg["quantization"] = {"quantization_mode": mode}
     eng = build_engine_from_model(m, cfg, device=dev, num_kv_blocks=8)
-    lg, _ = eng.put([1], [ids.to(dev)])
+    lg, _ = eng.put([1], [ids])
     outs = [lg[0].float().cpu()]
     for j in range(3):
-        lg, _ = eng.put([1], [ids[j:j + 1].to(dev)], capture_latents=False)
+        lg, _ = eng.put([1], [ids[j:j + 1]], capture_latents=False)
         outs.append(lg[0].float().cpu())
     want = full[[39, 40, 41, 42]]
     err = (torch.stack(outs) - want).norm() / want.norm()
