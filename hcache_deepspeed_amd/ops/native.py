@@ -60,6 +60,9 @@ _KERNEL_SIGS = {
     "hds_quant_minifloat": "i" + "ppp" + "l" + "iiiii" + "s",
     "hds_dequant_minifloat": "i" + "ppp" + "l" + "iii" + "s",
     "hds_fp6_gemv": "pppp" + "iiiiii" + "s",
+    "hds_wmix_splits": "iii",
+    "hds_wmix_supported": "iiii",
+    "hds_wmix_gemm": "pppppp" + "iiiiii" + "s",
     "hds_token_gather": "i" + "ppp" + "iiii" + "s",
     "hds_token_scatter": "i" + "ppp" + "iiii" + "s",
     "hds_token_sort": "p" + "ii" + "s",

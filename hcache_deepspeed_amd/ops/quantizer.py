@@ -137,6 +137,32 @@ def dequant_reduce(q, scales, world, n, group_size=512, bits=8, out=None, accumu
 _INT_GEMV_MAX_M = min(8, int(os.environ.get("HDS_INT_GEMV_MAX_M", "2")))
 
 
+_WMIX_MAX_M = int(os.environ.get("HDS_WMIX_MAX_M", "256"))
+
+
+def wmix_eligible(x2, out_features, in_features, group_size):
+    M = x2.shape[0]
+    return (native.use_native(x2) and x2.dtype == torch.bfloat16 and 0 < M <= _WMIX_MAX_M
+            and bool(native.kernels().hds_wmix_supported(M, out_features, in_features, group_size)))
+
+
+def wmix_gemm(x2, q_weight, scales, out_features, in_features, group_size, fmt, ebits=3, bias=None):
+    """Mixed-input MFMA GEMM (csrc/kernels/wmix_gemm.hip): bf16 [M, K] x packed weight [N, K] -> bf16 [M, N].
+    fmt: "int8" | "int4" | "fp6". The packed weight is decoded in registers; it never exists in bf16 in HBM."""
+    M = x2.shape[0]
+    x2 = x2.contiguous()
+    lib = native.kernels()
+    splits = lib.hds_wmix_splits(M, out_features, in_features)
+    y = torch.empty(M, out_features, dtype=torch.bfloat16, device=x2.device)
+    ws = torch.empty(splits, M, out_features, dtype=torch.float32, device=x2.device) if splits > 1 else None
+    if bias is not None:
+        bias = bias.to(torch.bfloat16).contiguous()
+    native.check(lib.hds_wmix_gemm(x2.data_ptr(), q_weight.data_ptr(), scales.data_ptr(), native.ptr(bias),
+                                   y.data_ptr(), native.ptr(ws), M, out_features, in_features, group_size,
+                                   {"int8": 0, "int4": 1, "fp6": 2}[fmt], int(ebits), native.stream()), "wmix_gemm")
+    return y
+
+
 def int_linear(x, q_weight, scales, out_features, in_features, group_size, bits=8, bias=None):
     """y = x @ dequant(W)^T for a symmetric group-quantized int8/int4 weight [out, in] (groups along ``in``).
 
@@ -155,6 +181,9 @@ def int_linear(x, q_weight, scales, out_features, in_features, group_size, bits=
                                                    native.stream()), "int_gemv")
         y = y.view(*lead, out_features)
         return y if bias is None else y + bias
+    if wmix_eligible(x2, out_features, in_features, group_size):  # batched decode / chunked prefill: MFMA
+        return wmix_gemm(x2, q_weight, scales, out_features, in_features, group_size, f"int{bits}",
+                         bias=bias).view(*lead, out_features)
     w = dequantize(q_weight, scales, None, group_size, bits, True, x.dtype).view(out_features, in_features)
     return torch.nn.functional.linear(x, w, bias)
 
@@ -397,5 +426,8 @@ def fp6_linear(x, q_weight, scales, out_features, in_features, group_size, manti
                                                    y.data_ptr(), M, out_features, in_features, group_size,
                                                    5 - mantissa_bits, mantissa_bits, native.stream()), "fp6_gemv")
         return y.view(*lead, out_features)
+    if wmix_eligible(x2, out_features, in_features, group_size):  # batched decode / chunked prefill: MFMA
+        return wmix_gemm(x2, q_weight, scales, out_features, in_features, group_size, "fp6",
+                         5 - mantissa_bits).view(*lead, out_features)
     w = dequantize_minifloat(q_weight, scales, group_size, 6, mantissa_bits, x.dtype).view(out_features, in_features)
     return torch.nn.functional.linear(x, w)
