@@ -96,20 +96,19 @@ __device__ __forceinline__ bf16x8 frag(const WRaw<FMT>& r, int j, float s) {
   return out;
 }
 
-constexpr int kNF = 4;                 // 32-row weight fragments per wave
-constexpr int kBN = 4 * 32 * kNF;      // weight rows per workgroup (4 waves)
 constexpr int kArow = 144;             // LDS bytes per A row of a 64-k chunk (128 + 16 pad: conflict-free b128 reads)
 
-template <int FMT, int MB, int E>
+template <int FMT, int MB, int E, int kNF>
 __global__ __launch_bounds__(256) void wmix_gemm_kernel(const bf16* __restrict__ A, const uint8_t* __restrict__ W,
                                                         const float* __restrict__ scales,
                                                         const bf16* __restrict__ bias, bf16* __restrict__ C,
                                                         float* __restrict__ part, int M, int N, int K, int G,
                                                         int kc) {
   constexpr int BM = 32 * MB;
+  constexpr int kBN = 4 * 32 * kNF;  // weight rows per workgroup
   __shared__ __attribute__((aligned(16))) char As[2][BM * kArow];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  const int nb = blockIdx.x * kBN + 128 * w + (lane & 31);  // row of fragment f: nb + 32 f
+  const int nb = blockIdx.x * kBN + 32 * kNF * w + (lane & 31);  // row of fragment f: nb + 32 f
   const int m0 = blockIdx.y * BM;
   const int k_begin = blockIdx.z * kc, k_end = min(K, k_begin + kc);
   int nr[kNF];
@@ -223,13 +222,16 @@ __global__ __launch_bounds__(256) void wmix_reduce_kernel(const float* __restric
   *reinterpret_cast<bf16x4*>(C + i) = o;
 }
 
-int pick_mb(int M) { return M <= 64 ? 1 : 2; }
+int pick_mb(int M) { return M <= 32 ? 1 : 2; }
+// weight fragments per wave: 1 at small M (more workgroups in flight for the weight stream), 4 once the A chunk
+// re-reads and the per-fragment MFMA chain matter (measured, profiles/wmix_bench_r2.log)
+int pick_nf(int M) { return M <= 64 ? 1 : 4; }
 
 }  // namespace
 
 // number of K splits (grid.z) for a problem; the caller provides an fp32 workspace of splits * M * N when > 1
 HDS_EXPORT int hds_wmix_splits(int M, int N, int K) {
-  const int mb = pick_mb(M);
+  const int mb = pick_mb(M), kBN = 128 * pick_nf(M);
   const int base = ((N + kBN - 1) / kBN) * ((M + 32 * mb - 1) / (32 * mb));
   int splits = (512 + base - 1) / base;
   const int max_splits = K / 256 > 1 ? K / 256 : 1;  // >= 4 chunks of 64 k per split
@@ -252,23 +254,25 @@ HDS_EXPORT int hds_wmix_gemm(const void* A, const void* W, const float* scales, 
   const int splits = hds_wmix_splits(M, N, K);
   if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
   const int kc = ((K / 64 + splits - 1) / splits) * 64;
-  const int mb = pick_mb(M);
+  const int mb = pick_mb(M), nf = pick_nf(M), kBN = 128 * nf;
   dim3 grid((N + kBN - 1) / kBN, (M + 32 * mb - 1) / (32 * mb), splits);
   float* part = splits > 1 ? ws : nullptr;
-#define HDS_WMIX(F, MB, E)                                                                                         \
-  hipLaunchKernelGGL((wmix_gemm_kernel<F, MB, E>), grid, dim3(256), 0, st, (const bf16*)A, (const uint8_t*)W,       \
-                     scales, (const bf16*)bias, (bf16*)C, part, M, N, K, G, kc)
-#define HDS_WMIX_MB(F, E)           \
-  do {                              \
-    if (mb == 1) HDS_WMIX(F, 1, E); \
-    else HDS_WMIX(F, 2, E);         \
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, (const bf16*)A, (const uint8_t*)W, scales, (const bf16*)bias,
+                       (bf16*)C, part, M, N, K, G, kc);
+  };
+#define HDS_WMIX(F, E)                                                 \
+  do {                                                                 \
+    if (mb == 1 && nf == 1) launch(wmix_gemm_kernel<F, 1, E, 1>);      \
+    else if (mb == 1) launch(wmix_gemm_kernel<F, 1, E, 4>);            \
+    else if (nf == 1) launch(wmix_gemm_kernel<F, 2, E, 1>);            \
+    else launch(wmix_gemm_kernel<F, 2, E, 4>);                         \
   } while (0)
-  if (fmt == 0) HDS_WMIX_MB(kInt8, 0);
-  else if (fmt == 1) HDS_WMIX_MB(kInt4, 0);
-  else if (fmt == 2 && ebits == 3) HDS_WMIX_MB(kFp6, 3);
-  else if (fmt == 2 && ebits == 2) HDS_WMIX_MB(kFp6, 2);
+  if (fmt == 0) HDS_WMIX(kInt8, 0);
+  else if (fmt == 1) HDS_WMIX(kInt4, 0);
+  else if (fmt == 2 && ebits == 3) HDS_WMIX(kFp6, 3);
+  else if (fmt == 2 && ebits == 2) HDS_WMIX(kFp6, 2);
   else return hipErrorInvalidValue;
-#undef HDS_WMIX_MB
 #undef HDS_WMIX
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || splits == 1) return e;

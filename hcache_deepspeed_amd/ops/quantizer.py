@@ -137,7 +137,8 @@ def dequant_reduce(q, scales, world, n, group_size=512, bits=8, out=None, accumu
 _INT_GEMV_MAX_M = min(8, int(os.environ.get("HDS_INT_GEMV_MAX_M", "2")))
 
 
-_WMIX_MAX_M = int(os.environ.get("HDS_WMIX_MAX_M", "256"))
+# above 64 rows dequantize-once + hipBLASLt wins on most shapes (profiles/wmix_bench_r2.log)
+_WMIX_MAX_M = int(os.environ.get("HDS_WMIX_MAX_M", "64"))
 
 
 def wmix_eligible(x2, out_features, in_features, group_size):
