@@ -3,7 +3,8 @@
 Reads ``*counter_collection.csv`` (per-dispatch counters) and ``*kernel_trace.csv`` (start/end), joins them on the
 dispatch id and prints, per kernel name: calls, GPU time, achieved bf16 matrix FLOP/s from SQ_INSTS_VALU_MFMA_MOPS_BF16
 (MOPS are counted in units of 512 FLOPs) against the 2.5 PF/s dense peak, and the MFMA-busy fraction
-SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CU_CYCLES) when both were collected.
+SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs x SQ_BUSY_CU_CYCLES) when both were collected (per-SIMD MFMA-busy share of the
+cycles the CUs were busy).
 
 Usage: python tools/pmc_summary.py <rocprof output dir> [out.csv]
 """
@@ -48,7 +49,7 @@ def main(d, out=None):
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
         cu = c.get("SQ_BUSY_CU_CYCLES")
         rows.append((name, int(c["_calls"]), ns / 1e6, flops / (ns * 1e-9) if ns else 0.0,
-                     (busy / cu) if busy and cu else None))
+                     (busy / (4 * cu)) if busy and cu else None))
     rows.sort(key=lambda r: -r[2])
     tot_ms = sum(r[2] for r in rows)
     tot_fl = sum(r[3] * r[2] * 1e-3 for r in rows)
