@@ -13,6 +13,7 @@ HF checkpoint names (q_proj/k_proj/v_proj, gate_proj/up_proj) are converted by
 ``deepspeed.initialize`` and inference/v2/model_implementations/llama_v2 (serving).
 """
 import math
+import os
 from dataclasses import asdict, dataclass, field
 from typing import Optional
 
@@ -282,7 +283,9 @@ class LlamaForCausalLM(nn.Module):
         self.lm_head = _Linear(cfg.hidden_size, cfg.vocab_size, std=cfg.initializer_range)
         if cfg.tie_word_embeddings:
             self.lm_head.weight = self.model.embed_tokens.weight
-        self.ce_chunk_rows = 4096
+        # LM-head + CE row chunk: each chunk costs one fp32 read-modify-write of the [V, H] weight-gradient
+        # accumulator, so fewer, larger chunks trade ~V*2 bytes of logits per extra row for less HBM traffic
+        self.ce_chunk_rows = int(os.environ.get("HDS_CE_CHUNK_ROWS", "4096"))
 
     def gradient_checkpointing_enable(self):
         self.model.gradient_checkpointing = True

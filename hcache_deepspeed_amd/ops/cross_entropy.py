@@ -118,8 +118,8 @@ class _FusedLinearCEFn(torch.autograd.Function):
         t = target.reshape(-1).to(torch.int64).contiguous()
         losses = torch.empty(T, device=hidden.device, dtype=torch.float32)
         dh = torch.empty_like(hidden) if (need_grad and hidden.requires_grad) else None
-        dw = torch.zeros(V, H, device=hidden.device, dtype=torch.float32) if (need_grad and weight.requires_grad) \
-            else None
+        want_dw = need_grad and weight.requires_grad
+        dw = None  # fp32 accumulator: the first chunk's GEMM writes it (beta = 0), no zero-fill pass
         native_path = native.use_native(hidden)
         for s in range(0, T, chunk_rows):
             e = min(T, s + chunk_rows)
@@ -141,8 +141,11 @@ class _FusedLinearCEFn(torch.autograd.Function):
             if need_grad:
                 if dh is not None:
                     torch.mm(dl, weight, out=dh[s:e])
-                if dw is not None:
-                    _addmm_f32_(dw, dl.t(), hc)
+                if want_dw:
+                    if dw is None:
+                        dw = _mm_f32(dl.t(), hc)
+                    else:
+                        _addmm_f32_(dw, dl.t(), hc)
             del logits
         ctx.save_for_backward(dh, dw)
         ctx.wdtype = weight.dtype
