@@ -142,7 +142,13 @@ class _FusedLinearCEFn(torch.autograd.Function):
                 if dh is not None:
                     torch.mm(dl, weight, out=dh[s:e])
                 if want_dw:
-                    if dw is None:
+                    if dl.is_cuda and _ADDMM_OUT_DTYPE[0] is not False and (
+                            _ADDMM_OUT_DTYPE[0] or _probe_addmm_out_dtype(dl.device)):
+                        from .gemm import wgrad  # fp32 accumulator, layout chosen per shape (TN or NT)
+                        if dw is None:
+                            dw = torch.empty(V, H, device=hidden.device, dtype=torch.float32)
+                        wgrad(dl, hc, dw, accumulate=s > 0)
+                    elif dw is None:
                         dw = _mm_f32(dl.t(), hc)
                     else:
                         _addmm_f32_(dw, dl.t(), hc)

@@ -4,6 +4,8 @@
 with bf16 operands and fp32 accumulation, optionally scaled and accumulated into ``out``. Shapes outside
 the kernel's tiling (M, N multiples of 256, K a multiple of 128) go to ``torch.matmul`` (hipBLASLt).
 """
+import os
+
 import torch
 
 from . import native
@@ -50,4 +52,74 @@ def gemm_nt(a, b, out=None, alpha=1.0, accumulate=False, variant=None):
                                               b.stride(0), out.stride(0), float(alpha), int(bool(accumulate)),
                                               VARIANT if variant is None else int(variant), native.stream()),
                  "gemm_nt")
+    return out
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# weight-gradient GEMM layout: dW[N, K] (+)= dY[T, N]^T X[T, K]
+# ----------------------------------------------------------------------------------------------------------------
+def transpose2d(x):
+    """[R, C] (unit last stride) -> contiguous [C, R]; HIP LDS-tiled kernel for bf16 on the GPU."""
+    R, C = x.shape
+    if not (native.use_native(x) and x.dtype == torch.bfloat16 and x.stride(1) == 1 and R % 8 == 0
+            and x.stride(0) % 8 == 0):
+        return x.t().contiguous()
+    out = torch.empty(C, R, dtype=x.dtype, device=x.device)
+    native.check(native.kernels().hds_transpose_bf16(x.data_ptr(), out.data_ptr(), R, C, x.stride(0),
+                                                     native.stream()), "transpose_bf16")
+    return out
+
+
+_WGRAD_LAYOUT = os.environ.get("HDS_WGRAD_LAYOUT", "auto")  # auto | direct | nt
+_WGRAD_CHOICE = {}
+
+
+def _wgrad_run(layout, dy2, x2, out, accumulate):
+    if layout == "nt":  # hipBLASLt's NT form on transposed copies (the forward GEMM's fast layout)
+        a, b = transpose2d(dy2), transpose2d(x2)
+        bt = b.t()
+    else:
+        a, bt = dy2.t(), x2
+    if out.dtype == a.dtype:
+        if accumulate:
+            out.addmm_(a, bt)
+        else:
+            torch.mm(a, bt, out=out)
+    else:  # fp32 accumulator from bf16 operands
+        if accumulate:
+            torch.addmm(out, a, bt, out_dtype=out.dtype, out=out)
+        else:
+            torch.mm(a, bt, out_dtype=out.dtype, out=out)
+
+
+def _time_layout(layout, dy2, x2, out, accumulate):
+    scratch = torch.zeros_like(out)
+    _wgrad_run(layout, dy2, x2, scratch, accumulate)  # warm (hipBLASLt solution lookup, allocator)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _wgrad_run(layout, dy2, x2, scratch, accumulate)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def wgrad(dy2, x2, out, accumulate=False):
+    """out[N, K] (+)= dy2[T, N]^T @ x2[T, K] with the faster of two layouts for this shape: the TN GEMM autograd
+    issues (``direct``) or two HBM-rate HIP transposes + the NT GEMM (``nt``). ``HDS_WGRAD_LAYOUT=auto`` times both
+    once per (shape, dtype, accumulate) on the first call (profiles/wgrad_layout_r2.log: NT runs 1.44-1.47 PF/s
+    where TN runs 0.94-1.10 at the o / gate_up shapes, and no faster at qkv / down)."""
+    layout = _WGRAD_LAYOUT
+    if layout == "auto":
+        if not (dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+                and dy2.stride(1) == 1 and x2.stride(1) == 1):
+            layout = "direct"
+        else:
+            key = (tuple(dy2.shape), tuple(x2.shape), out.dtype, bool(accumulate))
+            layout = _WGRAD_CHOICE.get(key)
+            if layout is None:
+                td = _time_layout("direct", dy2, x2, out, accumulate)
+                tn = _time_layout("nt", dy2, x2, out, accumulate)
+                layout = "nt" if tn < 0.97 * td else "direct"
+                _WGRAD_CHOICE[key] = layout
+    _wgrad_run(layout, dy2, x2, out, accumulate)
     return out

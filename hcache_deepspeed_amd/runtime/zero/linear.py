@@ -83,10 +83,8 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
             x2 = x.reshape(-1, x.shape[-1]).to(dy.dtype)
 
             def gemm(out, accumulate):
-                if accumulate:
-                    out.addmm_(dy2.t(), x2)
-                else:
-                    torch.mm(dy2.t(), x2, out=out)
+                from ...ops.gemm import wgrad
+                wgrad(dy2, x2, out, accumulate)
 
             if not write_weight_grad(w, gemm):
                 dw = dy2.t().matmul(x2)
