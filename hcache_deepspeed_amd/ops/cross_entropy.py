@@ -140,7 +140,11 @@ class _FusedLinearCEFn(torch.autograd.Function):
             losses[s:e] = loss_c
             if need_grad:
                 if dh is not None:
-                    torch.mm(dl, weight, out=dh[s:e])
+                    if dl.is_cuda:
+                        from .gemm import dgrad
+                        dgrad(dl, weight, out=dh[s:e])
+                    else:
+                        torch.mm(dl, weight, out=dh[s:e])
                 if want_dw:
                     if dl.is_cuda and _ADDMM_OUT_DTYPE[0] is not False and (
                             _ADDMM_OUT_DTYPE[0] or _probe_addmm_out_dtype(dl.device)):

@@ -123,3 +123,44 @@ def wgrad(dy2, x2, out, accumulate=False):
                 _WGRAD_CHOICE[key] = layout
     _wgrad_run(layout, dy2, x2, out, accumulate)
     return out
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# input-gradient GEMM layout: dX[T, K] = dY[T, N] W[N, K]
+# ----------------------------------------------------------------------------------------------------------------
+_DGRAD_LAYOUT = os.environ.get("HDS_DGRAD_LAYOUT", "auto")  # auto | direct | nt
+_DGRAD_CHOICE = {}
+
+
+def _dgrad_run(layout, dy2, w, out):
+    b = transpose2d(w).t() if layout == "nt" else w  # nt: dY @ (W^T)^T, hipBLASLt's NT form
+    if out is None:
+        return torch.mm(dy2, b)
+    return torch.mm(dy2, b, out=out)
+
+
+def dgrad(dy2, w, out=None):
+    """dy2[T, N] @ w[N, K] with the faster of the NN GEMM autograd issues and a HIP transpose of the (small) weight +
+    the NT GEMM, timed once per shape under ``HDS_DGRAD_LAYOUT=auto`` (the NT form ran 1.51-1.59 PF/s against
+    1.32-1.39 for NN at the bench shapes, profiles/gemm_layouts_r1.log)."""
+    layout = _DGRAD_LAYOUT
+    if layout == "auto":
+        if not (dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy2.stride(1) == 1
+                and w.stride(1) == 1):
+            layout = "direct"
+        else:
+            key = (tuple(dy2.shape), tuple(w.shape))
+            layout = _DGRAD_CHOICE.get(key)
+            if layout is None:
+                times = {}
+                for cand in ("direct", "nt"):
+                    _dgrad_run(cand, dy2, w, None)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    _dgrad_run(cand, dy2, w, None)
+                    e1.record()
+                    e1.synchronize()
+                    times[cand] = e0.elapsed_time(e1)
+                layout = "nt" if times["nt"] < 0.97 * times["direct"] else "direct"
+                _DGRAD_CHOICE[key] = layout
+    return _dgrad_run(layout, dy2, w, out)

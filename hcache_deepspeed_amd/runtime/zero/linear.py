@@ -77,7 +77,11 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
         w = ctx.weight
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = dy.matmul(w.to(dy.dtype))
+            if dy.is_cuda and dy.dim() >= 2 and w.dtype == dy.dtype:
+                from ...ops.gemm import dgrad
+                dx = dgrad(dy.reshape(-1, dy.shape[-1]), w).view(*dy.shape[:-1], w.shape[1])
+            else:
+                dx = dy.matmul(w.to(dy.dtype))
         if ctx.needs_input_grad[1]:
             dy2 = dy.reshape(-1, dy.shape[-1])
             x2 = x.reshape(-1, x.shape[-1]).to(dy.dtype)

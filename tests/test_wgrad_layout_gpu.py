@@ -27,3 +27,18 @@ def test_wgrad_layouts_match(layout, out_dtype, monkeypatch):
     gemm.wgrad(dy, x, out, accumulate=True)
     err = (out.float() - 2 * ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item() * 2, err
+
+
+@pytest.mark.parametrize("layout", ["direct", "nt", "auto"])
+def test_dgrad_layouts_match(layout, monkeypatch):
+    from hcache_deepspeed_amd.ops import gemm
+    monkeypatch.setattr(gemm, "_DGRAD_LAYOUT", layout)
+    torch.manual_seed(0)
+    dy = torch.randn(1024, 768, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(768, 512, device="cuda", dtype=torch.bfloat16)
+    ref = dy.float() @ w.float()
+    got = gemm.dgrad(dy, w)
+    assert (got.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    out = torch.empty(1024, 512, device="cuda", dtype=torch.bfloat16)
+    gemm.dgrad(dy, w, out=out)
+    assert torch.equal(out, got)
