@@ -59,6 +59,10 @@ def main():
     ap.add_argument("--nvme-path", default="/tmp/hds_nvme", help="swap folder of the NVMe tier (--offload nvme)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
     args = ap.parse_args()
+    if os.environ.get("HDS_HANG_DUMP"):
+        # diagnosis of a stuck run: every N seconds print the Python stacks of all threads to stderr
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["HDS_HANG_DUMP"]), repeat=True)
     tuned = _use_tuned_gemms()
 
     import torch

@@ -22,6 +22,11 @@ already a runtime mechanism of the engine, driven by the module-execution trace 
   * double_buffer / symmetric_memory            -> RCCL reduce-scatter buckets are already double-buffered per
     unit; symmetric memory has no RCCL analogue here and is ignored with a warning.
 
+The gather schedule itself is compiled (hcache_deepspeed_amd/compile/): with ``deepcompile`` at ZeRO-3 a
+``DeepCompileBackend`` profiles one step of the unit trace (HIP-event timestamps, live HBM bytes), measures an
+RCCL all-gather cost model, and runs the selective-gather and prefetch passes; the resulting
+``CompiledSchedule`` replaces the depth-bounded prefetch from the next step on.
+
 ``compile()`` therefore validates the configuration, switches those mechanisms on and records per-pass setup
 times (``get_compile_time``). User passes registered with ``register_compile_pass`` are called once with the
 engine (they may adjust knobs such as the prefetch depth).
@@ -83,6 +88,18 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
     if cfg.offload_parameters and not engine._config.zero_config.offload_param.enabled:
         logger.warning("compile: offload_parameters requires zero_optimization.offload_param at initialize(); "
                        "parameters stay on device")
+    if cfg.deepcompile and engine.zero_optimization_stage() == 3:
+        # profile-guided gather schedule (compile/backend.py): profiled on a later step, then installed
+        from ..compile import DeepCompileBackend
+        t0 = time.perf_counter()
+        kw = dict(compile_kwargs or {})
+        engine._dc_backend = DeepCompileBackend(
+            engine, profile_step=kw.get("profile_step", 1), margin=kw.get("mem_margin", 0.1),
+            mem_budget_bytes=kw.get("mem_budget_bytes"), max_buffered_bytes=kw.get("max_buffered_bytes"),
+            selective_gather=kw.get("selective_gather", True), comm_sizes=kw.get("comm_sizes"))
+        times["zero3_compile"] = time.perf_counter() - t0
+    elif cfg.deepcompile:
+        times["zero1_compile"] = 0.0
     t0 = time.perf_counter()
     if cfg.native_comm and engine.optimizer is not None and hasattr(engine.optimizer, "enable_native_comm"):
         # DeepCompile's private-communicator path (reference csrc/compile/deepcompile.cpp): ZeRO all-gathers and

@@ -450,6 +450,8 @@ class DeepSpeedEngine(nn.Module):
                 self.monitor.write_events([("Train/Samples/lr", self.get_lr()[0], self.global_samples)])
             if self.global_steps % self.steps_per_print() == 0 and self.wall_clock_breakdown():
                 self.timers.log([FORWARD_MICRO_TIMER, BACKWARD_MICRO_TIMER, STEP_MICRO_TIMER])
+        if boundary and getattr(self, "_dc_backend", None) is not None:
+            self._dc_backend.on_step_end()
         if boundary and getattr(self, "_dc_offload_opt_states", False):
             self.offload_states(include=["optim_states"], non_blocking=True)
             self._dc_states_offloaded = True

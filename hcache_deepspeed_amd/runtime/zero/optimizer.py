@@ -289,6 +289,10 @@ class ZeroOptimizer:
         self.max_reuse_distance = (int(self.zcfg.max_reuse_distance)
                                    if _explicit("stage3_max_reuse_distance", "max_reuse_distance") else None)
         self._reuse_keep = set()
+        # DeepCompile (compile/backend.py): a profiling probe and the compiled gather schedule, when installed
+        self.dc_probe = None
+        self.dc_schedule = None
+        self.ag_issued = 0  # all-gathers issued (test / profiling counter)
         self.pending_rs = []  # ZeRO-3 partitioned-unit reduce-scatters: bounded by max_reduce_inflight
         self.track_live = os.environ.get("HDS_ZERO_TRACK_LIVE", "0") == "1"
         self.live_peak_bytes = 0
@@ -864,6 +868,7 @@ class ZeroOptimizer:
             u.full = full
             u.bind_params(full)
             u.status = INFLIGHT
+            self.ag_issued += 1
             self._note_live()
         if wait and u.status == INFLIGHT:
             u.work.wait()
@@ -906,7 +911,12 @@ class ZeroOptimizer:
             return
         t = self._fwd_trace
         if self._trace_ok and self._trace_pos < len(t) and t[self._trace_pos] == u.uid:
-            self._prefetch(t[self._trace_pos + 1:])
+            if self.dc_probe is not None:
+                self.dc_probe.mark("fwd", self._trace_pos)
+            if self.dc_schedule is not None:
+                self._issue(self.dc_schedule.fwd_prefetch.get(self._trace_pos, ()))
+            else:
+                self._prefetch(t[self._trace_pos + 1:])
         else:
             self._trace_ok = False
         self._trace_pos += 1
@@ -922,7 +932,23 @@ class ZeroOptimizer:
                 i = len(t) - 1 - t[::-1].index(u.uid)
             except ValueError:
                 return
+            if self.dc_probe is not None:
+                self.dc_probe.mark("bwd", i)
+            if self.dc_schedule is not None:
+                self._issue(self.dc_schedule.bwd_prefetch.get(i, ()))
+                return
             self._prefetch(t[:i][::-1])
+
+    def _issue(self, uids):
+        """Compiled schedule: issue the all-gathers planned for this trace position."""
+        for uid in uids:
+            self._gather(self.units[uid], wait=False)
+
+    def install_schedule(self, sched):
+        """Install a DeepCompile ``CompiledSchedule`` (compile/passes.py): planned prefetch positions replace
+        the depth / bucket policy, resident units stay gathered from their forward to their backward."""
+        self.dc_schedule = sched
+        self._compute_reuse_keep()
 
     def _live_numel(self):
         return sum(u.padded for u in self.units if not u.persistent and u.full is not None)
@@ -949,7 +975,7 @@ class ZeroOptimizer:
     def _compute_reuse_keep(self):
         """Units whose next use (in backward) is within stage3_max_reuse_distance gathered elements stay
         resident after their forward instead of being released and re-gathered."""
-        self._reuse_keep = set()
+        self._reuse_keep = set(self.dc_schedule.resident) if self.dc_schedule is not None else set()
         if self.max_reuse_distance is None:
             return
         t = self._fwd_trace
@@ -1107,6 +1133,8 @@ class ZeroOptimizer:
                 u.bind_grads(u.grad_full)
 
     def finish_backward(self):
+        if self.dc_probe is not None:
+            self.dc_probe.end("bwd")
         for u in self.units:
             if not u.grads_reduced and u.requires_grad_count:
                 if u.grad_full is None and self.stage == 3:
@@ -1143,7 +1171,8 @@ class ZeroOptimizer:
             self._gather(u, wait=True)
 
     def post_forward(self):
-        pass
+        if self.dc_probe is not None:
+            self.dc_probe.end("fwd")
 
     # ------------------------------------------------------------------------------------
     # engine API
