@@ -5,8 +5,8 @@ Reference parity: moe/layer.py (``MoE`` :17-132), moe/sharded_moe.py (``TopKGate
 
 Dispatch is capacity based: tokens are permuted into an expert-major [E, C, H] tensor by the HIP dispatch
 kernel, ONE ``all_to_all_single`` with equal splits moves each expert's slots to its owner (on the full
-xGMI mesh this uses every link of every GPU at once), the local experts run as batched GEMMs
-(``torch.bmm`` -> hipBLASLt) over [E_local, ep*C, H], one all-to-all returns the results and the
+xGMI mesh this uses every link of every GPU at once), the local experts run as per-expert 2-D hipBLASLt GEMMs
+over [E_local, ep*C, H] slices (``expert_linear``), one all-to-all returns the results and the
 combine kernel un-permutes with the gate weights. No dense [T, E, C] dispatch masks are ever built.
 """
 import copy
@@ -86,6 +86,45 @@ class Experts(nn.Module):
         return torch.stack(outs, 0)
 
 
+class _ExpertLinear(torch.autograd.Function):
+    """y[e] = x[e] @ w[e]^T for stacked experts x [E, C, K], w [E, N, K], as E plain 2-D GEMMs written into slices
+    of one output (and, in backward, of one dX and one dW). Batched ``torch.bmm`` with the transposed stacked weight
+    hits a hipBLASLt failure on MI355X at Mixtral-8x7B shapes (HIPBLAS_STATUS_INTERNAL_ERROR for the strided batched
+    TN problem m 4096 n 1280 k 14336, then an illegal access in the rocBLAS fallback); the 2-D forms are the
+    projection GEMMs the dense model runs every step (NT forward, layout-timed dgrad / wgrad from ops/gemm.py)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        E, C, K = x.shape
+        y = x.new_empty(E, C, w.shape[1])
+        for e in range(E):
+            torch.mm(x[e], w[e].t(), out=y[e])
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops.gemm import dgrad, wgrad
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            for e in range(x.shape[0]):
+                dgrad(dy[e], w[e], out=dx[e])
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            for e in range(x.shape[0]):
+                wgrad(dy[e], x[e], dw[e])
+        return dx, dw
+
+
+def expert_linear(x, w):
+    if x.is_cuda:
+        return _ExpertLinear.apply(x.contiguous(), w)
+    return torch.bmm(x, w.transpose(1, 2))
+
+
 class GroupedSwiGLUExperts(nn.Module):
     """E_local SwiGLU experts stored stacked ([E, 2I, H], [E, H, I]) and run as batched GEMMs."""
 
@@ -109,8 +148,8 @@ class GroupedSwiGLUExperts(nn.Module):
         nn.init.normal_(self.w2, std=self._std)
 
     def forward(self, x):
-        h = torch.bmm(x, self.w13.transpose(1, 2))
-        return torch.bmm(glu(h, self.act), self.w2.transpose(1, 2))
+        h = expert_linear(x, self.w13)
+        return expert_linear(glu(h, self.act), self.w2)
 
 
 class MOELayer(nn.Module):
