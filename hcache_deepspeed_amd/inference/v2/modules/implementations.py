@@ -179,8 +179,10 @@ class GroupedGemmMoE(DSMoEBase):
         expert, pos, w, C, _, _ = topk_route(logits, c.top_k, 1.0, 1, drop_tokens=False, use_rts=False,
                                              normalize=c.normalize_scores, training=False)
         disp = moe_dispatch(x, expert, pos, E, C).view(E, C, H)
-        h = torch.bmm(disp, w13.transpose(1, 2))
-        y = torch.bmm(glu(h.reshape(E * C, -1), act).view(E, C, -1), w2.transpose(1, 2))
+        from ....parallel.moe import expert_linear  # per-expert 2-D GEMMs on the GPU (see its docstring)
+        with torch.no_grad():
+            h = expert_linear(disp, w13)
+            y = expert_linear(glu(h.reshape(E * C, -1), act).view(E, C, -1), w2)
         return moe_combine(y.reshape(E * C, H), expert, pos, w, C)
 
 
