@@ -35,6 +35,14 @@ def topk_route(logits, k, capacity_factor=1.0, min_capacity=4, drop_tokens=True,
     ce = F.one_hot(topi[:, 0], E).float().mean(0)
     l_aux = (me * ce).sum() * E
     mask = F.one_hot(topi.t().reshape(-1), E)  # [k*T, E], k-major
+    if not (use_rts and training):
+        # running count per expert as an inner-dim scan over [E, k*T]: the outer-dim scan of [k*T, E] runs one
+        # thread per column on the GPU (3 ms per layer at 16k assignments, 8 experts)
+        mt = mask.t().to(torch.int32)
+        pos = ((torch.cumsum(mt, 1) - 1) * mt).sum(0).view(k, T).t().contiguous()
+        exp_counts = mask.sum(0)
+        C = capacity(T, E, k, capacity_factor, min_capacity) if drop_tokens else int(exp_counts.max().item())
+        return topi.to(torch.int32).contiguous(), pos.to(torch.int32), topw.contiguous(), C, l_aux, exp_counts
     if use_rts and training:
         # random token selection: random priority inside each choice level
         noise = torch.rand(k, T, device=logits.device)
@@ -64,8 +72,9 @@ def topk_assign(logits, k, normalize=True):
     topw, topi = torch.topk(probs, k, dim=-1)
     if normalize and k > 1:
         topw = topw / topw.sum(-1, keepdim=True)
-    mask = F.one_hot(topi.t().reshape(-1), E)  # [k*T, E], k-major
-    pos = ((torch.cumsum(mask, 0) - 1) * mask).sum(-1).view(k, T).t()
+    mt = F.one_hot(topi.t().reshape(-1), E).t().to(torch.int32)  # [E, k*T], k-major; inner-dim scan
+    pos = ((torch.cumsum(mt, 1) - 1) * mt).sum(0).view(k, T).t()
+    mask = mt.t()
     return topi.to(torch.int32).contiguous(), pos.to(torch.int32).contiguous(), topw.contiguous(), mask.sum(0)
 
 

@@ -99,13 +99,17 @@ class _ExpertLinear(torch.autograd.Function):
         y = x.new_empty(E, C, w.shape[1])
         for e in range(E):
             torch.mm(x[e], w[e].t(), out=y[e])
-        ctx.save_for_backward(x, w)
+        # like runtime/zero/linear.py: keep the Parameter object, not its (ZeRO-3 gathered) data, for backward
+        ctx.save_for_backward(x)
+        ctx.weight = w
         return y
 
     @staticmethod
     def backward(ctx, dy):
         from ..ops.gemm import dgrad, wgrad
-        x, w = ctx.saved_tensors
+        from ..runtime.zero.linear import write_weight_grad
+        (x, ) = ctx.saved_tensors
+        w = ctx.weight
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -113,9 +117,14 @@ class _ExpertLinear(torch.autograd.Function):
             for e in range(x.shape[0]):
                 dgrad(dy[e], w[e], out=dx[e])
         if ctx.needs_input_grad[1]:
-            dw = torch.empty_like(w)
-            for e in range(x.shape[0]):
-                wgrad(dy[e], x[e], dw[e])
+
+            def gemm(out, accumulate):  # straight into the ZeRO gradient buffer (no AccumulateGrad add)
+                for e in range(x.shape[0]):
+                    wgrad(dy[e], x[e], out[e], accumulate)
+
+            if not write_weight_grad(w, gemm):
+                dw = torch.empty_like(w)
+                gemm(dw, False)
         return dx, dw
 
 

@@ -1217,6 +1217,11 @@ class ZeroOptimizer:
         from .linear import wrap_memory_efficient_linears
         cand = {id(m.weight) for m in self.module.modules()
                 if isinstance(m, nn.Linear) and id(m.weight) in self.param_to_unit and m.weight.requires_grad}
+        # stacked MoE experts write each expert's weight gradient into its slice (parallel/moe.py _ExpertLinear)
+        from ...parallel.moe import GroupedSwiGLUExperts
+        for m in self.module.modules():
+            if isinstance(m, GroupedSwiGLUExperts):
+                cand |= {id(p) for p in (m.w13, m.w2) if id(p) in self.param_to_unit and p.requires_grad}
         # the fused LM-head cross entropy writes its weight gradient the same way (ops/cross_entropy.py)
         for m in self.module.modules():
             w = getattr(getattr(m, "lm_head", None), "weight", None)

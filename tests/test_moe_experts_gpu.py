@@ -44,3 +44,33 @@ def test_mixtral_layer_full_width_step():
     assert torch.isfinite(loss).item()
     g = m.layers[0].block_sparse_moe.deepspeed_moe.experts.w2.grad
     assert g is not None and torch.isfinite(g.float()).all().item() and g.abs().sum().item() > 0
+
+
+def test_mixtral_engine_direct_expert_wgrad_matches():
+    """Stacked expert weight gradients written in place into the ZeRO gradient buffer (per-expert GEMMs with
+    out=slice) train the same trajectory as the dense AccumulateGrad path (``mi355x.direct_wgrad: false``),
+    with gradient accumulation over 2 micro-steps."""
+    import os
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.mixtral import MixtralForCausalLM, tiny_moe
+    os.environ.setdefault("MASTER_PORT", "29571")
+    res = {}
+    for direct in (True, False):
+        torch.manual_seed(0)
+        m = MixtralForCausalLM(tiny_moe(hidden_size=256, intermediate_size=512, num_hidden_layers=2))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2, "bf16": {"enabled": True},
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "zero_optimization": {"stage": 3},
+               "data_types": {"grad_accum_dtype": "bf16"}, "mi355x": {"direct_wgrad": direct}}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        if direct:
+            assert id(m.layers[0].block_sparse_moe.deepspeed_moe.experts.w13) in eng.optimizer._wgrad_ok
+        g = torch.Generator(device="cuda").manual_seed(1)
+        losses = []
+        for _ in range(6):
+            x = torch.randint(0, 512, (2, 256), device="cuda", generator=g)
+            loss = eng(x, labels=x)
+            eng.backward(loss)
+            eng.step()
+            losses.append(float(loss))
+        res[direct] = losses
+    assert res[True] == pytest.approx(res[False], rel=2e-2, abs=2e-2), res
