@@ -32,6 +32,8 @@ struct DecodeParams {
   int64_t sqb, sqh, skb, skh, sks, svb, svh, svs, sbias;
   int B, H, Hkv, S, splits, keys_per_split;
   float scale;
+  const int* lens;  // [B] valid keys per sequence, read on the device (may be null: S); HIP-graph decode
+  int window;       // > 0: only the last `window` valid keys attend
 };
 
 template <int D>
@@ -44,8 +46,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   const int G = p.H / p.Hkv;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kl = lane / LPK, c = lane % LPK;  // key slot in the wave step, 8-element chunk of the row
+  // valid key range [jb, Se): the cache buffer holds S slots, the sequence fills the first lens[b] of them
+  const int Se = p.lens ? min(p.S, p.lens[b]) : p.S;
+  const int jb = p.window > 0 ? max(0, Se - p.window) : 0;
   const int j0 = split * p.keys_per_split;
-  const int j1 = min(p.S, j0 + p.keys_per_split);
+  const int j1 = min(Se, j0 + p.keys_per_split);
 
   float qv[kGMax][8];
 #pragma unroll
@@ -71,7 +76,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   const bf16* kb = p.k + b * p.skb + hk * p.skh + c * 8;
   const bf16* vb = p.v + b * p.svb + hk * p.svh + c * 8;
   for (int j = j0 + w * KPW + kl; j - kl < j1; j += 4 * KPW) {
-    const bool ok = j < j1;
+    const bool ok = j < j1 && j >= jb;
     float kv[8], vv[8];
     if (ok) {
       Vec8<bf16>::load(kb + (int64_t)j * p.sks, kv);
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
       for (int e = 0; e < 8; ++e) s += qv[g][e] * kv[e];
 #pragma unroll
       for (int off = LPK / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-      s = ok ? s + bj + slope[g] * (float)(j - (p.S - 1)) : -INFINITY;
+      s = ok ? s + bj + slope[g] * (float)(j - (Se - 1)) : -INFINITY;
       const float mn = fmaxf(m[g], s);
       const bool none = mn == -INFINITY;  // nothing valid yet for this lane group (selects keep lanes converged)
       const float a = none ? 1.f : __expf(m[g] - mn), e_s = none ? 0.f : __expf(s - mn);
@@ -187,16 +192,19 @@ HDS_EXPORT int hds_decode_attn_splits(int B, int Hkv, int S) {
   return splits < 1 ? 1 : (splits > 64 ? 64 : splits);
 }
 
-HDS_EXPORT int hds_decode_attn(const void* q, int64_t sqb, int64_t sqh, const void* k, int64_t skb, int64_t skh,
-                               int64_t sks, const void* v, int64_t svb, int64_t svh, int64_t svs, const float* bias,
-                               int64_t sbias, const float* alibi, void* o, float* part_o, float* part_ml, int B,
-                               int H, int Hkv, int S, int D, int splits, float scale, hipStream_t st) {
+// ``lens`` (device [B] int32, or null) bounds each sequence's keys inside the S-slot cache on the device, so one
+// launch shape serves every decode step (HIP-graph replay); ``window`` > 0 keeps only the last window keys.
+HDS_EXPORT int hds_decode_attn_len(const void* q, int64_t sqb, int64_t sqh, const void* k, int64_t skb,
+                                   int64_t skh, int64_t sks, const void* v, int64_t svb, int64_t svh, int64_t svs,
+                                   const float* bias, int64_t sbias, const float* alibi, void* o, float* part_o,
+                                   float* part_ml, int B, int H, int Hkv, int S, int D, int splits, float scale,
+                                   const int* lens, int window, hipStream_t st) {
   if (B <= 0 || S <= 0 || Hkv <= 0 || H % Hkv || !hds_decode_attn_supported(D, H / Hkv) || splits < 1 ||
-      (splits > 1 && (!part_o || !part_ml)))
+      (splits > 1 && (!part_o || !part_ml)) || window < 0)
     return (int)hipErrorInvalidValue;
   const int kps = (S + splits - 1) / splits;
   DecodeParams p{(const bf16*)q, (const bf16*)k, (const bf16*)v, bias, alibi, (bf16*)o, part_o, part_ml,
-                 sqb, sqh, skb, skh, sks, svb, svh, svs, sbias, B, H, Hkv, S, splits, kps, scale};
+                 sqb, sqh, skb, skh, sks, svb, svh, svs, sbias, B, H, Hkv, S, splits, kps, scale, lens, window};
   const dim3 grid(splits, Hkv, B);
   switch (D) {
     case 64:
@@ -212,4 +220,12 @@ HDS_EXPORT int hds_decode_attn(const void* q, int64_t sqb, int64_t sqh, const vo
       if (splits > 1) hipLaunchKernelGGL(decode_combine_kernel<256>, dim3(B * H), dim3(256), 0, st, p);
   }
   return (int)hipGetLastError();
+}
+
+HDS_EXPORT int hds_decode_attn(const void* q, int64_t sqb, int64_t sqh, const void* k, int64_t skb, int64_t skh,
+                               int64_t sks, const void* v, int64_t svb, int64_t svh, int64_t svs, const float* bias,
+                               int64_t sbias, const float* alibi, void* o, float* part_o, float* part_ml, int B,
+                               int H, int Hkv, int S, int D, int splits, float scale, hipStream_t st) {
+  return hds_decode_attn_len(q, sqb, sqh, k, skb, skh, sks, v, svb, svh, svs, bias, sbias, alibi, o, part_o, part_ml,
+                             B, H, Hkv, S, D, splits, scale, nullptr, 0, st);
 }

@@ -132,6 +132,11 @@ class KVCacheGenerator:
             o = sdpa_gqa(q.reshape(B, S, L.nq, L.D).transpose(1, 2), kc[:, :, :S], vc[:, :, :S], mask=a["mask"],
                          scale=scale)
             return o.transpose(1, 2).reshape(B * S, L.nq, L.D)
+        if a["phase"] == "decode_graph":  # device-side position and length: one launch shape for every token
+            B = a["B"]
+            kc.index_copy_(2, a["cur_idx"], k.reshape(B, L.nkv, 1, L.D))
+            vc.index_copy_(2, a["cur_idx"], v.reshape(B, L.nkv, 1, L.D))
+            return decode_attention(q, kc, vc, scale, bias=a["bias"], lens=a["lens"], window=window)
         cur = a["cur"]
         kc[:, :, cur] = k
         vc[:, :, cur] = v
@@ -148,6 +153,20 @@ class KVCacheGenerator:
             h, residual = self._block(li, h, residual, self._cos, self._sin, pos, cache, step_args)
         h, _ = m.norm(h, residual)
         return h
+
+    def _graph_ok(self, dev, B, max_new_tokens):
+        """HIP-graph decode: single-GPU (no TP collectives in the step), the HIP decode kernel available."""
+        import os
+        from ..ops.decode_attention import decode_supported
+        if dev.type != "cuda" or self.tp > 1 or int(max_new_tokens) < 3 or os.environ.get("HDS_DECODE_GRAPH", "1") == "0":
+            return False
+        L = self.layers[0]
+        q = torch.empty(B, L.nq, L.D, device=dev, dtype=L.wqkv.dtype)
+        return decode_supported(q, torch.empty(B, L.nkv, 1, L.D, device=dev, dtype=L.wqkv.dtype))
+
+    def _decode_logits(self, ids, args, pos, cache):
+        h = self._forward(ids, pos, cache, args)
+        return F.linear(h, self.model.lm_head.weight).float()
 
     @torch.no_grad()
     def generate(self, input_ids, attention_mask=None, max_new_tokens=32, do_sample=False, temperature=1.0,
@@ -184,8 +203,21 @@ class KVCacheGenerator:
         out = [input_ids]
         finished = torch.zeros(B, dtype=torch.bool, device=dev)
         last = h.view(B, S, -1)[:, -1]
+        # Decode steps are launch-bound at small batch (~10 kernels per layer for one token): with ``graph`` the
+        # step is captured once as a HIP graph over static buffers (token ids, positions, the cache slot and the
+        # valid lengths live on the device and advance in place) and replayed for every further token.
+        graph = self._graph_ok(dev, B, max_new_tokens)
+        g = None
+        if graph:
+            ids_buf = torch.zeros(B, dtype=torch.long, device=dev)
+            pos_buf = next_pos.to(torch.int32).clone()
+            lens_buf = torch.full((B, ), S + 1, dtype=torch.int32, device=dev)
+            cur_idx = torch.full((1, ), S, dtype=torch.long, device=dev)
+            gargs = {"phase": "decode_graph", "B": B, "cur_idx": cur_idx, "lens": lens_buf, "bias": bias}
+        logits = None
         for t in range(int(max_new_tokens)):
-            logits = F.linear(last, head).float()
+            if logits is None:
+                logits = F.linear(last, head).float()
             if eos_token_id is not None and t < min_new_tokens:
                 logits[:, eos_token_id] = float("-inf")
             nxt = _sample(logits, do_sample, temperature, top_k, top_p, generator)
@@ -198,10 +230,29 @@ class KVCacheGenerator:
             out.append(nxt[:, None])
             if t + 1 == int(max_new_tokens) or (eos_token_id is not None and bool(finished.all())):
                 break
+            if graph:
+                ids_buf.copy_(nxt)
+                if g is None:  # first decode step: eager on a side stream (warms kernels / BLAS), then capture
+                    side = torch.cuda.Stream(dev)
+                    side.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(side):
+                        logits = self._decode_logits(ids_buf, gargs, pos_buf, cache).clone()
+                    torch.cuda.current_stream(dev).wait_stream(side)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        static_logits = self._decode_logits(ids_buf, gargs, pos_buf, cache)
+                else:
+                    g.replay()
+                    logits = static_logits
+                pos_buf += 1
+                lens_buf += 1
+                cur_idx += 1
+                continue
             h = self._forward(nxt, next_pos.to(torch.int32), cache, {"phase": "decode", "B": B, "cur": S + t,
                                                                          "bias": bias})
             next_pos = next_pos + 1
-            last = h
+            logits = F.linear(h, head).float()
+        self.used_graph = g is not None
         return torch.cat(out, 1)
 
 

@@ -34,11 +34,21 @@ def decode_supported(q, k):
     return bool(native.kernels().hds_decode_attn_supported(D, H // k.shape[1])) and H % k.shape[1] == 0
 
 
-def decode_attention(q, k, v, scale=None, bias=None, alibi=None):
-    """q [B, H, D] (any head/batch strides, last dim contiguous), k/v [B, Hkv, S, D] (last dim contiguous)."""
+def decode_attention(q, k, v, scale=None, bias=None, alibi=None, lens=None, window=0):
+    """q [B, H, D] (any head/batch strides, last dim contiguous), k/v [B, Hkv, S, D] (last dim contiguous).
+
+    ``lens`` (int32 [B] on the device): only the first lens[b] cache slots are keys (and, with ``window`` > 0,
+    only the last ``window`` of those). The launch shape then depends on the buffer size S alone, so a decode
+    step that calls this can be captured once in a HIP graph and replayed for every token."""
     B, H, D = q.shape
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if not decode_supported(q, k) or q.stride(2) != 1 or k.stride(3) != 1 or v.stride(3) != 1:
+        if lens is not None:  # reference path: mask the slots past each sequence's length (and outside the window)
+            j = torch.arange(k.shape[2], device=q.device)[None, :]
+            n = lens.to(torch.long)[:, None]
+            off = (j >= n) | ((j < n - window) if window > 0 else torch.zeros_like(j, dtype=torch.bool))
+            extra = torch.zeros(off.shape, device=q.device, dtype=torch.float32).masked_fill_(off, float("-inf"))
+            bias = extra if bias is None else bias.float() + extra
         return decode_attention_ref(q, k, v, scale, bias, alibi)
     Hkv, S = k.shape[1], k.shape[2]
     kern = native.kernels()
@@ -54,14 +64,17 @@ def decode_attention(q, k, v, scale=None, bias=None, alibi=None):
             bias = bias.contiguous()
     if alibi is not None:
         alibi = alibi.float().contiguous()
-    native.check(kern.hds_decode_attn(q.data_ptr(), q.stride(0), q.stride(1), k.data_ptr(), k.stride(0), k.stride(1),
+    if lens is not None:
+        assert lens.dtype == torch.int32 and lens.numel() == B and lens.is_contiguous()
+    native.check(kern.hds_decode_attn_len(q.data_ptr(), q.stride(0), q.stride(1), k.data_ptr(), k.stride(0), k.stride(1),
                                       k.stride(2), v.data_ptr(), v.stride(0), v.stride(1), v.stride(2),
                                       bias.data_ptr() if bias is not None else None,
                                       bias.stride(0) if bias is not None else 0,
                                       alibi.data_ptr() if alibi is not None else None, o.data_ptr(),
                                       part_o.data_ptr() if part_o is not None else None,
                                       part_ml.data_ptr() if part_ml is not None else None, B, H, Hkv, S, D, splits,
-                                      float(scale), native.stream()), "decode_attn")
+                                      float(scale), lens.data_ptr() if lens is not None else None, int(window),
+                                      native.stream()), "decode_attn")
     return o
 
 

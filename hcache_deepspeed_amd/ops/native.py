@@ -75,6 +75,7 @@ _KERNEL_SIGS = {
     "hds_decode_attn_supported": "ii",
     "hds_decode_attn_splits": "iii",
     "hds_decode_attn": "p" + "ll" + "p" + "lll" + "p" + "lll" + "p" + "l" + "p" + "ppp" + "iiiiii" + "f" + "s",
+    "hds_decode_attn_len": "p" + "ll" + "p" + "lll" + "p" + "lll" + "p" + "l" + "p" + "ppp" + "iiiiii" + "f" + "pi" + "s",
     "hds_evoformer_bwd": "p" * 10 + "pp" + "i" + "pp" + "iiiii" + "f" + "s",
     "hds_embed_bwd": "i" + "pppp" + "l" + "i" + "ll" + "s",
     "hds_slice_mask": "i" + "ppp" + "iiiii" + "s",

@@ -111,3 +111,19 @@ def _hybrid_tp(rank, world):
 
 def test_hybrid_engine_tp_generate_gloo():
     run_distributed(_hybrid_tp, 2)
+
+
+def test_decode_attention_device_lengths_reference():
+    """decode_attention(lens=, window=) over a larger cache buffer equals attention over the sliced cache (the
+    contract the HIP-graph decode step relies on)."""
+    from hcache_deepspeed_amd.ops.decode_attention import decode_attention, decode_attention_ref
+    g = torch.Generator().manual_seed(0)
+    B, H, Hkv, S, D = 3, 4, 2, 20, 16
+    q = torch.randn(B, H, D, generator=g)
+    k = torch.randn(B, Hkv, S, D, generator=g)
+    v = torch.randn(B, Hkv, S, D, generator=g)
+    for n, win in ((7, 0), (13, 4), (20, 0)):
+        lens = torch.full((B, ), n, dtype=torch.int32)
+        lo = max(0, n - win) if win else 0
+        ref = decode_attention_ref(q, k[:, :, lo:n], v[:, :, lo:n], 0.25)
+        assert torch.allclose(decode_attention(q, k, v, 0.25, lens=lens, window=win), ref, atol=1e-5)

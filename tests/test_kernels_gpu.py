@@ -663,3 +663,27 @@ def test_flash_fwd_staggered_variant_gpu(case):
             mask |= i[None, :] <= i[:, None] - kw["window"]
         ref = (torch.softmax(s.masked_fill(mask, float("-inf")), -1) @ vf).transpose(1, 2)
         torch.testing.assert_close(outs[4].float(), ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [0, 40])
+def test_hip_graph_decode_matches_eager_gpu(window, monkeypatch):
+    """KV-cached greedy generation with the decode step captured in a HIP graph (device-side positions / cache slot /
+    lengths, decode_attention(lens=...)) produces exactly the tokens of the eager loop, incl. left padding."""
+    from hcache_deepspeed_amd.models.generation import KVCacheGenerator
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(hidden_size=512, intermediate_size=1024, num_hidden_layers=3, num_attention_heads=4,
+                              num_key_value_heads=2, vocab_size=1000, sliding_window=window)).cuda().to(
+                                  torch.bfloat16).eval()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    prompt = torch.randint(1, 1000, (3, 50), device="cuda", generator=g)
+    mask = torch.ones_like(prompt)
+    mask[1, :7] = 0
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HDS_DECODE_GRAPH", mode)
+        gen = KVCacheGenerator(m)
+        outs[mode] = gen.generate(prompt, attention_mask=mask, max_new_tokens=24)
+        assert gen.used_graph == (mode == "1")
+    assert torch.equal(outs["1"], outs["0"])
