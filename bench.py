@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--offload-param", action="store_true")
     ap.add_argument("--nvme-path", default="/tmp/hds_nvme", help="swap folder of the NVMe tier (--offload nvme)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
+    ap.add_argument("--deepcompile", action="store_true",
+                    help="engine.compile() with DeepCompile: profiled ZeRO-3 gather schedule (selective gather + prefetch)")
     args = ap.parse_args()
     if os.environ.get("HDS_HANG_DUMP"):
         # diagnosis of a stuck run: every N seconds print the Python stacks of all threads to stderr
@@ -117,6 +119,8 @@ def main():
                                                                         "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }
+    if args.deepcompile:
+        ds_config["compile"] = {"deepcompile": True}
     if args.offload != "none":
         ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True}
         if args.offload_param:
@@ -132,6 +136,8 @@ def main():
     if args.ckpt:
         model.gradient_checkpointing_enable()
     engine, _, _, _ = hds.initialize(model=model, config=ds_config)
+    if args.deepcompile:
+        engine.compile()  # schedule compiled after the profiled warmup step (compile/backend.py)
     t_init = time.time() - t_init
     dev = engine.device
     S, mb = args.seq, args.micro_batch
@@ -203,7 +209,7 @@ def main():
                        "host_act_cache": bool(args.host_act_cache), "offload": args.offload,
                        "global_batch": world * mb * args.gas, "seq_len": S,
                        "parallelism": f"zero{args.zero}-dp{world}", "micro_batch_per_gpu": mb, "gas": args.gas,
-                       "activation_checkpointing": bool(args.ckpt)},
+                       "activation_checkpointing": bool(args.ckpt), "deepcompile": bool(args.deepcompile)},
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
                       "final_loss": round(float(loss.item()), 4), "peak_mem_gib": round(mem, 1),
                       "init_s": round(t_init, 1), "valid": on_gpu and not bool(args.layers),
