@@ -189,12 +189,17 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
     const int64_t base = (int64_t)row * cols;
     const float rstd = stat_rstd[row];
     const float mean = LN ? stat_mean[row] : 0.f;
-    vec8 hv[NV], dv[NV];  // packed in the activation dtype: 4 VGPRs per vector for bf16
+    vec8 hv[NV], dv[NV], rv[NV];  // packed in the activation dtype: 4 VGPRs per vector for bf16
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (i * 64 + lane) * 8;
       hv[i] = *reinterpret_cast<const vec8*>(h + base + c);
       dv[i] = *reinterpret_cast<const vec8*>(dy + base + c);
+    }
+    // the residual gradient is issued with the row's other loads, so its latency hides behind the reduction
+    if (dres != nullptr) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) rv[i] = *reinterpret_cast<const vec8*>(dres + base + (i * 64 + lane) * 8);
     }
     float sum_gx = 0.f, sum_g = 0.f;
 #pragma unroll
@@ -217,15 +222,14 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (i * 64 + lane) * 8;
-      float wv[8], o[8], dr[8];
+      float wv[8], o[8];
       Vec8<WT>::load(w + c, wv);
-      if (dres != nullptr) Vec8<T>::load(dres + base + c, dr);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = (to_f(hv[i][j]) - mean) * rstd;
         const float g = to_f(dv[i][j]) * wv[j];
         const float d = rstd * (g - xh * sum_gx - (LN ? sum_g : 0.f));
-        o[j] = d + (dres != nullptr ? dr[j] : 0.f);
+        o[j] = d + (dres != nullptr ? to_f(rv[i][j]) : 0.f);
       }
       Vec8<T>::store(dx + base + c, o);
     }
@@ -397,9 +401,18 @@ HDS_EXPORT int hds_norm_fwd(int is_ln, int dtype, int wdtype, const void* x, con
   HDS_DISPATCH2(dtype, wdtype, false, launch_fwd, x, res, res_out, w, b, y, mean, rstd, rows, cols, eps, st);
 }
 
+static int g_norm_bwd_max_parts = 512;
+
+// cap on the backward's workgroups = fp32 weight-gradient partial rows (A/B knob; 512 = 8 waves per CU)
+HDS_EXPORT int hds_norm_bwd_set_max_parts(int n) {
+  if (n < 1 || n > 8192) return hipErrorInvalidValue;
+  g_norm_bwd_max_parts = n;
+  return 0;
+}
+
 HDS_EXPORT int hds_norm_bwd_nparts(int rows) {
   int n = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
-  return n < 512 ? (n < 1 ? 1 : n) : 512;  // 512 partial rows: 8 waves/CU, small reduce
+  return n < g_norm_bwd_max_parts ? (n < 1 ? 1 : n) : g_norm_bwd_max_parts;
 }
 
 HDS_EXPORT int hds_norm_bwd(int is_ln, int dtype, int wdtype, const void* dy, const void* h, const void* dres,

@@ -21,6 +21,7 @@ _hlib = None
 _KERNEL_SIGS = {
     "hds_norm_fwd": "iii" + "p" * 8 + "ii" + "f" + "s",
     "hds_norm_bwd_nparts": "i",
+    "hds_norm_bwd_set_max_parts": "i",
     "hds_norm_bwd": "iii" + "p" * 9 + "i" + "pp" + "iii" + "s",
     "hds_rope": "ii" + "pppp" + "l" + "iii" + "l" + "ii" + "f" + "s",
     "hds_glu_fwd": "iipplis",
