@@ -179,9 +179,17 @@ def get_backend(group=None):
     return dist.get_backend(group) if is_initialized() else None
 
 
-def new_group(ranks=None, **kwargs):
+def new_group(ranks=None, high_priority=False, **kwargs):
+    """``high_priority``: with RCCL, the group's collectives run on high-priority HIP streams
+    (``ProcessGroupNCCL.Options.is_high_priority_stream``) so they are dispatched ahead of queued compute."""
     if not is_initialized():
         return None
+    if high_priority and "pg_options" not in kwargs and get_backend() == "nccl":
+        opts = getattr(dist, "ProcessGroupNCCL", None)
+        if opts is not None:
+            o = opts.Options()
+            o.is_high_priority_stream = True
+            kwargs["pg_options"] = o
     return dist.new_group(ranks=ranks, **kwargs)
 
 

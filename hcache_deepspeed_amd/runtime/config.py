@@ -12,7 +12,8 @@ MI355X-specific knobs live under ``"mi355x"``::
         "zero3_prefetch_depth": 2,      # units all-gathered ahead of compute
         "zero3_max_reduce_inflight": 2, # gradient reduce-scatters in flight before the oldest is retired
         "host_act_cache": {"enabled": false, "slots": 8, "slot_mb": 512, "min_layers_resident": 2},
-        "fused_lm_head_ce": true
+        "fused_lm_head_ce": true,
+        "comm_high_priority": true      # ZeRO-3 AG/RS communicators on high-priority streams
     }
 """
 import copy
@@ -180,6 +181,9 @@ class MI355XConfig:
     zero3_unit_bucket_mb: float = 128  # per-submodule ZeRO-3 units of ModuleList-free models are bucketed to this
     direct_wgrad: bool = True  # weight-gradient GEMMs write into the flat gradient buffer (runtime/zero/linear.py)
     fused_lm_head_ce: bool = True
+    # ZeRO-3 all-gather / reduce-scatter communicators run their RCCL kernels on high-priority HIP streams, so
+    # the few workgroups a collective needs are dispatched ahead of queued GEMM tiles (overlap under full load)
+    comm_high_priority: bool = True
     host_act_cache: HostActCacheConfig = field(default_factory=HostActCacheConfig)
 
 
@@ -300,6 +304,7 @@ class DeepSpeedConfig:
             zero3_unit_bucket_mb=float(m.get("zero3_unit_bucket_mb", 128)),
             direct_wgrad=bool(m.get("direct_wgrad", True)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
+            comm_high_priority=bool(m.get("comm_high_priority", True)),
             host_act_cache=HostActCacheConfig(**{f.name: hac[f.name]
                                                  for f in fields(HostActCacheConfig) if f.name in hac}))
 

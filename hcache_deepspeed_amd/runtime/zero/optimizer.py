@@ -235,8 +235,9 @@ class ZeroOptimizer:
                     torch.distributed.get_process_group_ranks(dp_group)) if self.dp_world > 1 else [dist.get_rank()]
         self._setup_zeropp(dp_ranks)
         if self.stage == 3 and self.dp_world > 1 and not self.mics:
-            self.ag_group = dist.new_group(ranks=dp_ranks)
-            self.rs_group = dist.new_group(ranks=dp_ranks)
+            hp = bool(getattr(self.mi, "comm_high_priority", True))
+            self.ag_group = dist.new_group(ranks=dp_ranks, high_priority=hp)
+            self.rs_group = dist.new_group(ranks=dp_ranks, high_priority=hp)
 
         op = self.zcfg.offload_param
         self.offload_param = bool(op.enabled) and self.stage == 3
