@@ -22,6 +22,7 @@ import torch.nn.functional as F
 from ..ops.activations import glu
 from ..ops.attention import flash_attn
 from ..ops.decode_attention import decode_attention, sdpa_gqa
+from ..ops.gemv import linear  # F.linear; decode-sized (<= 8 rows) bf16 inputs on the HIP GEMV
 from ..ops.norm import rms_norm
 from ..ops.rope import rope_
 
@@ -104,14 +105,14 @@ class KVCacheGenerator:
         else:
             x, residual = rms_norm(h, L.ln1.weight, L.ln1.eps, residual)
         T = x.shape[0]
-        qkv = F.linear(x, L.wqkv, L.bqkv).view(T, L.nq + 2 * L.nkv, L.D)
+        qkv = linear(x, L.wqkv, L.bqkv).view(T, L.nq + 2 * L.nkv, L.D)
         rope_(qkv, cos, sin, L.nq + L.nkv, pos_ids=pos)
         o = self._attend(li, qkv, cache, step_args).reshape(T, L.nq * L.D)
-        a = self._all_reduce(F.linear(o, L.wo))
+        a = self._all_reduce(linear(o, L.wo))
         if L.bo is not None:
             a = a + L.bo
         x, residual = rms_norm(a, L.ln2.weight, L.ln2.eps, residual)
-        m = self._all_reduce(F.linear(glu(F.linear(x, L.wgu), L.act), L.wdown))
+        m = self._all_reduce(linear(glu(linear(x, L.wgu), L.act), L.wdown))
         if L.bdown is not None:
             m = m + L.bdown
         return m, residual
@@ -166,7 +167,7 @@ class KVCacheGenerator:
 
     def _decode_logits(self, ids, args, pos, cache):
         h = self._forward(ids, pos, cache, args)
-        return F.linear(h, self.model.lm_head.weight).float()
+        return linear(h, self.model.lm_head.weight).float()
 
     @torch.no_grad()
     def generate(self, input_ids, attention_mask=None, max_new_tokens=32, do_sample=False, temperature=1.0,

@@ -687,3 +687,21 @@ def test_hip_graph_decode_matches_eager_gpu(window, monkeypatch):
         outs[mode] = gen.generate(prompt, attention_mask=mask, max_new_tokens=24)
         assert gen.used_graph == (mode == "1")
     assert torch.equal(outs["1"], outs["0"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (3, 4100, 4096), (8, 1000, 1032), (5, 128256, 512), (2, 7, 8)])
+def test_gemv_bf16_matches_fp32(M, N, K):
+    """Decode-sized HIP GEMV (ops/gemv.py) against an fp32 reference, incl. odd N (row tail), K not a multiple of
+    the 1024-element double chunk, bias, and a strided activation view."""
+    from hcache_deepspeed_amd.ops.gemv import gemv, gemv_ok
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K**-0.5).to(torch.bfloat16)
+    big = torch.randn(M, K + 8, device="cuda", generator=g).to(torch.bfloat16)
+    x = big[:, :K]  # row stride K + 8
+    b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    assert gemv_ok(x, w, b) or N * K > __import__("hcache_deepspeed_amd.ops.gemv", fromlist=["x"]).MAX_GEMV_NUMEL
+    y = gemv(x, w, b)
+    ref = x.float() @ w.float().t() + b.float()
+    rel = ((y.float() - ref).norm() / ref.norm()).item()
+    assert rel < 8e-3, rel
