@@ -6,8 +6,15 @@ import torch.nn.functional as F
 
 from . import native
 
-# weights up to this many elements take the GEMV (hipBLASLt is latency-bound below it at M <= 8)
-MAX_GEMV_NUMEL = int(__import__("os").environ.get("HDS_GEMV_MAX_NUMEL", "0"))  # set from the GPU measurement
+# Weight sizes (elements) that take the GEMV, from profiles/gemv_bench_r2.jsonl: at M = 1 the GEMV streams
+# 3.6-6.6 TB/s and beats hipBLASLt up to the 59M-element down projection (qkv 3.5x, o 2.1x, down 1.1x; gate_up 0.96x);
+# its dot products make it VALU-bound as M grows (M = 4: qkv 1.4x, down 0.73x; M = 8: o 1.36x, qkv 0.98x), so the
+# limit halves at M > 1 and again at M > 4.
+MAX_GEMV_NUMEL = int(__import__("os").environ.get("HDS_GEMV_MAX_NUMEL", str(64 * 1024 * 1024)))
+
+
+def max_numel(M):
+    return MAX_GEMV_NUMEL >> (0 if M == 1 else (1 if M <= 4 else 2))
 
 
 def gemv_ok(x2, w, b=None):
@@ -17,7 +24,7 @@ def gemv_ok(x2, w, b=None):
     N = w.shape[0]
     if M > 8 or w.shape[1] != K or not w.is_contiguous() or x2.stride(1) != 1 or x2.stride(0) % 8:
         return False
-    if x2.data_ptr() % 16 or w.data_ptr() % 16 or N * K > MAX_GEMV_NUMEL:
+    if x2.data_ptr() % 16 or w.data_ptr() % 16 or N * K > max_numel(M):
         return False
     if b is not None and (b.dtype != torch.bfloat16 or not b.is_contiguous()):
         return False
