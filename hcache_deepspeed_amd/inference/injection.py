@@ -84,7 +84,8 @@ class LinearBiasAct(nn.Module):
         self.act = act
 
     def forward(self, x):
-        return bias_act(F.linear(x, self.weight), self.bias, self.act)
+        from ..ops.gemv import linear  # decode steps (<= 8 tokens) on the HIP GEMV
+        return bias_act(linear(x, self.weight), self.bias, self.act)
 
 
 class QuantizedLinear(nn.Module):

@@ -76,9 +76,10 @@ class BlasFPLinear(DSLinearBase):
 
     def forward(self, x, w, b=None):
         a = self._config.activation
+        from ....ops.gemv import linear  # decode-sized ragged batches (<= 8 tokens) on the HIP GEMV
         if a == "identity" or a.endswith("_glu"):
-            return _act_tail(F.linear(x, w, b), None, a)
-        return bias_act(F.linear(x, w), b, a)
+            return _act_tail(linear(x, w, b), None, a)
+        return bias_act(linear(x, w), b, a)
 
 
 class _PackedWeight:
