@@ -187,7 +187,9 @@ HDS_EXPORT int hds_decode_attn_supported(int D, int G) { return (D == 64 || D ==
 HDS_EXPORT int hds_decode_attn_splits(int B, int Hkv, int S) {
   const int groups = B * Hkv;
   int splits = (512 + groups - 1) / groups;          // >= 2 workgroups per CU overall
-  const int max_by_len = (S + 127) / 128;            // >= 128 keys per split
+  // >= 32 keys per split: a split's waves walk their keys with one dependent K/V load per step, so at short
+  // contexts (a few hundred keys, B * Hkv = 8) the HBM latency of those steps, not bandwidth, sets the time
+  const int max_by_len = (S + 31) / 32;
   splits = splits < max_by_len ? splits : max_by_len;
   return splits < 1 ? 1 : (splits > 64 ? 64 : splits);
 }
