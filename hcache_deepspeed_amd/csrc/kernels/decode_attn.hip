@@ -231,3 +231,34 @@ HDS_EXPORT int hds_decode_attn(const void* q, int64_t sqb, int64_t sqh, const vo
   return hds_decode_attn_len(q, sqb, sqh, k, skb, skh, sks, v, svb, svh, svs, bias, sbias, alibi, o, part_o, part_ml,
                              B, H, Hkv, S, D, splits, scale, nullptr, 0, st);
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// KV append for the HIP-graph decode step: K and V of one new token per sequence written into cache slot
+// cur[0] (read on the device) of [B, Hkv, S, D] caches, one launch for both tensors (two index_copy kernels
+// before). Workgroup = one (b, kv head), 16-B vectors along D.
+// ---------------------------------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(64) void kv_append_kernel(const bf16* __restrict__ k, int64_t skb, int64_t skh,
+                                                       const bf16* __restrict__ v, int64_t svb, int64_t svh,
+                                                       bf16* __restrict__ kc, int64_t ckb, int64_t ckh,
+                                                       int64_t cks, bf16* __restrict__ vc, int64_t cvb, int64_t cvh,
+                                                       int64_t cvs, const int64_t* __restrict__ cur, int Hkv, int D) {
+  const int b = blockIdx.x / Hkv, h = blockIdx.x % Hkv;
+  const int64_t s = cur[0];
+  for (int c = threadIdx.x * 8; c < D; c += 64 * 8) {
+    *reinterpret_cast<bf16x8*>(kc + b * ckb + h * ckh + s * cks + c) =
+        *reinterpret_cast<const bf16x8*>(k + b * skb + h * skh + c);
+    *reinterpret_cast<bf16x8*>(vc + b * cvb + h * cvh + s * cvs + c) =
+        *reinterpret_cast<const bf16x8*>(v + b * svb + h * svh + c);
+  }
+}
+}  // namespace
+
+HDS_EXPORT int hds_kv_append(const void* k, int64_t skb, int64_t skh, const void* v, int64_t svb, int64_t svh, void* kc,
+                             int64_t ckb, int64_t ckh, int64_t cks, void* vc, int64_t cvb, int64_t cvh, int64_t cvs,
+                             const int64_t* cur, int B, int Hkv, int D, hipStream_t st) {
+  if (B <= 0 || Hkv <= 0 || D % 8 || !cur) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kv_append_kernel, dim3(B * Hkv), dim3(64), 0, st, (const bf16*)k, skb, skh, (const bf16*)v, svb,
+                     svh, (bf16*)kc, ckb, ckh, cks, (bf16*)vc, cvb, cvh, cvs, cur, Hkv, D);
+  return (int)hipGetLastError();
+}

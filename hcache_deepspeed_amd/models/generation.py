@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from ..ops.activations import glu
 from ..ops.attention import flash_attn
-from ..ops.decode_attention import decode_attention, sdpa_gqa
+from ..ops.decode_attention import decode_attention, kv_append, sdpa_gqa
 from ..ops.gemv import linear  # F.linear; decode-sized (<= 8 rows) bf16 inputs on the HIP GEMV
 from ..ops.norm import rms_norm
 from ..ops.rope import rope_
@@ -135,8 +135,7 @@ class KVCacheGenerator:
             return o.transpose(1, 2).reshape(B * S, L.nq, L.D)
         if a["phase"] == "decode_graph":  # device-side position and length: one launch shape for every token
             B = a["B"]
-            kc.index_copy_(2, a["cur_idx"], k.reshape(B, L.nkv, 1, L.D))
-            vc.index_copy_(2, a["cur_idx"], v.reshape(B, L.nkv, 1, L.D))
+            kv_append(k, v, kc, vc, a["cur_idx"])
             return decode_attention(q, kc, vc, scale, bias=a["bias"], lens=a["lens"], window=window)
         cur = a["cur"]
         kc[:, :, cur] = k

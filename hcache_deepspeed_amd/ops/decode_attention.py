@@ -82,3 +82,20 @@ def sdpa_gqa(q, k, v, mask=None, is_causal=False, scale=None):
     """[B, H, Sq, D] x [B, Hkv, Skv, D] attention without materialising repeated K/V."""
     return F.scaled_dot_product_attention(q, k, v, attn_mask=mask, is_causal=is_causal, scale=scale,
                                           enable_gqa=k.shape[1] != q.shape[1])
+
+
+def kv_append(k, v, kc, vc, cur_idx):
+    """kc[:, :, cur] = k ; vc[:, :, cur] = v for k/v [B, Hkv, D] (last dim contiguous) and caches [B, Hkv, S, D], with
+    the slot ``cur_idx`` (int64 [1]) read on the device: one HIP launch, capturable in the decode graph."""
+    B, H, D = k.shape
+    if not (native.use_native(k) and k.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16 and D % 8 == 0
+            and k.stride(2) == 1 and v.stride(2) == 1 and kc.stride(3) == 1 and vc.stride(3) == 1
+            and cur_idx.dtype == torch.int64 and k.data_ptr() % 16 == 0 and v.data_ptr() % 16 == 0
+            and all(st % 8 == 0 for st in (k.stride(0), k.stride(1), v.stride(0), v.stride(1)))):
+        kc.index_copy_(2, cur_idx, k.reshape(B, H, 1, D))
+        vc.index_copy_(2, cur_idx, v.reshape(B, H, 1, D))
+        return
+    native.check(native.kernels().hds_kv_append(k.data_ptr(), k.stride(0), k.stride(1), v.data_ptr(), v.stride(0),
+                                                v.stride(1), kc.data_ptr(), kc.stride(0), kc.stride(1), kc.stride(2),
+                                                vc.data_ptr(), vc.stride(0), vc.stride(1), vc.stride(2),
+                                                cur_idx.data_ptr(), B, H, D, native.stream()), "kv_append")

@@ -75,6 +75,7 @@ _KERNEL_SIGS = {
     "hds_gemm_mxfp8_supported": "iiiiii",
     "hds_gemm_mxfp8": "ppppp" + "iiiiii" + "f" + "i" + "s",
     "hds_mx_quant": "ppp" + "l" + "i" + "l" + "s",
+    "hds_kv_append": "p" + "ll" + "p" + "ll" + "p" + "lll" + "p" + "lll" + "p" + "iii" + "s",
     "hds_decode_attn_supported": "ii",
     "hds_decode_attn_splits": "iii",
     "hds_decode_attn": "p" + "ll" + "p" + "lll" + "p" + "lll" + "p" + "l" + "p" + "ppp" + "iiiiii" + "f" + "s",

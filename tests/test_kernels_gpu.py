@@ -705,3 +705,22 @@ def test_gemv_bf16_matches_fp32(M, N, K):
     ref = x.float() @ w.float().t() + b.float()
     rel = ((y.float() - ref).norm() / ref.norm()).item()
     assert rel < 8e-3, rel
+
+
+@pytest.mark.gpu
+def test_kv_append_matches_index_copy():
+    """HIP KV append (slot read on the device) equals two index_copy_ calls, for strided K/V views of a fused qkv."""
+    from hcache_deepspeed_amd.ops.decode_attention import kv_append
+    g = torch.Generator(device="cuda").manual_seed(0)
+    B, nq, nkv, D, S = 3, 8, 2, 128, 40
+    qkv = torch.randn(B, nq + 2 * nkv, D, device="cuda", generator=g).to(torch.bfloat16)
+    k, v = qkv[:, nq:nq + nkv], qkv[:, nq + nkv:]
+    kc = torch.randn(B, nkv, S, D, device="cuda", generator=g).to(torch.bfloat16)
+    vc = torch.randn(B, nkv, S, D, device="cuda", generator=g).to(torch.bfloat16)
+    kr, vr = kc.clone(), vc.clone()
+    cur = torch.tensor([17], device="cuda")
+    kv_append(k, v, kc, vc, cur)
+    kr.index_copy_(2, cur, k.reshape(B, nkv, 1, D))
+    vr.index_copy_(2, cur, v.reshape(B, nkv, 1, D))
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)
