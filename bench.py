@@ -171,6 +171,7 @@ def main():
     sync()
     tdist.barrier()
     sync()
+    retries0 = torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) if on_gpu else 0
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = train_step(args.warmup + i)
@@ -189,6 +190,8 @@ def main():
              6 * cfg_model.active_params() + 12 * cfg_model.num_hidden_layers * S * cfg_model.hidden_size) * tokens
     mfu = flops / dt / (2.5e15 * world)
     mem = torch.cuda.max_memory_allocated(dev) / 2**30 if on_gpu else 0.0
+    # caching-allocator retries in the timed steps: each one frees cached blocks after a device-wide synchronize
+    retries = (torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) - retries0) if on_gpu else 0
     if rank == 0:
         out = {
             "metric": ("tokens/sec (node) Llama-3-8B ZeRO-3 at 1/2/4/8 MI355X" if args.model == "llama3-8b" else
@@ -213,8 +216,12 @@ def main():
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
                       "final_loss": round(float(loss.item()), 4), "peak_mem_gib": round(mem, 1),
                       "init_s": round(t_init, 1), "valid": on_gpu and not bool(args.layers),
-                      "tuned_gemm_table": tuned, "device": "mi355x" if on_gpu else "cpu-dry-run"},
+                      "tuned_gemm_table": tuned, "device": "mi355x" if on_gpu else "cpu-dry-run",
+                      "alloc_retries_timed": int(retries)},
         }
+        ac = getattr(engine, "_activation_cache", None)
+        if ac is not None:
+            out["extra"]["act_cache"] = ac.stats()
         zo = engine.optimizer
         sw = getattr(zo, "opt_swapper", None)
         if sw is not None:  # ZeRO-Infinity NVMe tier: how much of the optimizer's swap I/O hid behind CPU Adam

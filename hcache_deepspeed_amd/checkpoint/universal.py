@@ -141,6 +141,23 @@ def _read_universal(path):
     return obj, {}
 
 
+def _universal_moment_keys(zdir):
+    """Per-parameter optimizer-state file names (e.g. exp_avg, exp_avg_sq) of a universal checkpoint."""
+    for name in sorted(os.listdir(zdir)):
+        pdir = os.path.join(zdir, name)
+        if not os.path.isdir(pdir) or not os.path.exists(os.path.join(pdir, "fp32.pt")):
+            continue
+        keys = []
+        for f in sorted(os.listdir(pdir)):
+            if not f.endswith(".pt") or f == "fp32.pt":
+                continue
+            t, _ = _read_universal(os.path.join(pdir, f))
+            if torch.is_tensor(t) and t.numel() > 1:
+                keys.append(f[:-3])
+        return keys
+    return []
+
+
 def load_universal_into(zopt, universal_dir, load_optimizer_states=True):
     """Fill a (possibly differently sized / TP-sliced) ZeroOptimizer's shards from a universal checkpoint.
 
@@ -155,6 +172,12 @@ def load_universal_into(zopt, universal_dir, load_optimizer_states=True):
     if groups._State.topo is not None:
         tp_world, tp_rank = groups.get_model_parallel_world_size(), groups.get_model_parallel_rank()
     flats = zopt._ckpt_flats()
+    if load_optimizer_states and zopt.kind == "generic":
+        # a wrapped torch optimizer creates its state lazily: before its first step it has no moment flats, so take
+        # the keys from the files and load into zero flats (as load_state_dict does)
+        for k in _universal_moment_keys(zdir):
+            if k not in flats:
+                flats[k] = torch.zeros_like(flats["fp32"])
     keys = ["fp32"] + ([k for k in flats if k != "fp32"] if load_optimizer_states else [])
     with torch.no_grad():
         for u in zopt.units:

@@ -105,7 +105,7 @@ def _numel(shape):
     return int(math.prod(shape))
 
 
-def _reconstruct(stage, shapes, parts):
+def _reconstruct(stage, shapes, parts, exact=True):
     """shapes: OrderedDict name -> shape of one flat group; parts: that group's partition on each rank, in rank
     order -> OrderedDict name -> fp32 tensor."""
     out = OrderedDict()
@@ -127,7 +127,7 @@ def _reconstruct(stage, shapes, parts):
         pn = math.ceil(n / W)
         out[name] = torch.cat([p.narrow(0, off, pn).float() for p in parts]).narrow(0, 0, n).view(tuple(shape)).clone()
         off += pn
-    if off != parts[0].numel():
+    if off > parts[0].numel() or (exact and off != parts[0].numel()):
         raise ValueError(f"consumed {off} of {parts[0].numel()} elements per rank: checkpoint / param_shapes mismatch")
     return out
 
@@ -162,13 +162,26 @@ def _one_mp_rank(optim_files, model_file, model_files_all, key="fp32"):
     shapes = msd["param_shapes"]
     metas = sds[0].get("hds_group_meta") or [None] * len(shapes)
     pcs = sds[0]["partition_count"]
-    pcs = pcs if isinstance(pcs, list) else [pcs] * len(shapes)
+    pcs = pcs if isinstance(pcs, list) else [pcs] * max(len(shapes), 1)
     by_rank = {_dp_rank(f): sd for f, sd in zip(optim_files, sds)}
     state = OrderedDict()
     buffers = set(msd.get("buffer_names") or [])
     for n, t in (msd.get("module") or {}).items():
         if n in buffers and key == "fp32":
             state[n] = t.float()
+    if stage == 3 and all(m is None for m in metas) and len(by_rank[0]["fp32_flat_groups"]) != len(shapes):
+        # the reference's stage 3 writes one flat per sub-group (sub_group_size), not per param group: walk the
+        # merged param_shapes over each rank's concatenated sub-group flats (reference zero_to_fp32.py:437-477)
+        W = int(pcs[0])
+        if len(by_rank) < W:
+            raise ValueError(f"expected {W} '*_optim_states.pt' files, found {len(by_rank)}")
+        merged = OrderedDict((n, s) for d in shapes for n, s in d.items())
+        parts = []
+        for r in range(W):
+            n_sub = len(by_rank[r]["fp32_flat_groups"])
+            parts.append(torch.cat([_partition(by_rank[r], i, key).view(-1) for i in range(n_sub)]))
+        state.update(_reconstruct(stage, merged, parts, exact=False))
+        shapes, metas = [], []
     for g, (shp, meta) in enumerate(zip(shapes, metas)):
         W = int(pcs[g])
         if meta is None or meta.get("expert_group") is None:

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   const bf16* vb = p.v + b * p.svb + hk * p.svh + c * 8;
   for (int j = j0 + w * KPW + kl; j - kl < j1; j += 4 * KPW) {
     const bool ok = j < j1 && j >= jb;
-    float kv[8], vv[8];
+    float kv[8] = {}, vv[8] = {};  // masked lanes still run the (e_s = 0) update: keep NaN bits out of acc
     if (ok) {
       Vec8<bf16>::load(kb + (int64_t)j * p.sks, kv);
       Vec8<bf16>::load(vb + (int64_t)j * p.svs, vv);

@@ -25,5 +25,6 @@ class QuantizationConfig:
     q_dtype: torch.dtype = torch.uint8
     # MI355X: 8-bit e4m3 weights of 2-D linears also keep an MX-FP8 copy (e8m0 scale per 32 elements) and run
     # prefill/training-sized inputs on the block-scaled FP8 matrix cores, with the activations MX-quantized on
-    # the fly (ops/fp8_gemm.py). False keeps the reference's weight-only path (dequantize + bf16 GEMM).
-    mx_fp8: bool = True
+    # the fly (ops/fp8_gemm.py). Opt-in: the default keeps the reference's weight-only path (dequantize + bf16 GEMM),
+    # whose numerics do not depend on the token count.
+    mx_fp8: bool = False

@@ -53,7 +53,7 @@ class LoRAOptimizedLinear(nn.Module):
         if quantization_config is not None:
             self.weight = QuantizedParameter(shard, quantization_config=quantization_config, dtype=dtype)
             if self.zero_shards == 1 and _mx_eligible(self.weight.quantization_config, output_dim, input_dim):
-                self.weight.enable_mx((output_dim, input_dim), w)
+                self.weight.enable_mx((output_dim, input_dim))
         else:
             self.weight = nn.Parameter(shard, requires_grad=False)
         self.weight.ds_optim_param = False

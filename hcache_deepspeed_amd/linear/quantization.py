@@ -4,7 +4,8 @@
 fpq.hip). The weight is dequantized to the compute dtype for each forward; FP6 linears with decode-sized inputs
 skip that and run the fused 6-bit GEMV (ops/quantizer.fp6_linear).
 
-8-bit e4m3 2-D weights additionally hold an MX-FP8 copy (``QuantizationConfig.mx_fp8``): inputs of >= 256 rows
+With ``QuantizationConfig.mx_fp8`` (opt-in; default off = the reference's weight-only numerics) 8-bit e4m3 2-D weights
+additionally hold an MX-FP8 copy derived from the quantized weight: inputs of >= 256 rows
 then run on the block-scaled FP8 matrix cores (ops/fp8_gemm.py, 1.5-1.8x the bf16 GEMM), forward AND the input
 gradient of the frozen weight (a transposed MX copy made on first use)."""
 import torch
@@ -49,18 +50,21 @@ class QuantizedParameter(nn.Parameter):
         else:
             self.q_data, self.q_scales = Q.quantize_minifloat(flat.contiguous(), gs, self.q_bits,
                                                               self.quantization_config.mantissa_bits)
+        if getattr(self, "mx_shape", None) is not None:  # re-quantized: the MX copy follows the new q_data
+            self.enable_mx(self.mx_shape)
 
-    def enable_mx(self, shape2d, source):
-        """Keep an MX-FP8 copy of the 2-D weight ``source`` (logical shape ``shape2d`` = [out, in])."""
+    def enable_mx(self, shape2d):
+        """Keep an MX-FP8 copy (logical shape ``shape2d`` = [out, in]) derived from the quantized weight itself, so
+        the two paths see the same weight values."""
         from ..ops.fp8_gemm import mx_quantize
         N, K = shape2d
         self.mx_shape = (N, K)
-        self.mx_w = mx_quantize(source.detach().reshape(N, K).to(torch.bfloat16).contiguous())
+        self.mx_w = mx_quantize(self.dequantized().reshape(N, K).to(torch.bfloat16).contiguous())
         self.mx_wt = None  # [in, out] copy for the input gradient, built on first backward
 
     def mx_ok(self):
         cfg = self.quantization_config
-        return getattr(self, "mx_w", None) is not None and getattr(cfg, "mx_fp8", True)
+        return getattr(self, "mx_w", None) is not None and getattr(cfg, "mx_fp8", False)
 
     def dequantized(self):
         if self.q_bits == 8:
@@ -97,7 +101,7 @@ class QuantizedParameter(nn.Parameter):
 
 def _mx_eligible(cfg, N, K):
     from ..ops.fp8_gemm import mx_supported
-    return cfg.q_bits == 8 and cfg.mantissa_bits == 3 and getattr(cfg, "mx_fp8", True) and mx_supported(256, N, K)
+    return cfg.q_bits == 8 and cfg.mantissa_bits == 3 and getattr(cfg, "mx_fp8", False) and mx_supported(256, N, K)
 
 
 class _MxLinearFn(torch.autograd.Function):
@@ -142,7 +146,7 @@ class QuantizedLinear(nn.Linear):
         data = self.weight.data
         self.weight = QuantizedParameter(data, quantization_config=quantization_config, dtype=dtype)
         if _mx_eligible(self.weight.quantization_config, output_dim, input_dim):
-            self.weight.enable_mx((output_dim, input_dim), data)
+            self.weight.enable_mx((output_dim, input_dim))
 
     def forward(self, x):
         w = self.weight

@@ -79,6 +79,12 @@ class HostActivationCache:
         self.n_layers = 0
         self.by_layer = {}
         self.bytes_offloaded = 0
+        # diagnostics: saved tensors unpacked before their prefetch was issued (a compute-stream stall on PCIe),
+        # tensors the runtime guard spilled outside the plan, bytes the host cap kept on the GPU
+        self.late_unpacks = 0
+        self.guard_spills = 0
+        self.host_capped_bytes = 0
+        self._capped_this_step = 0
         self._attached = []
 
     @classmethod
@@ -116,11 +122,15 @@ class HostActivationCache:
     def forward_context(self):
         if self.budget is not None and self.device.type == "cuda":
             if self._calibrating:  # the previous step spilled everything: plan from what it measured
-                peak = torch.cuda.max_memory_allocated(self.device)
-                self.plan = plan_offload(self.layer_bytes, peak, self.budget)
+                # tensors the host cap kept on the GPU were all alive at the forward/backward turn-around, so the
+                # "everything spilled" peak is the measured one minus them (plan_offload adds kept layers back)
+                peak = torch.cuda.max_memory_allocated(self.device) - self._capped_this_step
+                self.plan = calibrated_plan(self.layer_bytes, peak + self._capped_this_step, self._capped_this_step,
+                                            self.budget)
                 self._calibrating = False
                 log_dist(f"host activation cache: spilling {len(self.plan)} of {self.n_layers} layers (peak when spilling all {peak / 2**30:.1f} GiB, budget "
-                         f"{self.budget / 2**30:.1f} GiB)", ranks=[0])
+                         f"{self.budget / 2**30:.1f} GiB, {self._capped_this_step / 2**30:.1f} GiB kept by the host cap)",
+                         ranks=[0])
             elif self.plan is None:
                 self._calibrating = True
                 torch.cuda.reset_peak_memory_stats(self.device)
@@ -133,6 +143,7 @@ class HostActivationCache:
                     o.host = None
         self.by_layer = {}
         self.layer_bytes = {}
+        self._capped_this_step = 0
         with torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack):
             yield
 
@@ -144,10 +155,13 @@ class HostActivationCache:
             return t
         nbytes = t.numel() * t.element_size()
         self.layer_bytes[self.cur_layer] = self.layer_bytes.get(self.cur_layer, 0) + nbytes
-        if (self.plan is not None and self.cur_layer not in self.plan
-                and torch.cuda.memory_allocated(self.device) + nbytes <= self.budget):
-            return _Tagged(t, self.cur_layer) if self.by_layer else t  # tag only when something was spilled
+        if self.plan is not None and self.cur_layer not in self.plan:
+            if torch.cuda.memory_allocated(self.device) + nbytes <= self.budget:
+                return _Tagged(t, self.cur_layer) if self.by_layer else t  # tag only when something was spilled
+            self.guard_spills += 1
         if self.host_budget is not None and self.host_in_use + nbytes > self.host_budget:
+            self.host_capped_bytes += nbytes
+            self._capped_this_step += nbytes
             return _Tagged(t, self.cur_layer) if self.by_layer else t
         s = _Spilled()
         s.shape, s.dtype, s.device, s.layer = t.shape, t.dtype, t.device, self.cur_layer
@@ -202,6 +216,8 @@ class HostActivationCache:
             return s.t
         if not isinstance(s, _Spilled):
             return s
+        if s.dev is None:
+            self.late_unpacks += 1
         if self._DEBUG and s.dev is None:
             print(f"[act-cache] t={time.perf_counter():.3f} layer {s.layer} needed before its prefetch", file=sys.stderr,
                   flush=True)
@@ -216,7 +232,16 @@ class HostActivationCache:
         return out
 
     def stats(self):
-        return {"bytes_offloaded": self.bytes_offloaded, "pinned_pool_bytes": self.pool.bytes_allocated}
+        return {"bytes_offloaded": self.bytes_offloaded, "pinned_pool_bytes": self.pool.bytes_allocated,
+                "spilled_layers": None if self.plan is None else len(self.plan), "late_unpacks": self.late_unpacks,
+                "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes}
+
+
+def calibrated_plan(layer_bytes, measured_peak, host_capped_bytes, budget):
+    """Plan from a calibration step in which the pinned-host cap kept ``host_capped_bytes`` of eligible tensors on
+    the GPU: those bytes sit inside ``measured_peak`` (they are alive at the forward/backward turn-around) and are
+    also counted in ``layer_bytes``, so the all-spilled peak is the measured one minus them."""
+    return plan_offload(layer_bytes, measured_peak - host_capped_bytes, budget)
 
 
 def plan_offload(layer_bytes, peak_all, budget):

@@ -141,9 +141,15 @@ _INT_GEMV_MAX_M = min(8, int(os.environ.get("HDS_INT_GEMV_MAX_M", "2")))
 _WMIX_MAX_M = int(os.environ.get("HDS_WMIX_MAX_M", "64"))
 
 
+def _needs_grad(x):
+    """The fused GEMV / mixed-input kernels have no backward: an input that needs a gradient (a LoRA base under
+    training) takes the differentiable dequantize + GEMM path so dX still flows to earlier layers."""
+    return torch.is_grad_enabled() and x.requires_grad
+
+
 def wmix_eligible(x2, out_features, in_features, group_size):
     M = x2.shape[0]
-    return (native.use_native(x2) and x2.dtype == torch.bfloat16 and 0 < M <= _WMIX_MAX_M
+    return (not _needs_grad(x2) and native.use_native(x2) and x2.dtype == torch.bfloat16 and 0 < M <= _WMIX_MAX_M
             and bool(native.kernels().hds_wmix_supported(M, out_features, in_features, group_size)))
 
 
@@ -173,7 +179,7 @@ def int_linear(x, q_weight, scales, out_features, in_features, group_size, bits=
     lead = x.shape[:-1]
     x2 = x.reshape(-1, in_features)
     M = x2.shape[0]
-    if native.use_native(x2) and 0 < M <= _INT_GEMV_MAX_M and x2.dtype == torch.bfloat16 and in_features % 16 == 0 \
+    if not _needs_grad(x2) and native.use_native(x2) and 0 < M <= _INT_GEMV_MAX_M and x2.dtype == torch.bfloat16 and in_features % 16 == 0 \
             and group_size % 16 == 0:
         x2 = x2.contiguous()
         y = torch.empty(M, out_features, dtype=torch.bfloat16, device=x.device)
@@ -419,7 +425,8 @@ def fp6_linear(x, q_weight, scales, out_features, in_features, group_size, manti
     lead = x.shape[:-1]
     x2 = x.reshape(-1, in_features)
     M = x2.shape[0]
-    if native.use_native(x2) and M <= 8 and x2.dtype == torch.bfloat16 and in_features % 16 == 0 \
+    if not _needs_grad(x2) and native.use_native(x2) and M <= 8 and x2.dtype == torch.bfloat16 \
+            and in_features % 16 == 0 \
             and group_size % 16 == 0:
         x2 = x2.contiguous()
         y = torch.empty(M, out_features, dtype=torch.bfloat16, device=x.device)

@@ -229,6 +229,37 @@ def build_state_dict(z, flats, scalars):
     return sd
 
 
+def _split_like(flat, groups):
+    out, off = [], 0
+    for g in groups:
+        n = min(g.part, max(0, flat.numel() - off))
+        t = flat.narrow(0, off, n)
+        out.append(t if n == g.part else torch.cat([t, t.new_zeros(g.part - n)]))
+        off += g.part
+    if off < flat.numel() and bool(flat[off:].abs().sum() > 0):
+        raise ValueError(f"stage-3 sub-group flats hold {flat.numel()} elements per rank, this model {off}")
+    return out
+
+
+def _regroup_stage3(fp32, base, groups):
+    """Sub-group flats (any count) -> one partition per ref group of this optimizer, for fp32 and every moment."""
+    fp32 = _split_like(torch.cat([t.float().view(-1) for t in fp32]), groups)
+    st = base.get("state", {})
+    keys = sorted(st, key=lambda k: int(k))
+    new_st = {}
+    if keys:
+        first = st[keys[0]]
+        merged = {}
+        for k, v in first.items():
+            if torch.is_tensor(v) and v.dim() == 1:
+                merged[k] = _split_like(torch.cat([st[i][k].float().view(-1) for i in keys]), groups)
+        for gidx in range(len(groups)):
+            new_st[gidx] = {k: (merged[k][gidx] if k in merged else v) for k, v in first.items()}
+    base = dict(base)
+    base["state"] = new_st
+    return fp32, base
+
+
 def read_state_dict(z, sd, order=None):
     """Parse a reference-schema optimizer state (ours or the reference's) for optimizer ``z``.
 
@@ -249,6 +280,11 @@ def read_state_dict(z, sd, order=None):
         fp32 = sd["single_partition_of_fp32_groups"]
         base = sd["base_optimizer_state"]
     pc = sd.get("partition_count")
+    if stage == 3 and len(fp32) != len(groups):
+        # the reference's stage 3 writes one flat per sub-group (sub_group_size, stage3.py:2082-2144), not one per
+        # param group; params run back to back across them (reference utils/zero_to_fp32.py:437-477)
+        fp32, base = _regroup_stage3(fp32, base, groups)
+        pc = pc if not isinstance(pc, list) else pc[0]
     pcs = pc if isinstance(pc, list) else [pc] * len(groups)
     if len(fp32) != len(groups):
         raise ValueError(f"checkpoint has {len(fp32)} flat groups, this optimizer {len(groups)}")

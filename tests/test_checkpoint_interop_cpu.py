@@ -347,3 +347,118 @@ def _async(rank, world, d):
 
 def test_async_save_commits_latest_after_all_ranks(tmp_path):
     run_distributed(_async, 2, str(tmp_path))
+
+
+# ---------------------------------------------------------------------------------------------
+# reference stage-3 files with several sub-group flats (sub_group_size) and one param group
+# ---------------------------------------------------------------------------------------------
+def _to_subgroups(ckpt_dir, n_sub):
+    """Rewrite our stage-3 files the way the reference's stage 3 writes a model larger than sub_group_size: each
+    rank's fp32 / moment flats split into ``n_sub`` sub-group flats, one merged param_shapes group, none of our
+    private keys."""
+    for f in sorted(glob.glob(os.path.join(ckpt_dir, "*_optim_states.pt")), key=_natural):
+        sd = torch.load(f, map_location="cpu", weights_only=True)
+        osd = sd["optimizer_state_dict"]
+        flat = torch.cat([t.view(-1) for t in osd["fp32_flat_groups"]])
+        bounds = [round(i * flat.numel() / n_sub) for i in range(n_sub + 1)]
+        cut = lambda t: [t[bounds[i]:bounds[i + 1]].clone() for i in range(n_sub)]  # noqa: E731
+        osd["fp32_flat_groups"] = cut(flat)
+        st = osd["optimizer_state_dict"]["state"]
+        keys = sorted(st)
+        moments = {k: cut(torch.cat([st[g][k].view(-1) for g in keys])) for k, v in st[keys[0]].items()
+                   if torch.is_tensor(v) and v.dim() == 1}
+        osd["optimizer_state_dict"]["state"] = {
+            i: {**{k: v for k, v in st[keys[0]].items() if k not in moments}, **{k: moments[k][i] for k in moments}}
+            for i in range(n_sub)}
+        for k in ("hds_param_order", "hds_group_meta", "hds_optimizer_kind"):
+            osd.pop(k, None)
+        torch.save(sd, f)
+    for f in glob.glob(os.path.join(ckpt_dir, "*_model_states.pt")):
+        msd = torch.load(f, map_location="cpu", weights_only=True)
+        msd["param_shapes"] = [OrderedDict((n, s) for d in msd["param_shapes"] for n, s in d.items())]
+        torch.save(msd, f)
+
+
+def _subgroup_save(rank, world, d):
+    eng = _engine(3)
+    _train(eng, 2, 7 + rank)
+    eng.save_checkpoint(d, tag="sg")
+    states = _full_states(eng)
+    torch.distributed.barrier()
+    if rank == 0:
+        torch.save(states, os.path.join(d, "expected.pt"))
+        _to_subgroups(os.path.join(d, "sg"), 3)
+    torch.distributed.barrier()
+
+
+def _subgroup_load(rank, world, d):
+    eng = _engine(3, seed=123)
+    eng.load_checkpoint(d, tag="sg")
+    got = _full_states(eng)
+    exp = torch.load(os.path.join(d, "expected.pt"), weights_only=True)
+    for k, (w, m, v) in exp.items():
+        assert torch.equal(got[k][0], w), ("fp32", k)
+        assert torch.equal(got[k][1], m), ("exp_avg", k)
+        assert torch.equal(got[k][2], v), ("exp_avg_sq", k)
+
+
+def test_reference_stage3_subgroup_flats(tmp_path):
+    """a reference ZeRO-3 checkpoint of a model over sub_group_size holds more flat groups than param
+    groups; zero_to_fp32 and load_checkpoint must walk the merged param_shapes over the concatenated flats."""
+    d = str(tmp_path)
+    run_distributed(_subgroup_save, 2, d)
+    from hcache_deepspeed_amd.checkpoint.zero_to_fp32 import get_fp32_state_dict_from_zero_checkpoint
+    ours = get_fp32_state_dict_from_zero_checkpoint(d, tag="sg")
+    ref = _reference_zero_to_fp32(os.path.join(d, "sg"))
+    exp = torch.load(os.path.join(d, "expected.pt"), weights_only=True)
+    for k, (w, _, _) in exp.items():
+        assert torch.equal(ours[k], w), k
+        assert torch.equal(ref[k], w), k
+    run_distributed(_subgroup_load, 2, d)
+
+
+# ---------------------------------------------------------------------------------------------
+# wrapped torch optimizer (lazy state) loading a universal checkpoint before its first step
+# ---------------------------------------------------------------------------------------------
+def _generic_engine(seed, extra=None):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    torch.manual_seed(seed)
+    m = LlamaForCausalLM(tiny(**TINY))
+    opt = torch.optim.RMSprop(m.parameters(), lr=1e-3)
+    cfg = {"train_micro_batch_size_per_gpu": 2, "zero_optimization": {"stage": 2}}
+    cfg.update(extra or {})
+    eng, _, _, _ = ds.initialize(model=m, optimizer=opt, config=cfg)
+    assert eng.optimizer.kind == "generic"
+    return eng
+
+
+def _generic_flat(eng, key):
+    return eng.optimizer._generic_flat_states()[key].clone()
+
+
+def _generic_save(rank, world, d):
+    eng = _generic_engine(0)
+    _train(eng, 2, 5)
+    eng.save_checkpoint(d, tag="g")
+    torch.save({"square_avg": _generic_flat(eng, "square_avg"), "fp32": eng.optimizer.store.master.clone()},
+               os.path.join(d, "gexp.pt"))
+    from hcache_deepspeed_amd.checkpoint import ds_to_universal
+    ds_to_universal(d, os.path.join(d, "g_univ"), tag="g")
+
+
+def _generic_load(rank, world, d):
+    eng = _generic_engine(9, extra={"checkpoint": {"load_universal": True}})
+    assert not eng.optimizer._generic_flat_states()  # no state before the first step
+    eng.load_checkpoint(d, tag="g_univ")
+    exp = torch.load(os.path.join(d, "gexp.pt"), weights_only=True)
+    assert torch.equal(eng.optimizer.store.master, exp["fp32"])
+    assert torch.equal(_generic_flat(eng, "square_avg"), exp["square_avg"])
+
+
+def test_universal_moments_load_into_unstepped_generic_optimizer(tmp_path):
+    """moments of a wrapped torch optimizer must load from a universal checkpoint even though its
+    state does not exist yet (never a silent skip)."""
+    d = str(tmp_path)
+    run_distributed(_generic_save, 1, d)
+    run_distributed(_generic_load, 1, d)

@@ -580,8 +580,8 @@ def test_quantized_lora_linear_mx_fp8_gpu():
     from hcache_deepspeed_amd.ops.fp8_gemm import mx_dequantize, mx_quantize
     torch.manual_seed(0)
     lin = OptimizedLinear(1024, 512, lora_config=LoRAConfig(lora_r=8, lora_alpha=16),
-                          quantization_config=QuantizationConfig(q_bits=8, group_size=256), dtype=torch.bfloat16,
-                          device="cuda")
+                          quantization_config=QuantizationConfig(q_bits=8, group_size=256, mx_fp8=True),
+                          dtype=torch.bfloat16, device="cuda")
     lin.weight.to("cuda")
     assert lin.weight.mx_ok()
     x = torch.randn(2, 256, 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
@@ -623,6 +623,22 @@ def test_decode_attention_matches_reference_gpu(D, H, Hkv, S):
         out = decode_attention(q, k, v, 0.1, **kw)
         ref = decode_attention_ref(q.float(), k.float(), v.float(), 0.1, kw.get("bias"), kw.get("alibi"))
         torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    # device lengths + sliding window: masked lanes at split tails, before the window and past lens[b]; the
+    # cache past lens is filled with NaN so a masked lane that reads or accumulates it poisons the output
+    if S >= 37:
+        lens = torch.tensor([S, max(1, S // 2), max(1, S - 5)], device="cuda", dtype=torch.int32)
+        kn, vn = k.clone(), v.clone()
+        for b, n in enumerate(lens.tolist()):
+            kn[b, :, n:] = float("nan")
+            vn[b, :, n:] = float("nan")
+        for win in (0, 17):
+            out = decode_attention(q, kn, vn, 0.1, lens=lens, window=win)
+            assert torch.isfinite(out.float()).all()
+            for b, n in enumerate(lens.tolist()):
+                lo = max(0, n - win) if win else 0
+                ref = decode_attention_ref(q[b:b + 1].float(), k[b:b + 1, :, lo:n].float(), v[b:b + 1, :, lo:n].float(),
+                                           0.1)
+                torch.testing.assert_close(out[b:b + 1].float(), ref.float(), atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.gpu

@@ -51,17 +51,37 @@ def test_base_weight_sharding_world2():
 
 
 def test_quantized_linear_mx_fp8_cpu_reference():
-    """8-bit e4m3 QuantizedLinear keeps an MX-FP8 copy; off-GPU it runs the dequantized MX weight."""
+    """8-bit e4m3 QuantizedLinear with mx_fp8 keeps an MX-FP8 copy derived from the quantized weight; off-GPU it
+    runs the dequantized MX weight. The default is the reference's weight-only path."""
     from hcache_deepspeed_amd.linear import QuantizationConfig
     from hcache_deepspeed_amd.linear.quantization import QuantizedLinear
     from hcache_deepspeed_amd.ops.fp8_gemm import mx_dequantize
     torch.manual_seed(0)
-    ql = QuantizedLinear(512, 256, quantization_config=QuantizationConfig(q_bits=8, group_size=128),
+    ql = QuantizedLinear(512, 256, quantization_config=QuantizationConfig(q_bits=8, group_size=128, mx_fp8=True),
                          dtype=torch.float32)
     assert ql.weight.mx_ok() and ql.weight.mx_shape == (256, 512)
     x = torch.randn(4, 512)
     w = mx_dequantize(*ql.weight.mx_w)
     torch.testing.assert_close(ql(x), x @ w.t())
-    off = QuantizedLinear(512, 256, quantization_config=QuantizationConfig(q_bits=8, group_size=128, mx_fp8=False),
+    off = QuantizedLinear(512, 256, quantization_config=QuantizationConfig(q_bits=8, group_size=128),
                           dtype=torch.float32)
-    assert not off.weight.mx_ok()
+    assert not off.weight.mx_ok()  # default: weight-only
+    torch.testing.assert_close(off(x), x @ off.weight.dequantized().float().t())
+    # the MX copy tracks re-quantization (no stale snapshot)
+    ql.weight._ensure_quantized(torch.randn(256, 512))
+    torch.testing.assert_close(mx_dequantize(*ql.weight.mx_w).float(),
+                               mx_dequantize(*__import__("hcache_deepspeed_amd.ops.fp8_gemm", fromlist=["x"]).mx_quantize(
+                                   ql.weight.dequantized().reshape(256, 512).to(torch.bfloat16))).float())
+
+
+def test_quantized_fp6_lora_base_passes_input_gradient():
+    """a frozen FP6 base under LoRA training must pass dX to earlier layers at every token count."""
+    from hcache_deepspeed_amd.linear import QuantizationConfig
+    from hcache_deepspeed_amd.linear.quantization import QuantizedLinear
+    torch.manual_seed(0)
+    ql = QuantizedLinear(256, 128, quantization_config=QuantizationConfig(q_bits=6, mantissa_bits=2, group_size=64),
+                         dtype=torch.float32)
+    for rows in (1, 9, 64, 300):
+        x = torch.randn(rows, 256, requires_grad=True)
+        ql(x).sum().backward()
+        assert x.grad is not None and x.grad.abs().sum() > 0, rows

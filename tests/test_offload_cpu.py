@@ -122,6 +122,19 @@ def test_act_cache_plan_spills_earliest_layers_within_budget():
     assert plan_offload({}, peak_all=0, budget=1) == set()
 
 
+def test_act_cache_host_capped_calibration_plans_like_uncapped():
+    """A calibration step whose pinned-host cap kept some layers on the GPU must plan the same spill set as an
+    uncapped one: the capped bytes are inside the measured peak and must not be counted twice."""
+    from hcache_deepspeed_amd.offload.activation_cache import calibrated_plan, plan_offload
+    lb = {i: 10 for i in range(30)}
+    base = 130  # model states + working set with every eligible layer on the host
+    for budget in (140, 200, 265, 1000):
+        uncapped = plan_offload(lb, peak_all=base, budget=budget)
+        for capped_layers in (0, 5, 15):  # the cap kept the LAST layers of the forward on the GPU
+            capped = capped_layers * 10
+            assert calibrated_plan(lb, base + capped, capped, budget) == uncapped, (budget, capped_layers)
+
+
 def _nvme_vs_dram(rank, world, d, opt_device, param_device):
     """ZeRO-Infinity NVMe tier: optimizer states (and parameters) in swap files reproduce the in-DRAM offload
     trajectory bit for bit; the swap files exist and carry the bytes (nothing silently stays in DRAM)."""
