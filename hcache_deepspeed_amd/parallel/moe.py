@@ -8,6 +8,11 @@ kernel, ONE ``all_to_all_single`` with equal splits moves each expert's slots to
 xGMI mesh this uses every link of every GPU at once), the local experts run as per-expert 2-D hipBLASLt GEMMs
 over [E_local, ep*C, H] slices (``expert_linear``), one all-to-all returns the results and the
 combine kernel un-permutes with the gate weights. No dense [T, E, C] dispatch masks are ever built.
+
+Expert tensor parallelism (``enable_expert_tensor_parallelism`` under a TP dense model, reference moe/layer.py:52-58,
+moe/mappings.py:105-113): each TP rank sends only its 1/tp of the capacity slots through the expert all-to-all,
+all-gathers its experts' slots from the TP peers, runs column/row-sharded experts and folds the partial sums and
+the token drop into ONE reduce-scatter before the return all-to-all.
 """
 import copy
 
@@ -35,6 +40,90 @@ class _AllToAll(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         return _AllToAll.apply(g, ctx.group), None
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# tensor-parallel token mappings (reference moe/mappings.py:105-113 drop_tokens / gather_tokens). Tokens are
+# duplicated across the TP ranks of a tensor-parallel dense model; each rank keeps 1/tp of the capacity slots
+# across the expert all-to-all (1/tp of its bytes on xGMI). Every mapping works on a dim moved to the front so the
+# collective is one flat all_gather_into_tensor / reduce_scatter_tensor.
+# ---------------------------------------------------------------------------------------------------------------
+def _tp():
+    if groups._State.topo is None:
+        return None, 1, 0
+    n = groups.get_tensor_model_parallel_world_size()
+    return (groups._get_model_parallel_group() if n > 1 else None), n, groups.get_tensor_model_parallel_rank()
+
+
+def _tp_gather(x, dim):
+    grp, n, _ = _tp()
+    xt = x.movedim(dim, 0).contiguous()
+    out = xt.new_empty((n * xt.shape[0], ) + tuple(xt.shape[1:]))
+    dist.all_gather_into_tensor(out, xt, group=grp)
+    return out.movedim(0, dim)
+
+
+def _tp_reduce_scatter(x, dim):
+    grp, n, _ = _tp()
+    xt = x.movedim(dim, 0).contiguous()
+    out = xt.new_empty((xt.shape[0] // n, ) + tuple(xt.shape[1:]))
+    dist.reduce_scatter_tensor(out, xt, group=grp)
+    return out.movedim(0, dim)
+
+
+def _tp_narrow(x, dim):
+    _, n, r = _tp()
+    c = x.shape[dim] // n
+    return x.narrow(dim, r * c, c)
+
+
+class _DropTokens(torch.autograd.Function):
+    """fwd: this TP rank's 1/tp slice of ``dim`` (the inputs are replicated); bwd: all-gather."""
+
+    @staticmethod
+    def forward(ctx, x, dim):
+        ctx.dim = dim
+        return _tp_narrow(x, dim).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return _tp_gather(g, ctx.dim), None
+
+
+class _GatherTokens(torch.autograd.Function):
+    """fwd: all-gather ``dim`` over TP; bwd: this rank's slice (the consumer's gradient is replicated) or, with
+    ``partial_grad`` (the consumer is a TP-sharded expert whose input gradient is a partial sum), reduce-scatter."""
+
+    @staticmethod
+    def forward(ctx, x, dim, partial_grad):
+        ctx.dim, ctx.partial = dim, partial_grad
+        return _tp_gather(x, dim)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (_tp_reduce_scatter(g, ctx.dim) if ctx.partial else _tp_narrow(g, ctx.dim).contiguous()), None, None
+
+
+class _ReduceScatterTokens(torch.autograd.Function):
+    """fwd: sum the TP ranks' partial expert outputs and keep this rank's slice of ``dim`` (all-reduce + drop in
+    one reduce-scatter); bwd: all-gather."""
+
+    @staticmethod
+    def forward(ctx, x, dim):
+        ctx.dim = dim
+        return _tp_reduce_scatter(x, dim)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _tp_gather(g.contiguous(), ctx.dim), None
+
+
+def drop_tokens(x, dim=0):
+    return x if _tp()[1] == 1 else _DropTokens.apply(x, dim)
+
+
+def gather_tokens(x, dim=0, partial_grad=False):
+    return x if _tp()[1] == 1 else _GatherTokens.apply(x, dim, partial_grad)
 
 
 class TopKGate(nn.Module):
@@ -137,8 +226,13 @@ def expert_linear(x, w):
 class GroupedSwiGLUExperts(nn.Module):
     """E_local SwiGLU experts stored stacked ([E, 2I, H], [E, H, I]) and run as batched GEMMs."""
 
-    def __init__(self, hidden, inter, num_local_experts, expert_group_name=None, std=0.02, act="silu"):
+    def __init__(self, hidden, inter, num_local_experts, expert_group_name=None, std=0.02, act="silu", tp_size=1):
         super().__init__()
+        assert inter % tp_size == 0, f"expert intermediate size {inter} not divisible by expert TP size {tp_size}"
+        # expert tensor parallelism: this rank holds gate/up rows [r*I/tp, (r+1)*I/tp) (column parallel) and the
+        # matching w2 columns (row parallel); the partial outputs are summed by the MoE layer's reduce-scatter
+        self.tp_size = tp_size
+        inter = inter // tp_size
         self.w13 = nn.Parameter(torch.empty(num_local_experts, 2 * inter, hidden))
         self.w2 = nn.Parameter(torch.empty(num_local_experts, hidden, inter))
         self._std = std
@@ -150,11 +244,22 @@ class GroupedSwiGLUExperts(nn.Module):
             p.group_name = expert_group_name
             p._hds_expert_stacked = True  # dim 0 = local expert index
             p._hds_num_local = num_local_experts
+            p.tensor_model_parallel = tp_size > 1
         self.reset_parameters()
 
     def reset_parameters(self):
         nn.init.normal_(self.w13, std=self._std)
         nn.init.normal_(self.w2, std=self._std)
+
+    @torch.no_grad()
+    def load_full(self, w13, w2, tp_rank=0):
+        """Copy this TP rank's shard of full (unsharded) stacked weights w13 [E, 2I, H] (gate | up) and w2
+        [E, H, I]."""
+        i_full = w2.shape[-1]
+        i = i_full // self.tp_size
+        lo = tp_rank * i
+        self.w13.copy_(torch.cat([w13[:, lo:lo + i], w13[:, i_full + lo:i_full + lo + i]], 1))
+        self.w2.copy_(w2[:, :, lo:lo + i])
 
     def forward(self, x):
         h = expert_linear(x, self.w13)
@@ -163,8 +268,9 @@ class GroupedSwiGLUExperts(nn.Module):
 
 class MOELayer(nn.Module):
 
-    def __init__(self, gate, experts, ep_group_name, ep_size, num_local_experts):
+    def __init__(self, gate, experts, ep_group_name, ep_size, num_local_experts, expert_tp=False):
         super().__init__()
+        self.expert_tp = expert_tp
         self.gate = gate
         self.experts = experts
         self.ep_group_name = ep_group_name
@@ -183,19 +289,42 @@ class MOELayer(nn.Module):
         x2 = x.reshape(-1, H)
         E = self.num_local_experts * self.ep_size
         expert, pos, w, C, l_aux, counts = self.gate(x2)
-        disp = moe_dispatch(x2, expert, pos, E, C)  # [E*C, H], expert-major
+        tp = _tp()[1]
+        # expert TP: the TP ranks split the slots over the all-to-all. Without it the (replicated) experts run the
+        # same slots on every TP rank, so their gradients need no reduction over TP.
+        sharded = self.expert_tp and tp > 1
+        if sharded and C % tp:
+            # slots split evenly over the TP ranks: pad the buffer, keep every dropped assignment dropped
+            Cp = -(-C // tp) * tp
+            pos = torch.where(pos >= C, torch.full_like(pos, Cp), pos)
+            C = Cp
+        disp = moe_dispatch(x2, expert, pos, E, C).view(E, C, H)  # expert-major
+        # tokens are replicated over a TP dense model's ranks: each sends only its 1/tp of the slots
+        if sharded:
+            disp = drop_tokens(disp, 1)
+        Cl = disp.shape[1]
         if self.ep_size > 1:
-            disp = _AllToAll.apply(disp, self.ep_group)  # now [ep(src), E_local, C, H]
-            local = disp.view(self.ep_size, self.num_local_experts, C, H).transpose(0, 1).reshape(
-                self.num_local_experts, self.ep_size * C, H)
+            disp = _AllToAll.apply(disp.contiguous(), self.ep_group)  # now [ep(src), E_local, Cl, H]
+            local = disp.view(self.ep_size, self.num_local_experts, Cl, H).transpose(0, 1)
         else:
-            local = disp.view(E, C, H)
-        y = self.experts(local)
+            local = disp.view(1, E, Cl, H).transpose(0, 1)  # [E_local, 1, Cl, H]
+        if sharded:  # TP-sharded experts see every slot of their experts (gathered over the TP ranks)
+            local = gather_tokens(local, 2, partial_grad=isinstance(self.experts, GroupedSwiGLUExperts))
+        Cx = local.shape[2]
+        y = self.experts(local.reshape(self.num_local_experts, self.ep_size * Cx, H)).view(
+            self.num_local_experts, self.ep_size, Cx, H)
+        if sharded:
+            if isinstance(self.experts, GroupedSwiGLUExperts):
+                y = _ReduceScatterTokens.apply(y, 2)  # partial sums -> this rank's summed slots
+            else:  # a TP-aware user expert reduced internally: keep this rank's slots
+                y = drop_tokens(y, 2)
+        y = y.transpose(0, 1).contiguous()  # [ep, E_local, Cl, H]
         if self.ep_size > 1:
-            y = y.view(self.num_local_experts, self.ep_size, C, H).transpose(0, 1).reshape(E * C, H)
-            y = _AllToAll.apply(y.contiguous(), self.ep_group)
-        else:
-            y = y.reshape(E * C, H)
+            y = _AllToAll.apply(y, self.ep_group)
+        y = y.view(E, Cl, H)
+        if sharded:
+            y = gather_tokens(y, 1)
+        y = y.reshape(E * C, H)
         out = moe_combine(y, expert, pos, w, C)
         self.l_aux, self.exp_counts = l_aux, counts
         return out.view(shape)
@@ -218,14 +347,23 @@ class MoE(nn.Module):
             if groups._State.topo is None:
                 groups.initialize()
             groups._create_expert_and_data_parallel(ep_size)
+        # expert tensor parallelism (reference moe/layer.py:52-58, sharded_moe.py:609-660): with a TP dense model
+        # the EP groups already pair ranks of equal TP coordinate (utils/groups.py), so each TP rank's all-to-all
+        # carries 1/tp of the slots and the experts are sharded over the same TP group
+        tp = _tp()[1]
+        self.enable_expert_tensor_parallelism = bool(enable_expert_tensor_parallelism) and tp > 1
         if expert is None:
             experts = GroupedSwiGLUExperts(hidden_size, expert_intermediate_size or 4 * hidden_size,
-                                           self.num_local_experts, self.expert_group_name)
+                                           self.num_local_experts, self.expert_group_name,
+                                           tp_size=tp if self.enable_expert_tensor_parallelism else 1)
         else:
+            # a user expert under expert TP must be TP-aware itself (a Megatron-style MLP that all-reduces its
+            # output), exactly as in the reference
             experts = Experts(expert, self.num_local_experts, self.expert_group_name)
         gate = TopKGate(hidden_size, num_experts, k, capacity_factor, eval_capacity_factor, min_capacity,
                         noisy_gate_policy, drop_tokens, use_rts, None, top2_2nd_expert_sampling)
-        self.deepspeed_moe = MOELayer(gate, experts, self.expert_group_name, ep_size, self.num_local_experts)
+        self.deepspeed_moe = MOELayer(gate, experts, self.expert_group_name, ep_size, self.num_local_experts,
+                                      expert_tp=self.enable_expert_tensor_parallelism)
         gate.ep_group = self.deepspeed_moe.ep_group
         self.use_residual = use_residual
         if use_residual:

@@ -243,3 +243,58 @@ def _moe_ckpt(rank, world, ep, stage, d):
 @pytest.mark.parametrize("stage", [0, 2, 3])
 def test_moe_checkpoint_roundtrip_and_consolidation(tmp_path, stage):
     run_distributed(_moe_ckpt, 4, 2, stage, str(tmp_path))
+
+
+def _expert_tp(rank, world, cf):
+    """EP=2 x expert-TP=2 on 4 ranks (TP dense model: tokens replicated over each TP pair) against the unsharded
+    MoE run on every data-parallel rank's tokens."""
+    from hcache_deepspeed_amd.parallel.moe import MoE
+    from hcache_deepspeed_amd.utils import groups
+    groups.initialize(tp=2)
+    tp_rank, dp_rank = groups.get_tensor_model_parallel_rank(), groups.get_data_parallel_rank()
+    H, I, E, T = 16, 24, 4, 7
+    torch.manual_seed(0)
+    full_w13 = torch.randn(E, 2 * I, H) * 0.2
+    full_w2 = torch.randn(E, H, I) * 0.2
+    wg = torch.randn(E, H)
+    kw = dict(k=2, capacity_factor=cf, eval_capacity_factor=cf, min_capacity=1, use_rts=False,
+              expert_intermediate_size=I)
+    moe = MoE(H, None, E, ep_size=2, enable_expert_tensor_parallelism=True, **kw)
+    ex = moe.deepspeed_moe.experts
+    assert moe.enable_expert_tensor_parallelism and ex.tp_size == 2 and ex.w2.shape == (2, H, I // 2)
+    ep_rank = dp_rank  # EP groups pair ranks of equal TP coordinate
+    ex.load_full(full_w13[2 * ep_rank:2 * ep_rank + 2], full_w2[2 * ep_rank:2 * ep_rank + 2], tp_rank)
+    with torch.no_grad():
+        moe.deepspeed_moe.gate.wg.weight.copy_(wg)
+    xs = [torch.randn(T, H, generator=torch.Generator().manual_seed(100 + d)) for d in range(2)]
+    x = xs[dp_rank].clone().requires_grad_(True)
+    out, _, _ = moe(x)
+    out.sum().backward()
+
+    ref = MoE(H, None, E, ep_size=1, **kw)
+    with torch.no_grad():
+        ref.deepspeed_moe.experts.w13.copy_(full_w13)
+        ref.deepspeed_moe.experts.w2.copy_(full_w2)
+        ref.deepspeed_moe.gate.wg.weight.copy_(wg)
+    xr = [t.clone().requires_grad_(True) for t in xs]
+    outs = [ref(t)[0] for t in xr]
+    assert torch.allclose(out, outs[dp_rank], atol=1e-5, rtol=1e-4), (out - outs[dp_rank]).abs().max()
+    sum(o.sum() for o in outs).backward()
+    assert torch.allclose(x.grad, xr[dp_rank].grad, atol=1e-5, rtol=1e-4)
+    probe = GroupedSwiGLUExperts_shard(ref.deepspeed_moe.experts, 2 * ep_rank, tp_rank)
+    assert torch.allclose(ex.w13.grad, probe[0], atol=1e-4, rtol=1e-4)
+    assert torch.allclose(ex.w2.grad, probe[1], atol=1e-4, rtol=1e-4)
+
+
+def GroupedSwiGLUExperts_shard(full, e0, tp_rank, tp=2):
+    """This (EP, TP) rank's slice of the unsharded experts' weight gradients."""
+    I = full.w2.shape[-1]
+    i = I // tp
+    lo = tp_rank * i
+    g13 = full.w13.grad[e0:e0 + 2]
+    return (torch.cat([g13[:, lo:lo + i], g13[:, I + lo:I + lo + i]], 1), full.w2.grad[e0:e0 + 2, :, lo:lo + i])
+
+
+@pytest.mark.parametrize("cf", [16.0, 0.6])  # no drops / drops with a capacity padded to the TP size
+def test_expert_tensor_parallel_matches_unsharded(cf):
+    run_distributed(_expert_tp, 4, cf)
