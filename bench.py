@@ -74,6 +74,9 @@ def main():
     from hcache_deepspeed_amd.models import gpt2, llama, mixtral
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        # RCCL records start/end events per collective so the bench can report in-step AG/RS busbw (no sync)
+        os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
     if world > 1 or "RANK" in os.environ:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     else:
@@ -115,7 +118,7 @@ def main():
                                                    "weight_decay": 0.1}},
         "gradient_clipping": 1.0,
         "zero_optimization": {"stage": args.zero},
-        "mi355x": {"zero3_prefetch_depth": args.prefetch, "host_act_cache": {"enabled": bool(args.host_act_cache),
+        "mi355x": {"zero3_prefetch_depth": args.prefetch, "comm_stats": world > 1, "host_act_cache": {"enabled": bool(args.host_act_cache),
                                                                         "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }
@@ -172,6 +175,9 @@ def main():
     tdist.barrier()
     sync()
     retries0 = torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) if on_gpu else 0
+    cs = getattr(engine.optimizer, "comm_stats", None)
+    if cs is not None:
+        cs.reset()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = train_step(args.warmup + i)
@@ -192,6 +198,24 @@ def main():
     mem = torch.cuda.max_memory_allocated(dev) / 2**30 if on_gpu else 0.0
     # caching-allocator retries in the timed steps: each one frees cached blocks after a device-wide synchronize
     retries = (torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) - retries0) if on_gpu else 0
+    comm = None
+    if world > 1:
+        # per-rank communication evidence of the timed steps (exposed wait, in-step busbw) and peak HBM
+        mine = {"rank": rank, "peak_mem_gib": round(mem, 1)}
+        if cs is not None:
+            summ = cs.summary()
+            mine["exposed_comm_ms_per_step"] = round(summ["exposed_ms"] / args.steps, 2)
+            mine["collectives"] = summ["collectives"]
+        per_rank = [None] * world
+        tdist.all_gather_object(per_rank, mine)
+        comm = {"backend": tdist.get_backend(), "ranks": world,
+                "exposed_comm_ms_per_step_max": max(r.get("exposed_comm_ms_per_step", 0.0) for r in per_rank),
+                "peak_mem_gib_per_rank": [r["peak_mem_gib"] for r in per_rank],
+                "rank0": per_rank[0]}
+        for kind in ("all_gather", "reduce_scatter"):
+            bws = [r.get("collectives", {}).get(kind, {}).get("busbw_GBps") for r in per_rank]
+            bws = [b for b in bws if b]
+            comm[f"{kind}_busbw_GBps_min_over_ranks"] = min(bws) if bws else None
     if rank == 0:
         out = {
             "metric": ("tokens/sec (node) Llama-3-8B ZeRO-3 at 1/2/4/8 MI355X" if args.model == "llama3-8b" else
@@ -219,6 +243,8 @@ def main():
                       "tuned_gemm_table": tuned, "device": "mi355x" if on_gpu else "cpu-dry-run",
                       "alloc_retries_timed": int(retries)},
         }
+        if comm is not None:
+            out["extra"]["comm"] = comm
         ac = getattr(engine, "_activation_cache", None)
         if ac is not None:
             out["extra"]["act_cache"] = ac.stats()

@@ -173,6 +173,13 @@ class HostActCacheConfig:
     host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: min(40% of host RAM, 160 GiB))
 
 
+AUTO = -1
+
+
+def _auto_or(v, typ):
+    return AUTO if isinstance(v, str) and v.lower() == "auto" else typ(v)
+
+
 @dataclass
 class MI355XConfig:
     xgmi_bucket_mb: int = 256
@@ -184,6 +191,8 @@ class MI355XConfig:
     # ZeRO-3 all-gather / reduce-scatter communicators run their RCCL kernels on high-priority HIP streams, so
     # the few workgroups a collective needs are dispatched ahead of queued GEMM tiles (overlap under full load)
     comm_high_priority: bool = True
+    # per-step exposed-communication / busbw accounting of the ZeRO collectives (runtime/zero/comm_stats.py)
+    comm_stats: bool = False
     host_act_cache: HostActCacheConfig = field(default_factory=HostActCacheConfig)
 
 
@@ -299,9 +308,12 @@ class DeepSpeedConfig:
         m = c.get("mi355x") or {}
         hac = m.get("host_act_cache") or {}
         self.mi355x = MI355XConfig(
-            xgmi_bucket_mb=int(m.get("xgmi_bucket_mb", 256)), zero3_prefetch_depth=int(m.get("zero3_prefetch_depth", 2)),
+            # "auto": sized from an alpha-beta fit of the data-parallel all-gather measured at startup (AUTO = -1)
+            xgmi_bucket_mb=_auto_or(m.get("xgmi_bucket_mb", 256), int),
+            zero3_prefetch_depth=int(m.get("zero3_prefetch_depth", 2)),
             zero3_max_reduce_inflight=int(m.get("zero3_max_reduce_inflight", 2)),
-            zero3_unit_bucket_mb=float(m.get("zero3_unit_bucket_mb", 128)),
+            zero3_unit_bucket_mb=_auto_or(m.get("zero3_unit_bucket_mb", 128), float),
+            comm_stats=bool(m.get("comm_stats", False)),
             direct_wgrad=bool(m.get("direct_wgrad", True)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
             comm_high_priority=bool(m.get("comm_high_priority", True)),

@@ -1,0 +1,75 @@
+"""Per-step ZeRO collective accounting: how much communication the compute stream actually waited for, and what
+bandwidth the all-gathers / reduce-scatters achieved inside the real step.
+
+* **exposed time**: every place the ZeRO optimizer orders the compute stream after a collective
+  (``work.wait()`` in ``_gather`` / ``_release`` / ``_retire``) is bracketed by two HIP events on the compute
+  stream. Only the wait sits between them, so ``elapsed(before, after)`` is the GPU time compute was stalled on
+  communication. (On CPU / gloo, where ``wait()`` blocks the host, the host time of the wait is used.)
+* **collective time / busbw**: with ``TORCH_NCCL_ENABLE_TIMING=1`` RCCL records start/end events around every
+  collective kernel; ``Work._get_duration()`` reads them after the step. busbw uses the nccl-tests factors of
+  utils/comms_logging.py (all-gather and reduce-scatter: ``(n-1)/n`` of the full buffer per unit time).
+
+Enabled by ``mi355x.comm_stats`` (bench.py turns it on at N > 1). Reference counterpart: the comms logger's
+per-op latency/algbw/busbw (utils/comms_logging.py:33-178), which synchronizes around every op; this one does not
+synchronize inside the step.
+"""
+import time
+
+import torch
+
+
+class ZeroCommStats:
+
+    def __init__(self, device):
+        self.device = device
+        self.cuda = device.type == "cuda"
+        self.reset()
+
+    def reset(self):
+        self._waits = []  # (ev_before, ev_after) or host seconds
+        self._works = []  # (kind, total_bytes, world, work)
+        self.host_wait_s = 0.0
+
+    def issued(self, kind, total_bytes, world, work):
+        if world > 1 and work is not None:
+            self._works.append((kind, int(total_bytes), int(world), work))
+
+    def wait(self, work):
+        if not self.cuda:
+            t0 = time.perf_counter()
+            work.wait()
+            self.host_wait_s += time.perf_counter() - t0
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        work.wait()
+        e1.record()
+        self._waits.append((e0, e1))
+
+    def summary(self):
+        """Call after the step's work has completed (e.g. after ``torch.cuda.synchronize()``)."""
+        if self.cuda:
+            exposed_ms = sum(a.elapsed_time(b) for a, b in self._waits)
+        else:
+            exposed_ms = self.host_wait_s * 1e3
+        out = {"exposed_ms": round(exposed_ms, 3), "waits": len(self._waits) if self.cuda else None}
+        kinds = {}
+        for kind, nbytes, world, work in self._works:
+            d = kinds.setdefault(kind, {"count": 0, "bytes": 0, "timed_ms": 0.0, "timed_bytes_bus": 0.0,
+                                        "world": world})
+            d["count"] += 1
+            d["bytes"] += nbytes
+            try:
+                ms = float(work._get_duration())
+            except Exception:  # timing not enabled (TORCH_NCCL_ENABLE_TIMING) or not supported by the backend
+                ms = None
+            if ms is not None and ms > 0:
+                d["timed_ms"] += ms
+                d["timed_bytes_bus"] += nbytes * (world - 1) / world
+        for kind, d in kinds.items():
+            ms, bus = d.pop("timed_ms"), d.pop("timed_bytes_bus")
+            d["collective_ms"] = round(ms, 3) if bus else None
+            d["busbw_GBps"] = round(bus / (d["collective_ms"] * 1e-3) / 1e9, 1) if d["collective_ms"] else None
+            d["mean_msg_MiB"] = round(d["bytes"] / max(1, d["count"]) / 2**20, 2)
+        out["collectives"] = kinds
+        return out

@@ -248,6 +248,11 @@ class ZeroOptimizer:
             self.param_h2d_stream = torch.cuda.Stream(self.device, priority=-1)
         else:
             self.param_h2d_stream = None
+        self.comm_stats = None
+        if getattr(self.mi, "comm_stats", False):
+            from .comm_stats import ZeroCommStats
+            self.comm_stats = ZeroCommStats(self.device)
+        self._resolve_auto_buckets(dp_group)
         self._build_units(leaf_modules)
         self._build_store()
         self._install_hooks()
@@ -426,6 +431,37 @@ class ZeroOptimizer:
     def _ep_size(self, key):
         ep = groups._get_expert_parallel_group(key)
         return dist.get_world_size(ep) if ep is not None else 1
+
+    def _resolve_auto_buckets(self, dp_group):
+        """``xgmi_bucket_mb`` / ``zero3_unit_bucket_mb`` = "auto": measure the data-parallel all-gather at a few sizes,
+        fit t = alpha + bytes / beta (compile/profiler.py) and take the smallest bucket whose fixed cost alpha is
+        <= 5 % of its transfer time (bytes >= 20 * alpha * beta), clamped to [16 MiB, 1 GiB]. Point-to-point xGMI
+        rings have a per-hop latency that NVSwitch tuning does not account for; this measures it instead.
+        Without peers (dp = 1) the documented defaults (256 / 128 MiB) stay."""
+        from ..config import AUTO
+        self.auto_bucket_fit = None
+        keys = [k for k in ("xgmi_bucket_mb", "zero3_unit_bucket_mb") if getattr(self.mi, k, None) == AUTO]
+        if not keys:
+            return
+        mb = None
+        if self.dp_world > 1:
+            from ...compile.profiler import profile_allgather
+            fit = profile_allgather(dp_group, self.device, self.dtype)
+            self.auto_bucket_fit = fit.to_dict()
+            mb = min(1024.0, max(16.0, 20.0 * fit.alpha * fit.beta / 2**20))
+        for k in keys:
+            setattr(self.mi, k, (int(mb) if k == "xgmi_bucket_mb" else mb) if mb is not None else
+                    (256 if k == "xgmi_bucket_mb" else 128.0))
+        if mb is not None:
+            log_dist(f"ZeRO buckets from the measured all-gather (alpha {fit.alpha * 1e6:.1f} us, beta "
+                     f"{fit.beta / 1e9:.1f} GB/s): {mb:.0f} MiB for {', '.join(keys)}", ranks=[0])
+
+    def _cwait(self, work):
+        """Order the compute stream after a collective (accounted as exposed communication when enabled)."""
+        if self.comm_stats is not None:
+            self.comm_stats.wait(work)
+        else:
+            work.wait()
 
     def _build_units(self, leaf_modules):
         group_of = self._group_of()
@@ -866,13 +902,15 @@ class ZeroOptimizer:
                 u.work, u.post_gather = self._qwz_gather(u, full)
             else:
                 u.work = self._all_gather(full, u.shard_tensor, u.ag_group)
+                if self.comm_stats is not None:
+                    self.comm_stats.issued("all_gather", full.numel() * full.element_size(), u.world, u.work)
             u.full = full
             u.bind_params(full)
             u.status = INFLIGHT
             self.ag_issued += 1
             self._note_live()
         if wait and u.status == INFLIGHT:
-            u.work.wait()
+            self._cwait(u.work)
             u.work = None
             if getattr(u, "post_gather", None) is not None:
                 u.post_gather()
@@ -891,7 +929,7 @@ class ZeroOptimizer:
         if u.persistent or not self._partitioned(u) or u.status == NOT_AVAILABLE:
             return
         if u.status == INFLIGHT:
-            u.work.wait()
+            self._cwait(u.work)
             u.work = None
             u.post_gather = None
         elif self.hpz > 1 and not self.in_backward and u.expert_key is None and u.full is not None:
@@ -1029,14 +1067,13 @@ class ZeroOptimizer:
                 if u.grad_full is not None and not u.direct:
                     self._reset_grad_buffer(u)
 
-    @staticmethod
-    def _retire(queue, limit):
+    def _retire(self, queue, limit):
         """Wait on (and post-process) the oldest queued reductions until at most ``limit`` remain.
         On RCCL ``wait()`` only orders the compute stream after the collective, so this does not block the
         host; dropping the entry then returns its unsharded gradient buffer to the allocator."""
         while len(queue) > limit:
             item = queue.pop(0)
-            item[0].wait()
+            self._cwait(item[0])
             if item[1] is not None:
                 item[1]()
 
@@ -1092,6 +1129,8 @@ class ZeroOptimizer:
                 post = (lambda d=dst, t=tmp: d.copy_(t))
             else:
                 post = (lambda d=dst, t=tmp: d.add_(t))
+        if self.comm_stats is not None:
+            self.comm_stats.issued("reduce_scatter", src.numel() * src.element_size(), u.world, w)
         self._after_reduce(u, src, w, post, (src, ))
 
     def _after_reduce(self, u, src, w, post, keep):
@@ -1415,9 +1454,12 @@ class ZeroOptimizer:
                 continue  # aliased / re-gathered on demand by the next forward
             if u.full is None:
                 continue
-            works.append(dist.all_gather_into_tensor(u.full, u.shard_tensor, group=u.ag_group, async_op=True))
+            w = dist.all_gather_into_tensor(u.full, u.shard_tensor, group=u.ag_group, async_op=True)
+            if self.comm_stats is not None:
+                self.comm_stats.issued("all_gather", u.full.numel() * u.full.element_size(), u.world, w)
+            works.append(w)
         for w in works:
-            w.wait()
+            self._cwait(w)
 
     def get_global_norm(self):
         if self.global_norm is None:

@@ -175,6 +175,13 @@ def test_bench_torchrun_cpu_dry_run():
     assert out["n_gpus"] == 4 and out["steps"] == 2 and out["warmup"] == 1
     assert out["config"]["global_batch"] == 8 and out["config"]["parallelism"] == "zero3-dp4"
     assert out["value"] > 0 and out["extra"]["valid"] is False
+    # communication evidence the driver's N>1 runs carry (exposed wait, per-collective traffic, per-rank HBM)
+    comm = out["extra"]["comm"]
+    assert comm["ranks"] == 4 and len(comm["peak_mem_gib_per_rank"]) == 4
+    assert comm["exposed_comm_ms_per_step_max"] >= 0
+    coll = comm["rank0"]["collectives"]
+    assert coll["all_gather"]["count"] > 0 and coll["reduce_scatter"]["count"] > 0
+    assert coll["all_gather"]["bytes"] > 0 and coll["reduce_scatter"]["world"] == 4
 
 
 def test_memory_plan_bench_configs():
