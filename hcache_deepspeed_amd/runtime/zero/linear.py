@@ -53,12 +53,55 @@ def grad_accumulator(w, dtype):
 _FWD_GEMM = __import__("os").environ.get("HDS_GEMM_FWD", "0") == "1"  # experiment: hand-written MFMA fwd GEMM
 
 
+_FWD_SPLIT = __import__("os").environ.get("HDS_FWD_SPLIT", "auto")  # auto | off | on
+_FWD_CHOICE = {}
+
+
+def _col_split(n):
+    """Output-column split of an N that is not a multiple of the 4096-wide tiles hipBLASLt runs best (the fused
+    Llama-3 qkv projection, N = 6144 = 4096 + 2048), or None."""
+    if n <= 4096 or n % 4096 == 0 or (n % 4096) % 256:
+        return None
+    return n - n % 4096
+
+
+def _split_fwd(x2, weight, n1):
+    """y[:, :n1] = x W[:n1]^T and y[:, n1:] = x W[n1:]^T as two GEMMs writing column slices of ONE output (row
+    stride N: no concatenation copy)."""
+    y = torch.empty(x2.shape[0], weight.shape[0], dtype=x2.dtype, device=x2.device)
+    torch.mm(x2, weight[:n1].t(), out=y[:, :n1])
+    torch.mm(x2, weight[n1:].t(), out=y[:, n1:])
+    return y
+
+
+def _time(fn):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
 def _linear_fwd(x, weight, bias):
     if _FWD_GEMM and bias is None and x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16:
         from ...ops.gemm import gemm_nt, gemm_nt_supported
         x2 = x.reshape(-1, x.shape[-1])
         if gemm_nt_supported(x2.shape[0], weight.shape[0], x2.shape[1]) and x2.is_contiguous():
             return gemm_nt(x2, weight).view(*x.shape[:-1], weight.shape[0])
+    n1 = _col_split(weight.shape[0])
+    if (n1 is not None and _FWD_SPLIT != "off" and bias is None and x.is_cuda and x.dtype == weight.dtype
+            and x.is_contiguous() and weight.is_contiguous()):
+        x2 = x.reshape(-1, x.shape[-1])
+        key = (x2.shape[0], weight.shape[0], x2.shape[1], x.dtype)
+        split = _FWD_CHOICE.get(key) if _FWD_SPLIT == "auto" else True
+        if split is None:  # timed once per shape: the split wins where hipBLASLt's pick for the odd N is slow
+            t_fused = _time(lambda: F.linear(x2, weight))
+            t_split = _time(lambda: _split_fwd(x2, weight, n1))
+            split = _FWD_CHOICE[key] = t_split < 0.97 * t_fused
+        if split:
+            return _split_fwd(x2, weight, n1).view(*x.shape[:-1], weight.shape[0])
     return F.linear(x, weight, bias)
 
 

@@ -143,3 +143,15 @@ def test_grad_clip_cpu():
     assert math.isclose(s.item(), 52.0)
     c = clip_coef(s, 1.0)
     assert abs(c.item() - 1 / math.sqrt(52.0)) < 1e-5
+
+
+def test_split_column_forward_matches_fused_linear():
+    """The odd-N projection forward (two GEMMs into column slices of one output) equals F.linear."""
+    import torch.nn.functional as F
+    from hcache_deepspeed_amd.runtime.zero.linear import _col_split, _split_fwd
+    assert _col_split(6144) == 4096 and _col_split(4096) is None and _col_split(8192) is None
+    assert _col_split(4096 + 100) is None and _col_split(14336 * 2) is None
+    torch.manual_seed(0)
+    x = torch.randn(33, 64)
+    w = torch.randn(6144, 64)
+    torch.testing.assert_close(_split_fwd(x, w, 4096), F.linear(x, w))

@@ -38,5 +38,22 @@ def main():
                                                                 for k, v in r.items()}))
 
 
+
+
+def slices():
+    """The framework's split forward (two GEMMs into column slices of one output) vs fused, at the bench shape."""
+    from hcache_deepspeed_amd.runtime.zero.linear import _split_fwd
+    T, K, N = 28672, 4096, 6144
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+    ref = F.linear(x, w)
+    got = _split_fwd(x, w, 4096)
+    assert torch.equal(ref, got) or (ref.float() - got.float()).abs().max().item() < 1e-2
+    fl = 2 * T * N * K
+    r = {"fused_ms": t(lambda: F.linear(x, w)), "split_slices_ms": t(lambda: _split_fwd(x, w, 4096))}
+    print(json.dumps({k: round(v, 4) for k, v in r.items()} | {k.replace("_ms", "_PFs"): round(fl / v / 1e12, 3)
+                                                                for k, v in r.items()}))
+
+
 if __name__ == "__main__":
-    main()
+    slices() if "--slices" in sys.argv else main()
