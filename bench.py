@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--offload-param", action="store_true")
     ap.add_argument("--nvme-path", default="/tmp/hds_nvme", help="swap folder of the NVMe tier (--offload nvme)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
+    ap.add_argument("--offload-opt-states", action="store_true",
+                    help="DeepCompile offload_adam_states: Adam moments + fp32 master on pinned host between steps")
     ap.add_argument("--deepcompile", action="store_true",
                     help="engine.compile() with DeepCompile: profiled ZeRO-3 gather schedule (selective gather + prefetch)")
     args = ap.parse_args()
@@ -122,8 +124,8 @@ def main():
                                                                         "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }
-    if args.deepcompile:
-        ds_config["compile"] = {"deepcompile": True}
+    if args.deepcompile or args.offload_opt_states:
+        ds_config["compile"] = {"deepcompile": bool(args.deepcompile), "offload_opt_states": bool(args.offload_opt_states)}
     if args.offload != "none":
         ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True}
         if args.offload_param:
@@ -139,7 +141,7 @@ def main():
     if args.ckpt:
         model.gradient_checkpointing_enable()
     engine, _, _, _ = hds.initialize(model=model, config=ds_config)
-    if args.deepcompile:
+    if args.deepcompile or args.offload_opt_states:
         engine.compile()  # schedule compiled after the profiled warmup step (compile/backend.py)
     t_init = time.time() - t_init
     dev = engine.device
@@ -245,6 +247,10 @@ def main():
         }
         if comm is not None:
             out["extra"]["comm"] = comm
+        so = getattr(engine.optimizer, "state_offload", None)
+        if so is not None:
+            out["extra"]["offload_opt_states"] = so.stats()
+            out["config"]["offload_opt_states"] = True
         ac = getattr(engine, "_activation_cache", None)
         if ac is not None:
             out["extra"]["act_cache"] = ac.stats()

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as tdist
 
 from ..utils.logging import log_dist
-from .passes import CompiledSchedule, UnitGraph, compile_schedule, zero1_compile
+from .passes import CompiledSchedule, UnitGraph, compile_schedule, plan_state_offload, plan_state_reload
 from .profiler import CommPredictor, UnitProbe, combine, profile_allgather, profile_h2d
 
 
@@ -46,7 +46,8 @@ class DeepCompileBackend:
                        and getattr(self.opt, "partitioned", False))
         if not self.active:
             self.times["zero1_compile" if getattr(self.opt, "stage", 0) in (1, 2) else "zero3_compile"] = 0.0
-            self.meta = zero1_compile(getattr(self.opt, "stage", 0))
+            self.meta = {"stage": getattr(self.opt, "stage", 0), "schedule": None,
+                         "note": "nothing gathered (ZeRO-1/2, or dp = 1 without parameter offload)"}
             return
         self.probe = UnitProbe(self.opt.device)
 
@@ -113,12 +114,24 @@ class DeepCompileBackend:
         self.graph = UnitGraph(fwd, bwd, nbytes, gathered, peak, total)
         sched = compile_schedule(self.graph, self.predictor, self.margin, self.mem_budget, self.max_buffered,
                                  self.selective)
+        so = getattr(opt, "state_offload", None)
+        if so is not None and dev.type == "cuda":
+            # offload_adam_states: the reload goes where the remaining backward covers the measured H2D time
+            h2d = profile_h2d(dev, torch.float32)
+            nbytes_states = so.state_bytes()
+            limit = total * (1.0 - self.margin) if total else None
+            pos, rstats = plan_state_reload(self.graph, nbytes_states, h2d, mem_limit=limit)
+            sched.meta["offload_adam_states"] = {"reload": rstats,
+                                                 "offload": plan_state_offload(self.graph, nbytes_states, h2d)}
+            sched.meta["offload_adam_states"]["reload_pos"] = pos
         obj = [sched.to_dict()]
         src = tdist.get_global_rank(group, 0) if group is not None else 0
         tdist.broadcast_object_list(obj, src=src, group=group)
         sched = CompiledSchedule.from_dict(obj[0])
         self.times["passes"] = time.perf_counter() - t0
         opt.install_schedule(sched)
+        if so is not None and "offload_adam_states" in sched.meta:
+            so.reload_pos = sched.meta["offload_adam_states"]["reload_pos"]
         self.schedule = sched
         m = sched.meta
         log_dist(f"DeepCompile: {len(trace)} trace positions, resident units "

@@ -9,8 +9,10 @@ Reference parity:
   * compile/passes/prefetch.py -- reorders all-gathers earlier under a memory limit (``schedule_prefetch``
     below). The reference walks the FX graph backwards and fuses small gathers; fetch units here are already
     flat, coalesced buffers (one all-gather per unit), so the pass only decides WHERE each gather is issued;
-  * compile/passes/zero1_compile.py -- ZeRO-1 gradient reduction placement; the flat ZeRO-1/2 reduce already
-    runs per unit as each unit's gradients complete, so ``zero1_compile`` only reports that.
+  * compile/passes/offload_adam_states.py -- optimizer states to pinned host after the step, back during the
+    late backward (``plan_state_reload`` / ``plan_state_offload`` below, executed by
+    runtime/zero/state_offload.py). ZeRO-1 needs no schedule here: its flat reduce already runs per unit as each
+    unit's gradients complete (the reference's zero1_compile inserts exactly that).
 
 MI355X design: the pass works on measured costs -- per-position compute seconds and live HBM bytes from
 ``UnitProbe`` and an alpha-beta RCCL all-gather model -- and simulates the single all-gather stream (RCCL runs
@@ -60,14 +62,64 @@ class CompiledSchedule:
         return cls(d["fwd_prefetch"], d["bwd_prefetch"], d["resident"], d.get("meta"))
 
 
-def zero3_compile(graph):
-    """The gather/release program: every gathered unit is fetched at its use and released after it."""
-    return {"gathers_fwd": sum(1 for _, uid, _, _ in graph.fwd if uid in graph.gathered),
-            "gathers_bwd": sum(1 for _, uid, _, _ in graph.bwd if uid in graph.gathered)}
+def zero3_compile(graph, resident=()):
+    """The gather/release program of one step (reference zero3_compile.py inserts ``allgather_param`` before a
+    parameter's first use in a graph and ``release_param`` after its last): a list of
+    ``(phase, index, op, uid)`` with op in {"gather", "release"}, ``index`` the position in that phase's
+    execution order. A unit used several times in a phase is gathered once before its first use and released
+    after its last; ``resident`` units skip the release after their forward and the gather before their backward.
+    Returns (program, counts)."""
+    prog = []
+    counts = {"gathers_fwd": 0, "gathers_bwd": 0, "releases_fwd": 0, "releases_bwd": 0}
+    for phase, seq in (("fwd", graph.fwd), ("bwd", graph.bwd)):
+        first, last = {}, {}
+        for k, (_, uid, _, _) in enumerate(seq):
+            if uid in graph.gathered:
+                first.setdefault(uid, k)
+                last[uid] = k
+        for k, (_, uid, _, _) in enumerate(seq):
+            if uid not in graph.gathered:
+                continue
+            skip_gather = phase == "bwd" and uid in resident
+            skip_release = phase == "fwd" and uid in resident
+            if first[uid] == k and not skip_gather:
+                prog.append((phase, k, "gather", uid))
+                counts[f"gathers_{phase}"] += 1
+            if last[uid] == k and not skip_release:
+                prog.append((phase, k, "release", uid))
+                counts[f"releases_{phase}"] += 1
+    return prog, counts
 
 
-def zero1_compile(stage):
-    return {"stage": stage, "note": "flat per-unit reduce already issued as each unit's gradients complete"}
+def plan_state_reload(graph, state_bytes, h2d, margin=0.2, mem_limit=None):
+    """Placement of the optimizer-state reload (reference offload_adam_states.py: reload tasks in the backward
+    graph, early enough to land before the step). Walk the backward from its end and take the LATEST position whose
+    remaining backward compute covers the predicted H2D time ``h2d(state_bytes)`` with ``margin`` -- the states
+    then hold HBM for as short a time as possible. A position whose live bytes plus the states would exceed
+    ``mem_limit`` is skipped towards the end (less hiding, never an OOM). Returns (forward trace position or None,
+    stats)."""
+    if not graph.bwd or state_bytes <= 0:
+        return None, {"h2d_s": 0.0, "covered_s": 0.0}
+    t = h2d(state_bytes) * (1.0 + margin)
+    tail = 0.0
+    k = len(graph.bwd) - 1
+    while k > 0 and tail < t:
+        tail += graph.bwd[k][2]
+        k -= 1
+    while mem_limit is not None and k < len(graph.bwd) - 1 and \
+            any(m + state_bytes > mem_limit for _, _, _, m in graph.bwd[k:]):
+        tail -= graph.bwd[k + 1][2]
+        k += 1
+    return graph.bwd[k][0], {"h2d_s": t / (1.0 + margin), "covered_s": tail + graph.bwd[k][2],
+                             "bwd_index": k, "state_bytes": int(state_bytes)}
+
+
+def plan_state_offload(graph, state_bytes, d2h):
+    """Offload side of the same pass: the D2H is issued right after ``step()`` and overlaps the forward; report how
+    much of it the forward's compute covers (the rest delays the release, not compute)."""
+    fwd_s = sum(s for _, _, s, _ in graph.fwd)
+    t = d2h(state_bytes) if state_bytes > 0 else 0.0
+    return {"d2h_s": t, "forward_s": fwd_s, "hidden_frac": 1.0 if t <= 0 else min(1.0, fwd_s / t)}
 
 
 def selective_gather(graph, predictor, margin=0.1, mem_budget=None):
@@ -173,13 +225,15 @@ def schedule_prefetch(seq, predictor, nbytes, mem_limit=None, max_buffered=None)
 def compile_schedule(graph, predictor, margin=0.1, mem_budget=None, max_buffered=None, selective=True):
     """Run the passes in the reference's order (zero3 -> selective gather -> prefetch) and build the
     ``CompiledSchedule`` the optimizer executes."""
-    meta = {"zero3": zero3_compile(graph)}
     resident, used = (selective_gather(graph, predictor, margin, mem_budget) if selective else (set(), 0))
+    prog, counts = zero3_compile(graph, resident)
+    meta = {"zero3": counts}
     meta["selective_gather"] = {"resident_units": len(resident), "resident_bytes": used}
     limit = graph.total_mem * (1.0 - margin) - used if graph.total_mem else None
-    fwd_seq = [(pos, uid, s, m, uid in graph.gathered) for pos, uid, s, m in graph.fwd]
-    bwd_seq = [(pos, uid, s, m + used, uid in graph.gathered and uid not in resident)
-               for pos, uid, s, m in graph.bwd]
+    # a phase position needs a collective exactly where the gather/release program gathers
+    gat = {(ph, k) for ph, k, op, _ in prog if op == "gather"}
+    fwd_seq = [(pos, uid, s, m, ("fwd", k) in gat) for k, (pos, uid, s, m) in enumerate(graph.fwd)]
+    bwd_seq = [(pos, uid, s, m + used, ("bwd", k) in gat) for k, (pos, uid, s, m) in enumerate(graph.bwd)]
     fwd_plan, fstats = schedule_prefetch(fwd_seq, predictor, graph.nbytes, limit, max_buffered)
     bwd_plan, bstats = schedule_prefetch(bwd_seq, predictor, graph.nbytes, limit, max_buffered)
     meta["prefetch"] = {"fwd": fstats, "bwd": bstats}

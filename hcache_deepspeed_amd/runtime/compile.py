@@ -15,9 +15,9 @@ already a runtime mechanism of the engine, driven by the module-execution trace 
   * selective gather                            -> persistent small units (``stage3_param_persistence_threshold``);
   * offload_activation                          -> HCache host activation cache (offload/activation_cache.py):
     saved activations go D2H into pinned rings on a side stream, prefetched back in backward;
-  * offload_opt_states                          -> optimizer states move to pinned host right after
-    ``step()`` and return asynchronously at the start of the next forward (runtime/zero/offload_states.py),
-    overlapped with the forward of the first units;
+  * offload_opt_states                          -> optimizer states (and the fp32 master) move to pinned host
+    right after ``step()`` on a copy stream and come back during the late backward, at the trace position the
+    ``plan_state_reload`` pass picks from the profiled step (runtime/zero/state_offload.py);
   * offload_parameters                          -> ZeRO-Infinity parameter offload (configured at init);
   * double_buffer / symmetric_memory            -> RCCL reduce-scatter buckets are already double-buffered per
     unit; symmetric memory has no RCCL analogue here and is ignored with a warning.
@@ -83,7 +83,10 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
         engine._activation_cache = HostActivationCache.from_config(hc, engine.device).attach(engine.module)
     times["offload_activation"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    engine._dc_offload_opt_states = bool(cfg.offload_opt_states)
+    if cfg.offload_opt_states:
+        assert engine.optimizer is not None and hasattr(engine.optimizer, "enable_state_offload"), \
+            "offload_opt_states needs the ZeRO optimizer"
+        engine.optimizer.enable_state_offload(include_master=bool((compile_kwargs or {}).get("offload_master", True)))
     times["offload_adam_states"] = time.perf_counter() - t0
     if cfg.offload_parameters and not engine._config.zero_config.offload_param.enabled:
         logger.warning("compile: offload_parameters requires zero_optimization.offload_param at initialize(); "

@@ -380,9 +380,6 @@ class DeepSpeedEngine(nn.Module):
                 kwargs["curriculum_seqlen"] = d
         if self.progressive_layer_drop is not None and self.module.training:
             kwargs.update(self.progressive_layer_drop.get_state())
-        if getattr(self, "_dc_states_offloaded", False):
-            self.reload_states(non_blocking=True)  # DeepCompile offload_opt_states: bring states back
-            self._dc_states_offloaded = False
         if self.optimizer is not None:
             self.optimizer.pre_forward()
         ctx = self._activation_cache.forward_context() if (self._activation_cache is not None and
@@ -452,9 +449,6 @@ class DeepSpeedEngine(nn.Module):
                 self.timers.log([FORWARD_MICRO_TIMER, BACKWARD_MICRO_TIMER, STEP_MICRO_TIMER])
         if boundary and getattr(self, "_dc_backend", None) is not None:
             self._dc_backend.on_step_end()
-        if boundary and getattr(self, "_dc_offload_opt_states", False):
-            self.offload_states(include=["optim_states"], non_blocking=True)
-            self._dc_states_offloaded = True
         self.micro_steps += 1
         self._force_boundary = None
         self.timers(STEP_MICRO_TIMER).stop()

@@ -248,6 +248,7 @@ class ZeroOptimizer:
             self.param_h2d_stream = torch.cuda.Stream(self.device, priority=-1)
         else:
             self.param_h2d_stream = None
+        self.state_offload = None  # DeepCompile offload_adam_states executor (runtime/zero/state_offload.py)
         self.comm_stats = None
         if getattr(self.mi, "comm_stats", False):
             from .comm_stats import ZeroCommStats
@@ -973,6 +974,8 @@ class ZeroOptimizer:
                 return
             if self.dc_probe is not None:
                 self.dc_probe.mark("bwd", i)
+            if self.state_offload is not None and self.boundary:
+                self.state_offload.on_backward_position(i)
             if self.dc_schedule is not None:
                 self._issue(self.dc_schedule.bwd_prefetch.get(i, ()))
                 return
@@ -1166,6 +1169,9 @@ class ZeroOptimizer:
     def prepare_backward(self, boundary):
         self.boundary = boundary
         self.in_backward = True
+        so = self.state_offload
+        if so is not None and boundary and (so.reload_pos is None or not self._fwd_trace or self._recording):
+            so.reload()  # no planned position: the whole backward hides the H2D
         for u in self.units:
             u.pending = u.requires_grad_count
             u.grads_reduced = False
@@ -1358,8 +1364,23 @@ class ZeroOptimizer:
         return self.param_groups[seg.group]
 
     @torch.no_grad()
+    def enable_state_offload(self, include_master=True):
+        """Optimizer states (and the fp32 master) live in pinned host memory between ``step()`` and the late
+        backward of the next step (compile ``offload_opt_states``)."""
+        if self.kind == "generic":
+            raise NotImplementedError("offload_opt_states needs a fused optimizer (Adam/Lion/Adagrad) over the flat store")
+        from .state_offload import OptimizerStateOffload
+        if self.state_offload is None:
+            self.state_offload = OptimizerStateOffload(self, include_master)
+        return self.state_offload
+
+    def _states_resident(self):
+        if self.state_offload is not None:
+            self.state_offload.wait()
+
     def step(self, closure=None):
         s = self.store
+        self._states_resident()
         inv = 1.0 / (self.layout_world_for_avg() * self.loss_scaler.loss_scale)
         self._norm_buf.zero_()
         self._inf_buf.zero_()
@@ -1401,6 +1422,8 @@ class ZeroOptimizer:
                                        g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
         self._post_step_gather()
         self.zero_grad()
+        if self.state_offload is not None:
+            self.state_offload.offload()  # D2H overlaps the next forward
         return True
 
     def layout_world_for_avg(self):
@@ -1495,6 +1518,7 @@ class ZeroOptimizer:
 
     def _ckpt_flats(self):
         """Store-sized fp32 tensors a checkpoint holds: the master weights and every optimizer moment."""
+        self._states_resident()
         d = OrderedDict(fp32=self.store.master)
         if self.kind == "generic":
             d.update(self._generic_flat_states())

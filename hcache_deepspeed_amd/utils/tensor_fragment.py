@@ -33,6 +33,8 @@ def _zopt(param):
 
 
 def _buffer(z, key):
+    if key != _GRAD and getattr(z, "state_offload", None) is not None:
+        z.state_offload.wait()
     s = z.store
     if key == _FP32:
         return s.master

@@ -113,3 +113,82 @@ def test_deepcompile_zero3_schedule(world, tmp_path):
         assert none["sched"]["fwd_prefetch"] or none["sched"]["bwd_prefetch"]
         # every rank executes the same plan (collective order must match)
         assert big["sched"] == load(0, 1, 10**12)["sched"]
+
+
+def test_zero3_program_gathers_once_and_skips_resident():
+    """The gather/release program: one gather before a unit's first use and one release after its last, per
+    phase; resident units keep their forward buffers (no forward release, no backward gather)."""
+    from hcache_deepspeed_amd.compile import UnitGraph, zero3_compile
+    fwd = [(0, 0, 1e-3, 0), (1, 1, 1e-3, 0), (2, 2, 1e-3, 0), (3, 1, 1e-3, 0)]  # unit 1 used twice
+    bwd = [(3, 1, 1e-3, 0), (2, 2, 1e-3, 0), (1, 1, 1e-3, 0), (0, 0, 1e-3, 0)]
+    g = UnitGraph(fwd, bwd, {0: 1, 1: 1, 2: 1}, {1, 2}, 0, 0)  # unit 0 persistent (never gathered)
+    prog, counts = zero3_compile(g)
+    assert counts == {"gathers_fwd": 2, "gathers_bwd": 2, "releases_fwd": 2, "releases_bwd": 2}
+    assert ("fwd", 1, "gather", 1) in prog and ("fwd", 3, "release", 1) in prog
+    assert ("fwd", 1, "release", 1) not in prog
+    _, counts = zero3_compile(g, resident={2})
+    assert counts == {"gathers_fwd": 2, "gathers_bwd": 1, "releases_fwd": 1, "releases_bwd": 2}
+
+
+def test_state_reload_placement():
+    """offload_adam_states: the reload is placed where the remaining backward compute covers the H2D time (with
+    margin), as late as possible; a memory limit pushes it later."""
+    from hcache_deepspeed_amd.compile import UnitGraph, plan_state_reload
+    fwd = [(i, i, 1e-3, 0) for i in range(10)]
+    bwd = [(i, i, 1e-3, 100) for i in reversed(range(10))]
+    g = UnitGraph(fwd, bwd, {i: 1 for i in range(10)}, set(range(10)))
+    # H2D 2.5 ms (+20 %): 3 ms of trailing backward compute -> issued 3 positions before the end
+    pos, st = plan_state_reload(g, 1000, _pred(0.0, 1000 / 2.5e-3))
+    assert pos == 3 and st["covered_s"] >= 3e-3 - 1e-12
+    # H2D longer than the whole backward: issued at its start
+    pos, _ = plan_state_reload(g, 1000, _pred(0.0, 1000 / 50e-3))
+    assert pos == 9
+    # live bytes 100 + states 1000 may not exceed 1050 at positions 9..5: the reload moves to position 4
+    bwd2 = [(i, i, 1e-3, 100 if i >= 5 else 10) for i in reversed(range(10))]
+    g2 = UnitGraph(fwd, bwd2, {i: 1 for i in range(10)}, set(range(10)))
+    pos, _ = plan_state_reload(g2, 1000, _pred(0.0, 1000 / 50e-3), mem_limit=1050)
+    assert pos == 4
+
+
+def _state_offload_run(rank, world, stage, out):
+    import os
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    res = {}
+    for off in (False, True):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(**TINY))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2, "bf16": {"enabled": True},
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}, "zero_optimization": {"stage": stage},
+               "compile": {"offload_opt_states": off}}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        if off:
+            eng.compile()
+        z = eng.optimizer
+        g = torch.Generator().manual_seed(5 + rank)
+        losses = []
+        for step in range(3):
+            for _ in range(2):
+                x = torch.randint(0, TINY["vocab_size"], (2, 12), generator=g)
+                loss = eng(x, labels=x)
+                eng.backward(loss)
+                eng.step()
+                losses.append(float(loss))
+            if off:  # between steps the moments and the fp32 master live on the host only
+                assert z.store.states["exp_avg"].numel() == 0 and z.store.master.numel() == 0
+                assert z.state_offload.n_offloads == step + 1
+        if off:
+            assert z.state_offload.n_reloads == 2  # the first step had nothing to bring back
+        res[off] = losses
+        from hcache_deepspeed_amd.utils.tensor_fragment import safe_get_full_fp32_param
+        p = next(iter(eng.module.parameters()))
+        res[f"w{off}"] = safe_get_full_fp32_param(p).clone()  # reloads on demand
+    assert res[False] == res[True]
+    assert torch.equal(res["wFalse"], res["wTrue"])
+
+
+@pytest.mark.parametrize("stage,world", [(3, 1), (3, 2), (1, 2)])
+def test_offload_adam_states_keeps_trajectory(stage, world):
+    """Optimizer states and the fp32 master offloaded after every step and reloaded in the next backward: the
+    training trajectory is bit-identical to keeping them resident (GAS=2: only the boundary step moves them)."""
+    run_distributed(_state_offload_run, world, stage, None)
