@@ -82,6 +82,8 @@ class InferenceEngineV2:
         self._model.set_kv_cache(self._kv)
         self._state_manager = DSStateManager(sm, self._kv)
         self._batch = RaggedBatchWrapper(sm, device, self._state_manager.max_blocks_per_seq)
+        from ...ops.paged import ROWS_PER_ATOM
+        self._batch.set_attention_geometry(self._model.n_q, self._model.n_kv, ROWS_PER_ATOM)
         log_dist(f"InferenceEngineV2: {self._kv.num_blocks} KV blocks of {sm.kv_block_size} tokens "
                  f"(tp={self._model.tp}, latent_mode={self._config.latent_mode})", ranks=[0])
 

@@ -244,6 +244,8 @@ class RaggedTransformer:
         return out
 
     def _prep(self, batch):
+        if getattr(batch, "atoms", None) is not None and batch.n_atoms is not None:
+            return  # built with the rest of the metadata (RaggedBatchWrapper.finalize, csrc/host/ragged_meta.cpp)
         atoms, n_atoms = build_atoms(batch.seq_meta_host, self.n_q, self.n_kv)
         batch.atoms = atoms.to(self.device, non_blocking=True)
         batch.n_atoms = n_atoms

@@ -257,31 +257,83 @@ class RaggedBatchWrapper:
         self._tokens.append(tokens.reshape(-1).to(torch.int64))
         self.current_tokens += n
 
+    def set_attention_geometry(self, n_q, n_kv, rows_per_atom):
+        """Lets ``finalize`` also build the paged-attention work atoms (the model's query/KV head counts)."""
+        self._geom = (int(n_q), int(n_kv), int(rows_per_atom))
+
+    def _pinned_slot(self, need):
+        """One of two rotating pinned int32 staging buffers; a slot is reused only after its H2D drained."""
+        slots = self.__dict__.setdefault("_slots", [None, None])
+        evs = self.__dict__.setdefault("_slot_events", [None, None])
+        i = self.__dict__.get("_slot_next", 0)
+        self._slot_next = i ^ 1
+        if evs[i] is not None:
+            evs[i].synchronize()
+        if slots[i] is None or slots[i].numel() < need:
+            slots[i] = torch.empty(max(need, 4096), dtype=torch.int32, pin_memory=self.device.type == "cuda")
+        return i, slots[i]
+
     def finalize(self):
-        n = self.current_tokens
-        pin = self.device.type == "cuda"
+        """Ship the batch description to the device: the native builder (csrc/host/ragged_meta.cpp) writes seq_meta,
+        token -> sequence / position maps, last-token rows, the KV block table and the attention atoms into ONE
+        pinned int32 buffer, sent with one async H2D copy into a persistent device buffer (plus one for the token
+        ids); the device tensors below are views of it."""
+        import ctypes
+        import numpy as np
+        from ...ops import native
+        S, T = len(self._seqs), self.current_tokens
+        mb = self.max_blocks
+        n_new = np.fromiter((nn for (_, nn, _) in self.seq_meta_host), dtype=np.int32, count=S)
+        seen = np.fromiter((sn for (_, _, sn) in self.seq_meta_host), dtype=np.int32, count=S)
+        blk_lists = [seq.kv_blocks for seq in self._seqs]
+        off = np.zeros(S + 1, dtype=np.int64)
+        if S:
+            off[1:] = np.cumsum([len(b) for b in blk_lists])
+        flat = np.fromiter((b for bl in blk_lists for b in bl), dtype=np.int32, count=int(off[-1]))
+        n_q, n_kv, rpa = getattr(self, "_geom", (1, 1, 1 << 30))
+        lib = native.host_lib()
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        need = ctypes.c_int64(0)
+        lib.hds_ragged_meta_build(P(n_new), P(seen), S, P(flat), P(off), mb, n_q, n_kv, rpa, None, 0,
+                                  ctypes.byref(need))
+        si, host = self._pinned_slot(int(need.value))
+        A = lib.hds_ragged_meta_build(P(n_new), P(seen), S, P(flat), P(off), mb, n_q, n_kv, rpa,
+                                      ctypes.c_void_p(host.data_ptr()), host.numel(), ctypes.byref(need))
+        if A < 0:
+            raise RuntimeError(f"ragged metadata builder failed ({A})")
+        n = int(need.value)
+        dev_buf = self.__dict__.get("_dev_meta")
+        if dev_buf is None or dev_buf.numel() < n:
+            dev_buf = self._dev_meta = torch.empty(max(n, 4096), dtype=torch.int32, device=self.device)
+        dev_buf[:n].copy_(host[:n], non_blocking=True)
         ids = torch.cat(self._tokens) if self._tokens else torch.zeros(0, dtype=torch.int64)
-        tok_seq = torch.empty(n, dtype=torch.int32)
-        tok_pos = torch.empty(n, dtype=torch.int32)
-        tables = torch.zeros(max(1, len(self._seqs)), self.max_blocks, dtype=torch.int32)
-        for i, ((q0, nn, seen), seq) in enumerate(zip(self.seq_meta_host, self._seqs)):
-            tok_seq[q0:q0 + nn] = i
-            tok_pos[q0:q0 + nn] = torch.arange(seen, seen + nn, dtype=torch.int32)
-            blks = seq.kv_blocks
-            if blks:
-                tables[i, :len(blks)] = torch.tensor(blks, dtype=torch.int32)
-        meta = torch.tensor(self.seq_meta_host if self.seq_meta_host else [(0, 0, 0)], dtype=torch.int32)
-        if pin:
-            ids, tok_seq, tok_pos, tables, meta = (t.pin_memory() for t in (ids, tok_seq, tok_pos, tables, meta))
-        self.tables_host = tables
+        if self.device.type == "cuda":
+            ids = ids.pin_memory()
+            ev = torch.cuda.Event()
+            ev.record()
+            self._slot_events[si] = ev
         self.input_ids = ids.to(self.device, non_blocking=True)
-        self.tok_seq = tok_seq.to(self.device, non_blocking=True)
-        self.tok_pos = tok_pos.to(self.device, non_blocking=True)
-        self.block_tables = tables.to(self.device, non_blocking=True)
-        self.seq_meta = meta.to(self.device, non_blocking=True)
-        # last token of each sequence (for logits)
-        last = [q0 + nn - 1 for (q0, nn, _) in self.seq_meta_host]
-        self.last_token_idx = torch.tensor(last if last else [0], dtype=torch.int64).to(self.device, non_blocking=True)
+        o = 0
+
+        def take(k, shape):
+            nonlocal o
+            v = dev_buf[o:o + k].view(*shape)
+            o += k
+            return v
+
+        self.seq_meta = take(3 * S, (S, 3))
+        self.tok_seq = take(T, (T, ))
+        self.tok_pos = take(T, (T, ))
+        self.last_token_idx = take(S, (S, ))
+        self.block_tables = take(S * mb, (S, mb))
+        self.atoms = take(3 * A, (A, 3)) if hasattr(self, "_geom") else None
+        self.n_atoms = int(A) if hasattr(self, "_geom") else None
+        self.tables_host = host[4 * S + 2 * T:4 * S + 2 * T + S * mb].view(S, mb).clone() if S else \
+            torch.zeros(1, mb, dtype=torch.int32)
+        if S == 0:  # keep 1-row shapes for empty batches (kernels never run on them)
+            self.seq_meta = torch.zeros(1, 3, dtype=torch.int32, device=self.device)
+            self.block_tables = torch.zeros(1, mb, dtype=torch.int32, device=self.device)
+            self.last_token_idx = torch.zeros(1, dtype=torch.int32, device=self.device)
 
     @property
     def sequences(self):

@@ -19,6 +19,9 @@ SIGS = {
     "hds_ring_stream_wait": (I, [P, I, P]),
     "hds_ring_query": (I, [P, I]),
     "hds_memcpy_async": (I, [P, P, Z, I, P]),
+    # ragged_meta.cpp
+    "hds_ragged_meta_size": (L, [I, L, I, L]),
+    "hds_ragged_meta_build": (L, [P, P, I, P, P, I, I, I, I, P, L, P]),
     # cpu_optim.cpp
     "hds_cpu_adam": (I, [P, P, I, P, P, P, L, F, F, F, F, F, F, F, I, F]),
     "hds_cpu_lion": (I, [P, P, I, P, P, L, F, F, F, F, F]),

@@ -98,3 +98,50 @@ def test_allocator_and_scheduling():
                                             SchedulingResult.BatchTokenLimitExceeded)
     assert eng.can_schedule([1, 2], [99, 1]) == SchedulingResult.Success
     assert eng.can_schedule([1], [64 * 3 + 1]) != SchedulingResult.Success
+
+
+def test_native_ragged_metadata_matches_python_reference():
+    """csrc/host/ragged_meta.cpp packs seq_meta / token maps / last rows / block tables / atoms exactly as the
+    Python reference (ops/paged.build_atoms and the per-sequence loops) would build them."""
+    import ctypes
+    import numpy as np
+    from hcache_deepspeed_amd.ops import native
+    from hcache_deepspeed_amd.ops.paged import build_atoms
+    lib = native.host_lib()
+    rng = np.random.default_rng(0)
+    n_q, n_kv, rpa, mb = 32, 8, 128, 6
+    for S in (0, 1, 5):
+        n_new = rng.integers(1, 70, S).astype(np.int32)
+        seen = rng.integers(0, 200, S).astype(np.int32)
+        blocks = [list(rng.integers(0, 1000, rng.integers(1, mb + 1))) for _ in range(S)]
+        off = np.zeros(S + 1, dtype=np.int64)
+        if S:
+            off[1:] = np.cumsum([len(b) for b in blocks])
+        flat = np.array([b for bl in blocks for b in bl], dtype=np.int32)
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        need = ctypes.c_int64(0)
+        out = np.zeros(1 << 16, dtype=np.int32)
+        A = lib.hds_ragged_meta_build(P(n_new), P(seen), S, P(flat), P(off), mb, n_q, n_kv, rpa, P(out),
+                                      out.size, ctypes.byref(need))
+        meta_host = []
+        q0 = 0
+        for i in range(S):
+            meta_host.append((q0, int(n_new[i]), int(seen[i])))
+            q0 += int(n_new[i])
+        T = q0
+        ref_atoms, nref = build_atoms(meta_host, n_q, n_kv)
+        assert A == nref and need.value == 4 * S + 2 * T + S * mb + 3 * A
+        o = 0
+        meta = out[o:o + 3 * S].reshape(S, 3); o += 3 * S
+        tok_seq = out[o:o + T]; o += T
+        tok_pos = out[o:o + T]; o += T
+        last = out[o:o + S]; o += S
+        tables = out[o:o + S * mb].reshape(S, mb); o += S * mb
+        atoms = out[o:o + 3 * A].reshape(A, 3)
+        assert meta.tolist() == [list(m) for m in meta_host]
+        for i, (q, n, sn) in enumerate(meta_host):
+            assert (tok_seq[q:q + n] == i).all() and tok_pos[q:q + n].tolist() == list(range(sn, sn + n))
+            assert last[i] == q + n - 1
+            assert tables[i, :len(blocks[i])].tolist() == blocks[i] and (tables[i, len(blocks[i]):] == 0).all()
+        if A:
+            assert atoms.tolist() == ref_atoms.tolist()
