@@ -132,7 +132,10 @@ class InferenceEngineV2:
             seq.pre_forward(tokens.numel())
             batch.insert_sequence(seq, tokens, do_checks=do_checks)
         batch.finalize()
-        logits, latents = self._model.forward(batch, capture_latents=capture_latents)
+        if self._model.decode_graph_eligible(batch, capture_latents):
+            logits, latents = self._model.forward_decode_graph(batch), None  # HIP-graph decode step
+        else:
+            logits, latents = self._model.forward(batch, capture_latents=capture_latents)
         split = []
         for (q0, n, _) in batch.seq_meta_host:
             split.append(latents[:, q0:q0 + n] if latents is not None else None)

@@ -22,6 +22,7 @@ HCache, as implemented here (with the defects fixed):
 * every family above implements the contract (the reference broke ``put`` for all non-Llama models).
 """
 import math
+import types
 
 import torch
 import torch.nn.functional as F
@@ -75,6 +76,10 @@ class RaggedTransformer:
             self.cos = self.sin = None
         self.kv_cache = None
         self.copy_stream = torch.cuda.Stream(device, priority=-1) if device.type == "cuda" else None
+        self._decode_graphs = {}
+        self._graph_pool = None
+        import os as _os
+        self.decode_graph_max_batch = int(_os.environ.get("HDS_V2_DECODE_GRAPH_MAX_B", "64"))
 
     def _build_modules(self, ec):
         """Compute modules chosen by the inference-v2 heuristics (modules/heuristics.py): the engine config's
@@ -262,6 +267,35 @@ class RaggedTransformer:
         return self.o_lin(o, L["o.w"], L["o.b"])
 
     # ------------------------------------------------------------------------------------------
+    def decode_graph_eligible(self, batch, capture_latents):
+        """A decode-only ragged batch (one new token per sequence) of a dense model without tensor parallelism:
+        its whole forward depends on the batch size alone, so it replays from a HIP graph captured per size."""
+        if (self.device.type != "cuda" or capture_latents or self.tp != 1 or self.spec.moe is not None
+                or self.decode_graph_max_batch <= 0):
+            return False
+        S = batch.current_sequences
+        return (0 < S <= self.decode_graph_max_batch and batch.current_tokens == S
+                and getattr(batch, "atoms", None) is not None and getattr(batch, "_dev_meta", None) is not None)
+
+    @torch.no_grad()
+    def forward_decode_graph(self, batch):
+        """Replay the decode step for ``batch.current_sequences`` sequences: the step's token ids and packed
+        metadata (same layout as ``RaggedBatchWrapper.finalize``) are copied into the graph's static buffers, the
+        graph replays every layer's kernels with one launch, and the logits are copied out. The first step of a
+        batch size runs the forward eagerly once (it writes the same KV the replay writes) and captures it."""
+        B = batch.current_sequences
+        g = self._decode_graphs.get(B)
+        n = batch.seq_meta.numel() + batch.tok_seq.numel() + batch.tok_pos.numel() + batch.last_token_idx.numel() \
+            + batch.block_tables.numel() + batch.atoms.numel()
+        if g is None:
+            g = self._decode_graphs[B] = _DecodeGraph(self, batch, n)
+        g.ids.copy_(batch.input_ids, non_blocking=True)
+        g.meta.copy_(batch._dev_meta[:n], non_blocking=True)
+        if g.graph is None:
+            g.capture(self)
+        g.graph.replay()
+        return g.out.clone()
+
     @torch.no_grad()
     def forward(self, batch, capture_latents=True):
         """Returns (logits [n_seqs, V], latents host [L, T, H] or [L, T, 2*n_kv*D] or None)."""
@@ -375,3 +409,53 @@ class RaggedTransformer:
             kv = x.view(T, 2 * nkv, D).contiguous()  # stored pre-RoPE: rotation happens on the way in
         kv_rope_scatter(kv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, self.cos, self.sin, 0, nkv,
                         rotate_q=False, do_rope=self.cos is not None, rotary_dim=self.rot)
+
+
+class _DecodeGraph:
+    """Static inputs, captured graph and output of one decode batch size (RaggedTransformer.forward_decode_graph)."""
+
+    def __init__(self, model, batch, n):
+        dev = model.device
+        B = batch.current_sequences
+        mb = batch.block_tables.shape[1]
+        A = batch.n_atoms
+        self.ids = torch.zeros(B, dtype=batch.input_ids.dtype, device=dev)
+        self.meta = torch.zeros(n, dtype=torch.int32, device=dev)
+        o = 0
+
+        def take(k, shape):
+            nonlocal o
+            v = self.meta[o:o + k].view(*shape)
+            o += k
+            return v
+
+        sb = types.SimpleNamespace()
+        sb.input_ids = self.ids
+        sb.seq_meta = take(3 * B, (B, 3))
+        sb.tok_seq = take(B, (B, ))
+        sb.tok_pos = take(B, (B, ))
+        sb.last_token_idx = take(B, (B, ))
+        sb.block_tables = take(B * mb, (B, mb))
+        sb.atoms = take(3 * A, (A, 3))
+        sb.n_atoms = A
+        sb.current_tokens = B
+        sb.current_sequences = B
+        sb.seq_meta_host = None
+        sb.tables_host = None
+        self.batch = sb
+        self.graph = None
+        self.out = None
+
+    def capture(self, model):
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            model.forward(self.batch, capture_latents=False)  # warm-up: hipBLASLt / GEMV handles, KV (idempotent)
+        cur.wait_stream(side)
+        if model._graph_pool is None:
+            model._graph_pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=model._graph_pool):
+            self.out, _ = model.forward(self.batch, capture_latents=False)
+        self.graph = g

@@ -78,6 +78,33 @@ def test_hcache_consistency_gpu(latent_mode):
     _run_consistency("cuda", torch.bfloat16, latent_mode, 6e-2)
 
 
+@pytest.mark.gpu
+def test_decode_graph_matches_eager_gpu():
+    """HIP-graph decode (one captured forward per batch size, replayed with new metadata) produces the logits of the
+    eager ragged forward, across steps whose context lengths, KV slots and sequence sets change."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    m = _model("cuda", torch.bfloat16)
+    econf = {"dtype": "bf16", "state_manager": {"max_context": 1024, "kv_block_size": 64}}
+    engs = {}
+    for mode in ("graph", "eager"):
+        eng = build_engine_from_model(m, econf, device=torch.device("cuda"), num_kv_blocks=64)
+        if mode == "eager":
+            eng._model.decode_graph_max_batch = 0
+        engs[mode] = eng
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, 211, (n, ), generator=g) for n in (40, 65, 7)]
+    for eng in engs.values():
+        eng.put([1, 2, 3], prompts, capture_latents=False)
+    for step in range(6):
+        uids = [1, 2, 3] if step % 3 else [1, 3]  # two batch sizes -> two captured graphs
+        toks = [torch.randint(0, 211, (1, ), generator=g) for _ in uids]
+        out = {k: e.put(uids, toks, capture_latents=False)[0].float() for k, e in engs.items()}
+        assert torch.allclose(out["graph"], out["eager"], atol=2e-2, rtol=2e-2), step
+    assert set(engs["graph"]._model._decode_graphs) == {2, 3}
+    assert not engs["eager"]._model._decode_graphs
+
+
 def test_allocator_and_scheduling():
     from hcache_deepspeed_amd.inference.v2 import BlockedAllocator, SchedulingResult
     a = BlockedAllocator(10)
