@@ -58,8 +58,21 @@ class _Tagged:
 class HostActivationCache:
 
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
-                 gpu_budget_bytes=None, host_budget_bytes=None):
+                 gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None):
         self.device = device
+        # Copy window: bytes of D2H (forward) / H2D (backward) the host may have queued on the copy stream and not
+        # yet seen complete. Autograd runs far ahead of the GPU on the host; a freed spilled tensor (forward) or
+        # consumed prefetch buffer (backward) is recycled by the caching allocator only once its copy drained
+        # (record_stream), so without a window every layer's pending bytes pile up at once, the allocator runs out,
+        # frees its cache with a device-wide synchronize and the copies stop overlapping compute.
+        if copy_window_bytes is None:
+            copy_window_bytes = 8 << 30
+            if gpu_budget_bytes is not None and device.type == "cuda":
+                head = torch.cuda.get_device_properties(device).total_memory - gpu_budget_bytes
+                copy_window_bytes = int(min(16 << 30, max(4 << 30, head // 3)))
+        self.copy_window = int(copy_window_bytes)
+        self._d2h_q, self._h2d_q = [], []
+        self.throttle_waits = 0
         # pinned host bytes the cache may hold at once (the calibration step spills every eligible layer; at long
         # context that alone can exceed the host's memory): beyond it tensors stay on the GPU
         self.host_budget = host_budget_bytes
@@ -98,9 +111,10 @@ class HostActivationCache:
         if hgib <= 0:
             import psutil
             hgib = min(0.4 * psutil.virtual_memory().total / 2**30, 160.0)
+        wgib = float(getattr(cfg, "copy_window_gib", 0.0) or 0.0)
         return cls(device, min_bytes=1 << 20, min_layers_resident=cfg.min_layers_resident,
                    prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget,
-                   host_budget_bytes=int(hgib * 2**30))
+                   host_budget_bytes=int(hgib * 2**30), copy_window_bytes=int(wgib * 2**30) if wgib > 0 else None)
 
     # ---------------------------------------------------------------------------------------
     def attach(self, model):
@@ -148,6 +162,15 @@ class HostActivationCache:
             yield
 
     # ---------------------------------------------------------------------------------------
+    def _window(self, q, nbytes):
+        """Block the host until the copies queued in ``q`` leave room for ``nbytes`` more in the copy window."""
+        while q and q[0][0].query():
+            q.pop(0)
+        while q and sum(b for _, b in q) + nbytes > self.copy_window:
+            ev, _ = q.pop(0)
+            ev.synchronize()
+            self.throttle_waits += 1
+
     def _pack(self, t):
         if (not isinstance(t, torch.Tensor) or not t.is_cuda or t.is_leaf or self.cur_layer < 0
                 or self.cur_layer >= self.n_layers - self.keep
@@ -165,6 +188,7 @@ class HostActivationCache:
             return _Tagged(t, self.cur_layer) if self.by_layer else t
         s = _Spilled()
         s.shape, s.dtype, s.device, s.layer = t.shape, t.dtype, t.device, self.cur_layer
+        self._window(self._d2h_q, nbytes)
         src = t if t.is_contiguous() else t.contiguous()
         s.host = self.pool.get(src.numel(), src.dtype)
         ev = torch.cuda.Event()
@@ -175,6 +199,7 @@ class HostActivationCache:
             src.record_stream(self.stream)
             s.d2h_done = torch.cuda.Event()
             s.d2h_done.record(self.stream)
+        self._d2h_q.append((s.d2h_done, nbytes))
         self.bytes_offloaded += src.numel() * src.element_size()
         self.host_in_use += src.numel() * src.element_size()
         self.by_layer.setdefault(s.layer, []).append(s)
@@ -187,6 +212,8 @@ class HostActivationCache:
         # an allocation on the copy stream finds an empty per-stream pool and, with HBM nearly full, makes the
         # allocator free cached blocks -- a device-wide synchronize that serialises every copy with compute.
         cur = torch.cuda.current_stream()
+        nbytes = s.host.numel() * s.host.element_size()
+        self._window(self._h2d_q, nbytes)
         s.dev = torch.empty(s.shape, dtype=s.dtype, device=s.device)
         ready = torch.cuda.Event()
         ready.record(cur)
@@ -197,6 +224,7 @@ class HostActivationCache:
             s.dev.record_stream(self.stream)
             s.h2d_done = torch.cuda.Event()
             s.h2d_done.record(self.stream)
+        self._h2d_q.append((s.h2d_done, nbytes))
 
     _DEBUG = os.environ.get("HDS_ACT_CACHE_DEBUG") == "1"
 
@@ -234,7 +262,8 @@ class HostActivationCache:
     def stats(self):
         return {"bytes_offloaded": self.bytes_offloaded, "pinned_pool_bytes": self.pool.bytes_allocated,
                 "spilled_layers": None if self.plan is None else len(self.plan), "late_unpacks": self.late_unpacks,
-                "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes}
+                "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
+                "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits}
 
 
 def calibrated_plan(layer_bytes, measured_peak, host_capped_bytes, budget):

@@ -171,6 +171,7 @@ class HostActCacheConfig:
     gpu_budget_gib: float = 0.0  # 0: 92% of device memory
     prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block
     host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: min(40% of host RAM, 160 GiB))
+    copy_window_gib: float = 0.0  # queued-but-unfinished copy bytes per direction (0: from the HBM headroom)
 
 
 AUTO = -1

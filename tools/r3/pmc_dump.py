@@ -13,7 +13,9 @@ def main(d):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in rows:
-        name = r.get("Kernel_Name", "?").split("(")[0][-70:]
+        name = r.get("Kernel_Name", "?")
+        name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+        name = name.split("((")[0].split("(")[0][:80]
         per[name][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[name].add(r.get("Dispatch_Id"))
     for name, c in sorted(per.items(), key=lambda kv: -sum(kv[1].values())):
