@@ -70,16 +70,11 @@ def transpose2d(x):
     return out
 
 
-_WGRAD_LAYOUT = os.environ.get("HDS_WGRAD_LAYOUT", "auto")  # auto | direct | nt
+_WGRAD_LAYOUT = os.environ.get("HDS_WGRAD_LAYOUT", "auto")  # auto | direct | nt | direct_sk2 | nt_sk2
 _WGRAD_CHOICE = {}
 
 
-def _wgrad_run(layout, dy2, x2, out, accumulate):
-    if layout == "nt":  # hipBLASLt's NT form on transposed copies (the forward GEMM's fast layout)
-        a, b = transpose2d(dy2), transpose2d(x2)
-        bt = b.t()
-    else:
-        a, bt = dy2.t(), x2
+def _mm_into(out, a, bt, accumulate):
     if out.dtype == a.dtype:
         if accumulate:
             out.addmm_(a, bt)
@@ -90,6 +85,46 @@ def _wgrad_run(layout, dy2, x2, out, accumulate):
             torch.addmm(out, a, bt, out_dtype=out.dtype, out=out)
         else:
             torch.mm(a, bt, out_dtype=out.dtype, out=out)
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def _wgrad_run(layout, dy2, x2, out, accumulate):
+    """``layout``: "direct" (TN as autograd issues it), "nt" (HIP transposes + the NT GEMM), or either with "_sk2":
+    the token (reduction) dimension split in two halves run as CONCURRENT GEMMs on two streams, the second into a
+    scratch buffer added at the join. A projection with few output tiles (qkv: 24 x 16 tiles of 256 = 1.5 waves on
+    256 CUs; down: 3.5 waves) otherwise idles part of the chip in its last wave; two half-K GEMMs in flight fill it."""
+    base, sk2 = layout.split("_")[0], layout.endswith("_sk2")
+    if base == "nt":  # hipBLASLt's NT form on transposed copies (the forward GEMM's fast layout)
+        a, bt = transpose2d(dy2), transpose2d(x2).t()
+        split_a, split_b = (lambda t, lo, hi: t[:, lo:hi]), (lambda t, lo, hi: t[lo:hi])
+    else:
+        a, bt = dy2.t(), x2
+        split_a, split_b = (lambda t, lo, hi: t[:, lo:hi]), (lambda t, lo, hi: t[lo:hi])
+    if not sk2 or not out.is_cuda:
+        _mm_into(out, a, bt, accumulate)
+        return
+    T = a.shape[1]
+    h = (T // 2) // 256 * 256 or T // 2
+    cur = torch.cuda.current_stream(out.device)
+    side = _side_stream(out.device)
+    tmp = torch.empty_like(out)
+    side.wait_stream(cur)
+    _mm_into(out, split_a(a, 0, h), split_b(bt, 0, h), accumulate)
+    with torch.cuda.stream(side):
+        _mm_into(tmp, split_a(a, h, T), split_b(bt, h, T), False)
+        for t in (a, bt, tmp):
+            t.record_stream(side)
+    cur.wait_stream(side)
+    out.add_(tmp)
 
 
 def _time_layout(layout, dy2, x2, out, accumulate):
@@ -117,9 +152,11 @@ def wgrad(dy2, x2, out, accumulate=False):
             key = (tuple(dy2.shape), tuple(x2.shape), out.dtype, bool(accumulate))
             layout = _WGRAD_CHOICE.get(key)
             if layout is None:
-                td = _time_layout("direct", dy2, x2, out, accumulate)
-                tn = _time_layout("nt", dy2, x2, out, accumulate)
-                layout = "nt" if tn < 0.97 * td else "direct"
+                times = {c: _time_layout(c, dy2, x2, out, accumulate)
+                         for c in ("direct", "nt", "direct_sk2", "nt_sk2")}
+                layout = min(times, key=times.get)
+                if layout != "direct" and times[layout] > 0.97 * times["direct"]:
+                    layout = "direct"  # within noise: keep the plain form
                 _WGRAD_CHOICE[key] = layout
     _wgrad_run(layout, dy2, x2, out, accumulate)
     return out

@@ -13,7 +13,7 @@ def test_transpose_matches_torch(R, C, ld):
     assert torch.equal(transpose2d(x), x.t().contiguous())
 
 
-@pytest.mark.parametrize("layout", ["direct", "nt", "auto"])
+@pytest.mark.parametrize("layout", ["direct", "nt", "direct_sk2", "nt_sk2", "auto"])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
 def test_wgrad_layouts_match(layout, out_dtype, monkeypatch):
     from hcache_deepspeed_amd.ops import gemm

@@ -46,5 +46,23 @@ def main():
     print(f"per layer: direct {tot['direct']*1e3:.2f} ms, nt+transposes {tot['nt+tr']*1e3:.2f} ms")
 
 
+def splitk():
+    """Every wgrad candidate of ops/gemm.wgrad at the bench shapes (incl. two-stream split-K) + the auto pick."""
+    from hcache_deepspeed_amd.ops import gemm
+    T = 7 * 4096
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    for name, (N, K) in shapes.items():
+        dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+        fl = 2 * T * N * K
+        res = {}
+        for lay in ("direct", "nt", "direct_sk2", "nt_sk2"):
+            ts = t(lambda: gemm._wgrad_run(lay, dy, x, out, False))
+            res[lay] = (round(ts * 1e3, 3), round(fl / ts / 1e15, 3))
+        print(name, json.dumps(res), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    import json
+    splitk() if "--splitk" in sys.argv else main()
