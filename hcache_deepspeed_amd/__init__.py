@@ -102,6 +102,13 @@ def init_inference(model, config=None, **kwargs):
     from .inference.config import DeepSpeedInferenceConfig
     cfg = dict(config or {})
     cfg.update(kwargs)
+    import torch.nn as _nn
+    if not isinstance(model, _nn.Module) and any(hasattr(model, a) for a in ("unet", "vae", "text_encoder")):
+        # a diffusion pipeline (reference replace_module.generic_injection): UNet / VAE / CLIP text encoder are
+        # wrapped in place with HIP-graph replay and the fused attention processor
+        from .inference.diffusers import inject_pipeline
+        inject_pipeline(model, enable_cuda_graph=bool(cfg.get("enable_cuda_graph", True)))
+        return model
     return InferenceEngine(model, config=DeepSpeedInferenceConfig(**cfg))
 
 

@@ -219,6 +219,12 @@ def inject(model, quant=None, trainable=False, fuse_mlp=True):
     already fused and are left alone. ``trainable``/``fuse_mlp=False`` keep parameter names and grads (used
     by the hybrid engine before ZeRO partitions the model)."""
     n = 0
+    if not trainable:
+        # family containers that replace whole blocks come first (they read the original LayerNorm weights)
+        from .megatron import inject_internlm, inject_megatron_layers
+        n += inject_megatron_layers(model) + inject_internlm(model)
+        from .diffusers import inject_attention_processors
+        n += inject_attention_processors(model)  # diffusers-style Attention modules (UNet / VAE blocks)
     for parent in list(model.modules()):
         for cname, child in list(parent.named_children()):
             cls = type(child).__name__

@@ -1,0 +1,12 @@
+# GPU: split-K wgrad micro-benchmark + layout tests, qkv split forward, then the headline bench + kernel stats
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out/rc
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_wgrad_layout_gpu.py > gpurun_out/rc/wgrad_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u tools/bench_wgrad_layout.py --splitk > gpurun_out/rc/wgrad_splitk.log 2>&1 || exit 1
+timeout -k 10 200 python -u tools/bench_qkv_split.py --slices > gpurun_out/rc/qkv_slices.log 2>&1 || exit 1
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > gpurun_out/rc/bench.log 2>&1 || exit 1
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rc/prof -o run -- python3 bench.py --steps 3 --warmup 2 > gpurun_out/rc/prof.log 2>&1 || exit 1
+find gpurun_out/rc -name "*kernel_trace.csv" -delete
+timeout -k 10 300 python -u tools/r3/aten_op_census.py > gpurun_out/rc/census.log 2>&1 || exit 1
