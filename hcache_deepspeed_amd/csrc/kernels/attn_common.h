@@ -90,6 +90,47 @@ __device__ __forceinline__ bf16x8 read_tr_asm(const char* lds_tile, int s, int d
 __device__ __forceinline__ bf16x8 tr_d_asm(const char* tile, int s, int dt) {
   return read_tr_asm(tile + (dt >> 2) * 16384, s, dt & 3);
 }
+// Closed-form addresses of the XOR layout, for kernels short of registers: with ch = 2ks + h,
+//   tile_off(row, ch) = P ^ (32 ks),            P = row*256 | 16 (h ^ swz(row))          (row reads)
+// and for the transposed reads of k-step s, column block dt (rows r0 = 4(g>>1) + q and r0 + 8, c = 2(g&1) + (p>>1)):
+//   off = 4096 s + (Y ^ 64 dt),                 Y = (r*256 + 8(p&1)) | 16 (c ^ swz(r))
+// so each read costs one XOR with a compile-time constant on ONE per-lane register instead of one precomputed
+// offset register per k-step.
+__device__ __forceinline__ uint32_t rows_lane_off(int row0) {
+  const int lane = threadIdx.x & 63;
+  const int row = row0 + (lane & 31);
+  return (uint32_t)(row * 256) | (uint32_t)(16 * ((lane >> 5) ^ swz(row)));
+}
+__device__ __forceinline__ bf16x8 read_rows_off_asm(const char* tile, uint32_t P, int ks) {
+  bf16x8 r;
+  const uint32_t a = (uint32_t)(uintptr_t)tile + (P ^ (32u * (uint32_t)ks));
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+__device__ __forceinline__ void tr_lane_offs(uint32_t& y0, uint32_t& y1) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c = 2 * (g & 1) + (p >> 1);
+  const int r0 = 4 * (g >> 1) + q, r1 = r0 + 8;
+  y0 = (uint32_t)(r0 * 256 + 8 * (p & 1)) | (uint32_t)(16 * (c ^ swz(r0)));
+  y1 = (uint32_t)(r1 * 256 + 8 * (p & 1)) | (uint32_t)(16 * (c ^ swz(r1)));
+}
+__device__ __forceinline__ bf16x8 read_tr_off_asm(const char* tile, uint32_t y0, uint32_t y1, int s, int dt) {
+  const uint32_t base = (uint32_t)(uintptr_t)tile + 4096u * (uint32_t)s;
+  const bf16x4 lo = ds_tr_asm((const char*)(uintptr_t)(base + (y0 ^ (64u * (uint32_t)dt))));
+  const bf16x4 hi = ds_tr_asm((const char*)(uintptr_t)(base + (y1 ^ (64u * (uint32_t)dt))));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// row fragment (read_rows) issued as inline asm, retired by lds_wait<N>() like read_tr_asm
+__device__ __forceinline__ bf16x8 read_rows_asm(const char* lds_tile, int row0, int ks) {
+  const int lane = threadIdx.x & 63;
+  const int row = row0 + (lane & 31);
+  const int ch = 2 * ks + (lane >> 5);
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)(lds_tile + tile_off(row, ch))) : "memory");
+  return r;
+}
 template <int N>
 __device__ __forceinline__ void lds_wait() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");

@@ -640,7 +640,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
 // (128 regs) + one 32x32 S/dP pair, which fits 256 registers -> 2 waves per SIMD, so one wave's
 // softmax/VALU section overlaps the other wave's MFMAs. The two query halves' partial dK/dV are
 // summed through LDS once at the end.
-template <int D, int PRIO, bool EVO = false>
+// PIPE: LDS operand reads issued two MFMAs ahead of their use as inline asm with counted lgkmcnt waits (a ring of
+// three fragments), instead of the compiler's load -> lgkmcnt(0) -> MFMA per product, which exposes the LDS latency
+// of every read (the MFMA pipe sat idle ~2/3 of the time: PMC 37 % MFMA busy).
+template <int D, int PRIO, bool EVO = false, int PIPE = 0>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) {
   constexpr int BK = 128;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT;
@@ -667,6 +670,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
   const char* Kw = Kt + (kg >> 1) * 16384;
   const char* Vw = Vt + (kg >> 1) * 16384;
   const int krow0 = 32 * (kg & 1);
+  // PIPE: one per-lane register per operand role (closed-form XOR-layout addresses, attn_common.h)
+  const uint32_t pq = rows_lane_off(32 * qh), pk = rows_lane_off(krow0);
+  uint32_t ty0, ty1;
+  tr_lane_offs(ty0, ty1);
 
   // K / V tiles of the block (rows clamped to the sequence)
 #pragma unroll
@@ -739,10 +746,36 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
     if (!skip) {
       const bool need_mask = (p.causal && q0 < kw0 + 31) || p.window > 0 || q0 + 32 > len || kw0 + 32 > len;
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
+      if constexpr (PIPE != 0 && D == 128) {
+        bf16x8 fa[3], fb[3];
+        auto ld = [&](int j) {
+          const int ks = j % KS;
+          fa[j % 3] = read_rows_off_asm(j < KS ? Qt : Ot, pq, ks);
+          fb[j % 3] = read_rows_off_asm(j < KS ? Kw : Vw, pk, ks);
+        };
+        ld(0);
+        ld(1);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) sacc = mfma(read_rows(Qt, 32 * qh, ks), read_rows(Kw, krow0, ks), sacc);
+        for (int j = 0; j < 2 * KS; ++j) {
+          if (j + 2 < 2 * KS) {
+            ld(j + 2);
+            lds_wait<4>();
+          } else if (j + 1 < 2 * KS) {
+            lds_wait<2>();
+          } else {
+            lds_wait<0>();
+          }
+          if (j < KS)
+            sacc = mfma(fa[j % 3], fb[j % 3], sacc);
+          else
+            dpacc = mfma(fa[j % 3], fb[j % 3], dpacc);
+        }
+      } else {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) dpacc = mfma(read_rows(Ot, 32 * qh, ks), read_rows(Vw, krow0, ks), dpacc);
+        for (int ks = 0; ks < KS; ++ks) sacc = mfma(read_rows(Qt, 32 * qh, ks), read_rows(Kw, krow0, ks), sacc);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) dpacc = mfma(read_rows(Ot, 32 * qh, ks), read_rows(Vw, krow0, ks), dpacc);
+      }
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
         const int qr0 = 32 * qh + 8 * r4 + 4 * h;  // rows acc_row(4*r4 + j, h) = qr0 + j
@@ -761,12 +794,38 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
       }
       const bf16x8 p0 = acc_to_b<0>(sacc), p1 = acc_to_b<1>(sacc);
       const bf16x8 s0 = acc_to_b<0>(dpacc), s1 = acc_to_b<1>(dpacc);
+      if constexpr (PIPE != 0 && D == 128) {
+        // j = 4 dt + r: r 0/1 -> dV with dO^T halves, r 2/3 -> dK with Q^T halves
+        bf16x8 ft[3];
+        auto ldt = [&](int j) { ft[j % 3] = read_tr_off_asm((j & 3) < 2 ? Ot : Qt, ty0, ty1, 2 * qh + (j & 1), j >> 2); };
+        ldt(0);
+        ldt(1);
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        dv[dt] = mfma(read_tr(Ot, 2 * qh, dt), p0, dv[dt]);
-        dv[dt] = mfma(read_tr(Ot, 2 * qh + 1, dt), p1, dv[dt]);
-        dk[dt] = mfma(read_tr(Qt, 2 * qh, dt), s0, dk[dt]);
-        dk[dt] = mfma(read_tr(Qt, 2 * qh + 1, dt), s1, dk[dt]);
+        for (int j = 0; j < 4 * DT; ++j) {
+          if (j + 2 < 4 * DT) {
+            ldt(j + 2);
+            lds_wait<4>();
+          } else if (j + 1 < 4 * DT) {
+            lds_wait<2>();
+          } else {
+            lds_wait<0>();
+          }
+          const int dt = j >> 2;
+          switch (j & 3) {
+            case 0: dv[dt] = mfma(ft[j % 3], p0, dv[dt]); break;
+            case 1: dv[dt] = mfma(ft[j % 3], p1, dv[dt]); break;
+            case 2: dk[dt] = mfma(ft[j % 3], s0, dk[dt]); break;
+            default: dk[dt] = mfma(ft[j % 3], s1, dk[dt]); break;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dv[dt] = mfma(read_tr(Ot, 2 * qh, dt), p0, dv[dt]);
+          dv[dt] = mfma(read_tr(Ot, 2 * qh + 1, dt), p1, dv[dt]);
+          dk[dt] = mfma(read_tr(Qt, 2 * qh, dt), s0, dk[dt]);
+          dk[dt] = mfma(read_tr(Qt, 2 * qh + 1, dt), s1, dk[dt]);
+        }
       }
     }
     __syncthreads();
@@ -803,7 +862,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
 // =====================================================================================
 // backward dQ
 // =====================================================================================
-template <int D, int NW, int PRIO, bool EVO = false>
+// PIPE: as in the dK/dV kernel -- LDS operand reads two MFMAs ahead as inline asm with counted waits, so neither
+// the per-read LDS latency nor the compiler's vmcnt(0) in front of the transposed-read builtin (which waits for
+// the NEXT tile's LDS-DMA in the middle of every iteration) stalls the MFMA pipe.
+template <int D, int NW, int PRIO, bool EVO = false, int PIPE = 0>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
@@ -863,6 +925,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
   for (int i = 0; i < DT; ++i) dq[i] = f32x16{};
   const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
+  const uint32_t pr0 = rows_lane_off(0), pr1 = rows_lane_off(32);  // PIPE: closed-form LDS addresses
+  uint32_t ty0, ty1;
+  tr_lane_offs(ty0, ty1);
 
   stage_tile_d<NW, D>(smem + 0, kptr(kt_begin));
   stage_tile_d<NW, D>(smem + 2 * TL, vptr(kt_begin));
@@ -884,14 +949,42 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
     if (p.window > 0 && k0 + BN - 1 <= wq_lo - p.window) skip = true;
     if (!skip) {
       f32x16 s[2], dp[2];
+      if constexpr (PIPE != 0 && D == 128 && !EVO) {
+        // j = 16 t + 8 which + ks: which 0 -> S (K rows x Q), 1 -> dP (V rows x dO)
+        s[0] = s[1] = dp[0] = dp[1] = f32x16{};
+        bf16x8 fa[3];
+        auto ld = [&](int j) {
+          const int t = j >> 4, which = (j >> 3) & 1, ks = j & 7;
+          fa[j % 3] = read_rows_off_asm(which ? Vt : Kt, t ? pr1 : pr0, ks);
+        };
+        ld(0);
+        ld(1);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        s[t] = f32x16{};
-        dp[t] = f32x16{};
+        for (int j = 0; j < 32; ++j) {
+          if (j + 2 < 32) {
+            ld(j + 2);
+            lds_wait<2>();
+          } else if (j + 1 < 32) {
+            lds_wait<1>();
+          } else {
+            lds_wait<0>();
+          }
+          const int t = j >> 4, which = (j >> 3) & 1, ks = j & 7;
+          if (which)
+            dp[t] = mfma(fa[j % 3], df[ks], dp[t]);
+          else
+            s[t] = mfma(fa[j % 3], qf[ks], s[t]);
+        }
+      } else {
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[t] = mfma(rows_d(Kt, 32 * t, ks), qf[ks], s[t]);
+        for (int t = 0; t < 2; ++t) {
+          s[t] = f32x16{};
+          dp[t] = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) dp[t] = mfma(rows_d(Vt, 32 * t, ks), df[ks], dp[t]);
+          for (int ks = 0; ks < KS; ++ks) s[t] = mfma(rows_d(Kt, 32 * t, ks), qf[ks], s[t]);
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) dp[t] = mfma(rows_d(Vt, 32 * t, ks), df[ks], dp[t]);
+        }
       }
       // only tiles that straddle the causal diagonal / window edge / sequence end need the per-element mask
       const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
@@ -928,10 +1021,29 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
         }
       }
       const bf16x8 sb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
+      if constexpr (PIPE != 0 && D == 128 && !EVO) {
+        bf16x8 ft[3];
+        auto ldt = [&](int j) { ft[j % 3] = read_tr_off_asm(Kt, ty0, ty1, j & 3, j >> 2); };
+        ldt(0);
+        ldt(1);
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
+        for (int j = 0; j < 4 * DT; ++j) {
+          if (j + 2 < 4 * DT) {
+            ldt(j + 2);
+            lds_wait<4>();
+          } else if (j + 1 < 4 * DT) {
+            lds_wait<2>();
+          } else {
+            lds_wait<0>();
+          }
+          dq[j >> 2] = mfma(ft[j % 3], sb[j & 3], dq[j >> 2]);
+        }
+      } else {
 #pragma unroll
-        for (int st = 0; st < 4; ++st) dq[dt] = mfma(tr_d(Kt, st, dt), sb[st], dq[dt]);
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int st = 0; st < 4; ++st) dq[dt] = mfma(tr_d(Kt, st, dt), sb[st], dq[dt]);
+      }
     }
     __syncthreads();
   }
@@ -984,13 +1096,19 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 }  // namespace
 
-int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1;
+int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_bwd_pipe = 0;
 
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
 // 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
   if (var < 0 || var > 4) return hipErrorInvalidValue;
   g_fwd_var = var;
+  return 0;
+}
+
+// backward: dK/dV kernel with LDS reads pipelined two MFMAs ahead (0 / 1; head_dim 128)
+HDS_EXPORT int hds_attn_bwd_pipe(int on) {
+  g_bwd_pipe = on ? 1 : 0;
   return 0;
 }
 
@@ -1042,7 +1160,9 @@ int launch_bwd(const AttnParams& p, int batch, int max_len, int total_tokens, in
   if constexpr (D <= 128) {
     if (g_dkdv_nw == 8) {
       const dim3 grid((max_len + 127) / 128, hkv, batch);
-      if (g_bwd_prio)
+      if (g_bwd_pipe && D == 128)
+        hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 1, false, 1>), grid, dim3(512), 0, st, p);
+      else if (g_bwd_prio)
         hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 1>), grid, dim3(512), 0, st, p);
       else
         hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 0>), grid, dim3(512), 0, st, p);
@@ -1068,7 +1188,9 @@ int launch_bwd(const AttnParams& p, int batch, int max_len, int total_tokens, in
   if constexpr (D <= 128) {
     if (g_dq_nw == 8) {
       const dim3 grid((max_len + 255) / 256, hq, batch);
-      if (g_bwd_prio)
+      if (g_bwd_pipe && D == 128)
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 1, false, 1>), grid, dim3(512), 0, st, p);
+      else if (g_bwd_prio)
         hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 1>), grid, dim3(512), 0, st, p);
       else
         hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 0>), grid, dim3(512), 0, st, p);

@@ -43,6 +43,7 @@ _KERNEL_SIGS = {
     "hds_attn_config": "iii",
     "hds_attn_fwd_variant": "i",
     "hds_attn_bwd_prio": "i",
+    "hds_attn_bwd_pipe": "i",
     "hds_bsattn_fwd": "p" * 8 + "i" * 7 + "f" + "i" + "s",
     "hds_bsattn_bwd": "p" * 15 + "i" * 7 + "f" + "i" + "s",
     "hds_kv_rope_scatter": "i" + "p" + "l" + "pppp" + "i" + "pp" + "i" * 8 + "s",
@@ -131,6 +132,8 @@ def load_kernels(build_if_missing=True):
             return None
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         _bind(lib, _KERNEL_SIGS)
+        # FlashAttention backward with LDS reads pipelined two MFMAs ahead (csrc/kernels/flash_attn.hip PIPE)
+        lib.hds_attn_bwd_pipe(int(os.environ.get("HDS_ATTN_BWD_PIPE", "1")))
         _klib = lib
         return _klib
 

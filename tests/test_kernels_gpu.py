@@ -740,3 +740,49 @@ def test_kv_append_matches_index_copy():
     vr.index_copy_(2, cur, v.reshape(B, nkv, 1, D))
     torch.cuda.synchronize()
     assert torch.equal(kc, kr) and torch.equal(vc, vr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["causal", "full", "window", "varlen", "gqa_tail"])
+def test_flash_bwd_pipelined_matches_plain_gpu(case):
+    """dK/dV and dQ kernels with LDS reads pipelined two MFMAs ahead (PIPE) give the plain kernels' gradients, and
+    both match fp32 autograd."""
+    from hcache_deepspeed_amd.ops import native
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    lib = native.kernels()
+    torch.manual_seed(11)
+    B, S, Hq, Hkv, D = 2, (701 if case == "gqa_tail" else 640), 8, 2, 128
+    q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    do = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
+    kw = dict(causal=case != "full", window=100 if case == "window" else 0)
+    grads = {}
+    try:
+        for pipe in (0, 1):
+            lib.hds_attn_bwd_pipe(pipe)
+            q.grad = k.grad = v.grad = None
+            if case == "varlen":
+                cu = torch.tensor([0, 333, 2 * S], device="cuda", dtype=torch.int32)
+                o = flash_attn(q.reshape(-1, Hq, D), k.reshape(-1, Hkv, D), v.reshape(-1, Hkv, D), causal=True,
+                               cu_seqlens=cu).view(B, S, Hq, D)
+            else:
+                o = flash_attn(q, k, v, **kw)
+            o.backward(do)
+            grads[pipe] = [t.grad.float().clone() for t in (q, k, v)]
+    finally:
+        lib.hds_attn_bwd_pipe(1)
+    for a, b in zip(grads[0], grads[1]):
+        assert (a - b).abs().max().item() <= 2e-2 * max(1.0, a.abs().max().item()), case
+    if case in ("causal", "full", "gqa_tail"):
+        qf, kf, vf = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+        kk, vv = kf.repeat_interleave(4, 2), vf.repeat_interleave(4, 2)
+        s = torch.einsum("bqhd,bkhd->bhqk", qf, kk) / D**0.5
+        if kw["causal"]:
+            i = torch.arange(S, device="cuda")
+            s = s.masked_fill(i[None, :] > i[:, None], float("-inf"))
+        ref = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), vv)
+        ref.backward(do.float())
+        for g, r in zip(grads[1], (qf.grad, kf.grad, vf.grad)):
+            rel = ((g - r).norm() / r.norm()).item()
+            assert rel < 2e-2, (case, rel)
