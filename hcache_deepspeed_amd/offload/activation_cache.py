@@ -60,16 +60,18 @@ class HostActivationCache:
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
                  gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None):
         self.device = device
-        # Copy window: bytes of D2H (forward) / H2D (backward) the host may have queued on the copy stream and not
-        # yet seen complete. Autograd runs far ahead of the GPU on the host; a freed spilled tensor (forward) or
-        # consumed prefetch buffer (backward) is recycled by the caching allocator only once its copy drained
-        # (record_stream), so without a window every layer's pending bytes pile up at once, the allocator runs out,
-        # frees its cache with a device-wide synchronize and the copies stop overlapping compute.
+        # D2H copy window: spilled bytes the host may have queued on the copy stream and not yet seen copied.
+        # Autograd runs far ahead of the GPU on the host, and a spilled tensor's HBM is recycled only once its D2H
+        # drained (record_stream) -- with PCIe slower than a layer's forward the backlog grows layer by layer. Left
+        # unbounded it exhausts the allocator, which then frees its cache behind a device-wide synchronize; the
+        # window keeps it inside the HBM the budget leaves free (the host waits only when it would not fit). The
+        # backward needs no window: prefetch buffers are allocated and consumed on the compute stream and the
+        # copy stream waits for them (see _prefetch), so their blocks recycle in stream order.
         if copy_window_bytes is None:
-            copy_window_bytes = 8 << 30
+            copy_window_bytes = 16 << 30
             if gpu_budget_bytes is not None and device.type == "cuda":
                 head = torch.cuda.get_device_properties(device).total_memory - gpu_budget_bytes
-                copy_window_bytes = int(min(16 << 30, max(4 << 30, head // 3)))
+                copy_window_bytes = int(max(4 << 30, head - (6 << 30)))
         self.copy_window = int(copy_window_bytes)
         self._d2h_q, self._h2d_q = [], []
         self.throttle_waits = 0
@@ -212,8 +214,6 @@ class HostActivationCache:
         # an allocation on the copy stream finds an empty per-stream pool and, with HBM nearly full, makes the
         # allocator free cached blocks -- a device-wide synchronize that serialises every copy with compute.
         cur = torch.cuda.current_stream()
-        nbytes = s.host.numel() * s.host.element_size()
-        self._window(self._h2d_q, nbytes)
         s.dev = torch.empty(s.shape, dtype=s.dtype, device=s.device)
         ready = torch.cuda.Event()
         ready.record(cur)
@@ -221,10 +221,11 @@ class HostActivationCache:
             self.stream.wait_event(s.d2h_done)
             self.stream.wait_event(ready)
             s.dev.view(-1).copy_(s.host, non_blocking=True)
-            s.dev.record_stream(self.stream)
+            # no record_stream: the buffer was allocated on the compute stream after everything that used its block
+            # (`ready`), and every later user of the block is a compute-stream kernel ordered after the consumer,
+            # which waits for h2d_done -- so the block may recycle as soon as the consumer is enqueued
             s.h2d_done = torch.cuda.Event()
             s.h2d_done.record(self.stream)
-        self._h2d_q.append((s.h2d_done, nbytes))
 
     _DEBUG = os.environ.get("HDS_ACT_CACHE_DEBUG") == "1"
 
