@@ -72,6 +72,7 @@ def transpose2d(x):
 
 _WGRAD_LAYOUT = os.environ.get("HDS_WGRAD_LAYOUT", "auto")  # auto | direct | nt | direct_sk2 | nt_sk2
 _WGRAD_CHOICE = {}
+_SPLITK = os.environ.get("HDS_WGRAD_SPLITK", "0") == "1"  # two-stream split-K candidates in the timed choice
 
 
 def _mm_into(out, a, bt, accumulate):
@@ -152,8 +153,8 @@ def wgrad(dy2, x2, out, accumulate=False):
             key = (tuple(dy2.shape), tuple(x2.shape), out.dtype, bool(accumulate))
             layout = _WGRAD_CHOICE.get(key)
             if layout is None:
-                times = {c: _time_layout(c, dy2, x2, out, accumulate)
-                         for c in ("direct", "nt", "direct_sk2", "nt_sk2")}
+                cands = ("direct", "nt", "direct_sk2", "nt_sk2") if _SPLITK else ("direct", "nt")
+                times = {c: _time_layout(c, dy2, x2, out, accumulate) for c in cands}
                 layout = min(times, key=times.get)
                 if layout != "direct" and times[layout] > 0.97 * times["direct"]:
                     layout = "direct"  # within noise: keep the plain form

@@ -91,6 +91,8 @@ def _compare(got, ref):
         worst[n] = rel
     bad = {n: round(v, 4) for n, v in worst.items() if not v < 3e-2}
     assert not bad, bad
+    top = sorted(worst.items(), key=lambda kv: -kv[1])[:3]
+    print("worst parameters:", [(n, round(v, 4)) for n, v in top])
     return max(worst.values())
 
 
