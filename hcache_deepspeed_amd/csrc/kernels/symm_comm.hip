@@ -1,0 +1,255 @@
+// Symmetric-memory collectives over xGMI: one-shot all-reduce, direct-read all-gather and reduce-scatter between the
+// GPUs of one node, for the small / latency-bound collectives where a ring's 2(W-1) steps dominate.
+//
+// Reference parity: DeepCompile's SymmetricMemory all-gather (csrc/compile/z3.cpp:91-110, compile config
+// ``symmetric_memory``) and the one-shot small-message all-reduce SURVEY.md §5.8 asks for. The reference rides
+// torch's SymmetricMemory over NVLink; here every rank allocates ONE uncached device buffer (hipExtMallocWithFlags
+// hipDeviceMallocUncached: stores bypass L2, so a peer reading it over xGMI never sees a stale line), exports it
+// with hipIpcGetMemHandle, and maps every peer's buffer (hipIpcOpenMemHandle). xGMI is point-to-point, so a kernel
+// that reads all W-1 peers at once drives all 7 links concurrently instead of one ring neighbour per step.
+//
+// Buffer layout (per rank): flags [kMaxRanks][kMaxBlocks] u32 | error word | data parity 0 [cap] | data parity 1.
+// Protocol of one collective with epoch e (host counter, same on every rank; parity = e & 1):
+//   block b copies its chunk of the input into its OWN data[parity], fences at system scope, then stores e into
+//   flags[rank][b] of every peer's buffer; it then waits until its own flags[src][b] >= e for every peer src and
+//   reads chunk b of each peer's data[parity]. Per-block flags need no grid-wide barrier (every rank splits the
+//   message into the same blocks). Two parities make reuse safe: a rank rewrites data[parity] only at epoch e+2,
+//   after every peer signalled e+1, which a peer does only after its epoch-e kernel (all reads of e) has finished.
+// Every wait is bounded (kSpinMax polls): a missing peer sets the error word and the grid still drains; the host
+// reads the error word (hds_symm_error) -- no wave can spin forever.
+#include <cstring>
+
+#include "hds_common.h"
+
+namespace {
+using namespace hds;
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 256;
+constexpr int64_t kFlagBytes = (int64_t)kMaxRanks * kMaxBlocks * 4;
+constexpr int64_t kErrOff = kFlagBytes;
+constexpr int64_t kDataOff = kFlagBytes + 256;
+constexpr int kSpinMax = 1 << 22;
+constexpr int kThreads = 512;
+
+struct SymmArgs {
+  char* base[kMaxRanks];  // every rank's mapped buffer (own included)
+  int rank, world;
+  int64_t cap;            // bytes per parity
+  uint32_t epoch;
+  const void* in;
+  void* out;
+  int64_t n;              // all-reduce: elements; all-gather: bytes per rank; reduce-scatter: elements per rank
+};
+
+__device__ __forceinline__ uint32_t* flag_ptr(char* base, int src, int blk) {
+  return reinterpret_cast<uint32_t*>(base) + src * kMaxBlocks + blk;
+}
+
+__device__ __forceinline__ char* data_ptr(const SymmArgs& a, int r) {
+  return a.base[r] + kDataOff + (int64_t)(a.epoch & 1u) * a.cap;
+}
+
+// publish this block's chunk (all threads' stores) to every peer, then wait for every peer's chunk
+__device__ __forceinline__ void exchange(const SymmArgs& a) {
+  __threadfence_system();
+  __syncthreads();
+  const int t = threadIdx.x, b = blockIdx.x;
+  if (t < a.world && t != a.rank) {
+    char* peer = nullptr;
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+      if (r == t) peer = a.base[r];
+    __hip_atomic_store(flag_ptr(peer, a.rank, b), a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = flag_ptr(a.base[a.rank], t, b);
+    bool ok = false;
+    for (int it = 0; it < kSpinMax; ++it) {
+      const uint32_t v = __hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((int32_t)(v - a.epoch) >= 0) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(a.base[a.rank] + kErrOff), 1u + (uint32_t)t, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  __threadfence_system();
+}
+
+__device__ __forceinline__ void block_range(int64_t nvec, int64_t& lo, int64_t& hi) {
+  const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+  lo = (int64_t)blockIdx.x * per;
+  hi = lo + per < nvec ? lo + per : nvec;
+}
+
+// all-reduce (sum) of n elements (n % 8 == 0), accumulated in fp32, out may alias in
+template <typename T>
+__global__ __launch_bounds__(kThreads) void symm_allreduce_kernel(SymmArgs a) {
+  int64_t lo, hi;
+  block_range(a.n / 8, lo, hi);
+  const T* in = reinterpret_cast<const T*>(a.in);
+  T* mine = reinterpret_cast<T*>(data_ptr(a, a.rank));
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(in + 8 * i);
+    *reinterpret_cast<u32x4*>(mine + 8 * i) = v;
+  }
+  exchange(a);
+  T* out = reinterpret_cast<T*>(a.out);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // fixed rank order: every rank computes the bit-identical sum
+    for (int r = 0; r < a.world; ++r) {
+      float v[8];
+      Vec8<T>::load(reinterpret_cast<const T*>(data_ptr(a, r)) + 8 * i, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    Vec8<T>::store(out + 8 * i, acc);
+  }
+}
+
+// all-gather of n bytes per rank (n % 16 == 0): out[r * n ...] = rank r's input
+__global__ __launch_bounds__(kThreads) void symm_allgather_kernel(SymmArgs a) {
+  int64_t lo, hi;
+  block_range(a.n / 16, lo, hi);
+  const u32x4* in = reinterpret_cast<const u32x4*>(a.in);
+  u32x4* mine = reinterpret_cast<u32x4*>(data_ptr(a, a.rank));
+  u32x4* out = reinterpret_cast<u32x4*>(a.out);
+  const int64_t nv = a.n / 16;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+    const u32x4 v = in[i];
+    mine[i] = v;
+    out[(int64_t)a.rank * nv + i] = v;
+  }
+  exchange(a);
+  for (int d = 1; d < a.world; ++d) {
+    const int r = (a.rank + d) % a.world;  // staggered source order spreads the first reads over the links
+    const u32x4* src = reinterpret_cast<const u32x4*>(data_ptr(a, r));
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) out[(int64_t)r * nv + i] = src[i];
+  }
+}
+
+// reduce-scatter (sum): input [world * n] elements, out[n] = sum over ranks of their input segment `rank`
+template <typename T>
+__global__ __launch_bounds__(kThreads) void symm_reduce_scatter_kernel(SymmArgs a) {
+  int64_t lo, hi;
+  block_range(a.n / 8, lo, hi);
+  const T* in = reinterpret_cast<const T*>(a.in);
+  T* mine = reinterpret_cast<T*>(data_ptr(a, a.rank));
+  for (int s = 0; s < a.world; ++s)
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+      const int64_t e = (int64_t)s * a.n + 8 * i;
+      *reinterpret_cast<u32x4*>(mine + e) = *reinterpret_cast<const u32x4*>(in + e);
+    }
+  exchange(a);
+  T* out = reinterpret_cast<T*>(a.out);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < a.world; ++r) {
+      float v[8];
+      Vec8<T>::load(reinterpret_cast<const T*>(data_ptr(a, r)) + (int64_t)a.rank * a.n + 8 * i, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    Vec8<T>::store(out + 8 * i, acc);
+  }
+}
+
+int blocks_for(int64_t nvec) {
+  int64_t nb = (nvec + 2 * kThreads - 1) / (2 * kThreads);
+  return (int)(nb < 1 ? 1 : (nb > kMaxBlocks ? kMaxBlocks : nb));
+}
+
+bool make_args(SymmArgs& a, const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch, const void* in,
+               void* out, int64_t n) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || !in || !out || epoch == 0) return false;
+  for (int r = 0; r < kMaxRanks; ++r) a.base[r] = r < world ? reinterpret_cast<char*>(bases[r]) : nullptr;
+  for (int r = 0; r < world; ++r)
+    if (!a.base[r]) return false;
+  a.rank = rank;
+  a.world = world;
+  a.cap = cap;
+  a.epoch = epoch;
+  a.in = in;
+  a.out = out;
+  a.n = n;
+  return true;
+}
+
+}  // namespace
+
+HDS_EXPORT int hds_symm_header_bytes() { return (int)kDataOff; }
+
+// one uncached device buffer of kDataOff + 2 * cap bytes, zeroed, and its 64-byte IPC handle
+HDS_EXPORT int hds_symm_alloc(int64_t cap, void** ptr, void* handle) {
+  if (cap <= 0 || cap % 16) return hipErrorInvalidValue;
+  const size_t bytes = (size_t)(kDataOff + 2 * cap);
+  hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return e;
+  e = hipMemset(*ptr, 0, bytes);
+  if (e != hipSuccess) return e;
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return e;
+  return hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), *ptr);
+}
+
+HDS_EXPORT int hds_symm_open(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+HDS_EXPORT int hds_symm_close(void* ptr) { return hipIpcCloseMemHandle(ptr); }
+
+HDS_EXPORT int hds_symm_free(void* ptr) { return hipFree(ptr); }
+
+// error word of this rank's buffer: 0, or 1 + the peer whose flag never arrived
+HDS_EXPORT int hds_symm_error(void* base) {
+  uint32_t v = 0;
+  hipError_t e = hipMemcpy(&v, static_cast<char*>(base) + kErrOff, 4, hipMemcpyDeviceToHost);
+  return e != hipSuccess ? -(int)e : (int)v;
+}
+
+// dtype: 0 fp32, 1 bf16, 2 fp16 (ops/native.py dt())
+HDS_EXPORT int hds_symm_allreduce(const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch,
+                                  const void* in, void* out, int64_t n, int dtype, hipStream_t st) {
+  SymmArgs a;
+  const int64_t es = dtype == 0 ? 4 : 2;
+  if (!make_args(a, bases, rank, world, cap, epoch, in, out, n) || n % 8 || n * es > cap) return hipErrorInvalidValue;
+  const dim3 grid(blocks_for(n / 8));
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(symm_allreduce_kernel<float>, grid, dim3(kThreads), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(symm_allreduce_kernel<bf16>, grid, dim3(kThreads), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(symm_allreduce_kernel<_Float16>, grid, dim3(kThreads), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+HDS_EXPORT int hds_symm_allgather(const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch,
+                                  const void* in, void* out, int64_t nbytes, hipStream_t st) {
+  SymmArgs a;
+  if (!make_args(a, bases, rank, world, cap, epoch, in, out, nbytes) || nbytes % 16 || nbytes > cap)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(symm_allgather_kernel, dim3(blocks_for(nbytes / 16)), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+HDS_EXPORT int hds_symm_reduce_scatter(const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch,
+                                       const void* in, void* out, int64_t n, int dtype, hipStream_t st) {
+  SymmArgs a;
+  const int64_t es = dtype == 0 ? 4 : 2;
+  if (!make_args(a, bases, rank, world, cap, epoch, in, out, n) || n % 8 || world * n * es > cap)
+    return hipErrorInvalidValue;
+  const dim3 grid(blocks_for(n / 8));
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(symm_reduce_scatter_kernel<float>, grid, dim3(kThreads), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(symm_reduce_scatter_kernel<bf16>, grid, dim3(kThreads), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(symm_reduce_scatter_kernel<_Float16>, grid, dim3(kThreads), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}

@@ -34,6 +34,9 @@ def _megatron_attn(layer):
 
 
 def is_megatron_layer(m):
+    # HF GPT-NeoX / BLOOM blocks share the attribute names; they have their own containers (inference/containers.py)
+    if type(m).__module__.startswith("transformers."):
+        return False
     a, _ = _megatron_attn(m)
     return (a is not None and hasattr(m, "input_layernorm") and hasattr(m, "post_attention_layernorm")
             and hasattr(m, "mlp"))

@@ -221,7 +221,8 @@ class RaggedTransformer:
 
     def _allreduce(self, x):
         if self.tp > 1:
-            dist.all_reduce(x, group=self.tp_group)
+            from ...comm.symmetric import small_all_reduce
+            small_all_reduce(x, self.tp_group)  # one-shot over xGMI for decode-sized messages when enabled
         return x
 
     def _norm(self, x, w, b, residual=None):

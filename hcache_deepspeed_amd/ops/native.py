@@ -17,7 +17,7 @@ _lock = threading.Lock()
 _klib = None
 _hlib = None
 
-# argument spec letters: p=void*, i=int32, l=int64, f=float, s=hipStream_t
+# argument spec letters: p=void*, i=int32, u=uint32, l=int64, f=float, s=hipStream_t
 _KERNEL_SIGS = {
     "hds_norm_fwd": "iii" + "p" * 8 + "ii" + "f" + "s",
     "hds_norm_bwd_nparts": "i",
@@ -88,9 +88,18 @@ _KERNEL_SIGS = {
     "hds_grouped_gemm": "ppppp" + "iiiiii" + "s",
     "hds_evoformer_fwd": "ppppp" + "i" + "pp" + "iiiii" + "f" + "s",
     "hds_nhwc_bias_add": "i" + "ppppp" + "l" + "ii" + "s",
+    "hds_symm_header_bytes": "",
+    "hds_symm_alloc": "lpp",
+    "hds_symm_open": "pp",
+    "hds_symm_close": "p",
+    "hds_symm_free": "p",
+    "hds_symm_error": "p",
+    "hds_symm_allreduce": "p" + "ii" + "l" + "u" + "pp" + "l" + "i" + "s",
+    "hds_symm_allgather": "p" + "ii" + "l" + "u" + "pp" + "l" + "s",
+    "hds_symm_reduce_scatter": "p" + "ii" + "l" + "u" + "pp" + "l" + "i" + "s",
 }
 
-_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}
+_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "u": ctypes.c_uint32, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}
 
 
 def _bind(lib, sigs):

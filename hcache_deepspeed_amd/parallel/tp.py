@@ -48,8 +48,8 @@ class _AllReduceFwd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group):
         if _ws(group) > 1:
-            x = x.contiguous()
-            dist.all_reduce(x, group=group)
+            from ..comm.symmetric import small_all_reduce
+            x = small_all_reduce(x.contiguous(), group)
         return x
 
     @staticmethod

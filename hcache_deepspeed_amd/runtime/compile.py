@@ -19,8 +19,11 @@ already a runtime mechanism of the engine, driven by the module-execution trace 
     right after ``step()`` on a copy stream and come back during the late backward, at the trace position the
     ``plan_state_reload`` pass picks from the profiled step (runtime/zero/state_offload.py);
   * offload_parameters                          -> ZeRO-Infinity parameter offload (configured at init);
-  * double_buffer / symmetric_memory            -> RCCL reduce-scatter buckets are already double-buffered per
-    unit; symmetric memory has no RCCL analogue here and is ignored with a warning.
+  * double_buffer                               -> RCCL reduce-scatter buckets are already double-buffered per
+    unit;
+  * symmetric_memory                            -> the ZeRO unit all-gathers / reduce-scatters of intra-node groups
+    run as one-kernel direct-read collectives over IPC-mapped uncached buffers (comm/symmetric.py,
+    csrc/kernels/symm_comm.hip; reference csrc/compile/z3.cpp:91-110).
 
 The gather schedule itself is compiled (hcache_deepspeed_amd/compile/): with ``deepcompile`` at ZeRO-3 a
 ``DeepCompileBackend`` profiles one step of the unit trace (HIP-event timestamps, live HBM bytes), measures an
@@ -109,8 +112,11 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
         # reduce-scatters go through the C++ RCCL executor (comm/native_rccl.py) on its own priority stream
         engine.optimizer.enable_native_comm()
     times["native_comm"] = time.perf_counter() - t0
-    if cfg.symmetric_memory:
-        logger.warning("compile: symmetric_memory has no RCCL equivalent here; ignored")
+    t0 = time.perf_counter()
+    if cfg.symmetric_memory and engine.optimizer is not None and hasattr(engine.optimizer, "enable_symmetric_comm"):
+        # one-kernel direct-read unit collectives over IPC-mapped symmetric buffers (comm/symmetric.py)
+        engine.optimizer.enable_symmetric_comm()
+    times["symmetric_memory"] = time.perf_counter() - t0
     for name, fn in _user_passes.items():
         t0 = time.perf_counter()
         fn(engine)

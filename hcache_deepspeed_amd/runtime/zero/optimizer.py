@@ -104,6 +104,17 @@ class _EventWork:
         return True
 
 
+class _SymmWork(_EventWork):
+    """Symmetric-memory collective on its own stream; timed by events (``_get_duration`` like a c10d Work)."""
+
+    def __init__(self, ev0, ev):
+        super().__init__(ev)
+        self.ev0 = ev0
+
+    def _get_duration(self):
+        return self.ev0.elapsed_time(self.ev) if self.ev.query() else None
+
+
 class _NvmeFetch:
     """In-flight NVMe parameter fetch of one unit: swap-file read -> pinned staging -> H2D (+ all-gather)."""
 
@@ -878,13 +889,65 @@ class ZeroOptimizer:
             cache[key] = RcclCommunicator(group)
         return cache[key]
 
+    def enable_symmetric_comm(self, cap_limit_bytes=1 << 30):
+        """``compile.symmetric_memory``: unit all-gathers / reduce-scatters of intra-node groups run as one-kernel
+        direct-read collectives over symmetric (IPC-mapped, uncached) buffers (comm/symmetric.py) on two dedicated
+        priority streams -- the reference's SymmetricMemory all-gather (csrc/compile/z3.cpp:91-110). Each buffer is
+        sized for the largest unit collective of its group (up to ``cap_limit_bytes``; larger units keep RCCL).
+        Collective: every rank must call it. Returns False (RCCL kept) on CPU or for groups of > 8 ranks."""
+        from ...comm import symmetric
+        if self.device.type != "cuda":
+            log_dist("symmetric_memory: CPU run, keeping torch.distributed", ranks=[0])
+            return False
+        need = {}
+        lp_es = torch.empty(0, dtype=self.dtype).element_size()
+        rs_es = torch.empty(0, dtype=self.comm_dtype).element_size()
+        for u in self.units:
+            if u.world <= 1 or u.expert_key is not None:
+                continue
+            for kind, g, nb in (("ag", u.ag_group, u.shard * lp_es), ("rs", u.rs_group, u.padded * rs_es)):
+                if nb > cap_limit_bytes:
+                    continue
+                key = (kind, id(g))
+                need[key] = (g, max(need.get(key, (g, 0))[1], nb))
+        if not need or not all(symmetric.supported(g) for g, _ in need.values()):
+            log_dist("symmetric_memory: no intra-node group of <= 8 ranks, keeping RCCL", ranks=[0])
+            return False
+        self._symm = {key: symmetric.SymmetricMemory(g, nb) for key, (g, nb) in need.items()}
+        self._symm_streams = {k: torch.cuda.Stream(device=self.device, priority=-1) for k in ("ag", "rs")}
+        log_dist(f"symmetric_memory: {len(self._symm)} buffers, "
+                 f"{sum(sm.cap for sm in self._symm.values()) * 2 / 2**20:.0f} MiB per rank", ranks=[0])
+        return True
+
+    def _symm_issue(self, kind, group, nbytes, fn):
+        sm = getattr(self, "_symm", {}).get((kind, id(group)))
+        if sm is None or not sm.fits(nbytes):
+            return None
+        s = self._symm_streams[kind]
+        s.wait_stream(torch.cuda.current_stream())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            e0.record(s)
+            fn(sm)
+            e1.record(s)
+        return _SymmWork(e0, e1)
+
     def _all_gather(self, out, inp, group):
+        w = self._symm_issue("ag", group, inp.numel() * inp.element_size(),
+                             lambda sm: sm.all_gather_into_tensor(out, inp))
+        if w is not None:
+            return w
         c = self._ncomm(group)
         if c is not None:
             return c.all_gather_into_tensor(out, inp, async_op=True)
         return dist.all_gather_into_tensor(out, inp, group=group, async_op=True)
 
     def _reduce_scatter(self, out, inp, group):
+        if out.numel() % 8 == 0 and inp.dtype == out.dtype:
+            w = self._symm_issue("rs", group, inp.numel() * inp.element_size(),
+                                 lambda sm: sm.reduce_scatter_tensor(out, inp))
+            if w is not None:
+                return w
         c = self._ncomm(group)
         if c is not None:
             return c.reduce_scatter_tensor(out, inp, async_op=True)

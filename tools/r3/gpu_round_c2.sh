@@ -15,6 +15,7 @@ for qd in 32 128; do
   timeout -k 10 120 python -u -m hcache_deepspeed_amd.nvme.ds_io --folder /tmp/hds_nvme --io_size 8G --read --queue_depth $qd --threads 8 --block_size 4M >> gpurun_out/rc/ds_io.log 2>&1 || exit 1
 done
 rm -rf /tmp/hds_nvme
+timeout -k 10 200 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_symmetric_gpu.py > gpurun_out/rc/symm.log 2>&1 || exit 1
 for lay in direct nt direct_sk2 nt_sk2; do
   timeout -k 5 60 python -u tools/r3/wgrad_down_diag.py $lay >> gpurun_out/rc/down_diag.log 2>&1 || exit 1
 done
