@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
     ap.add_argument("--offload-opt-states", action="store_true",
                     help="DeepCompile offload_adam_states: Adam moments + fp32 master on pinned host between steps")
+    ap.add_argument("--offload-params-compile", type=float, default=None, metavar="BUDGET_GIB",
+                    help="DeepCompile offload_parameters on the GPU-optimizer engine; the pass keeps shards on the "
+                         "device within BUDGET_GIB of HBM (0: every shard on the host)")
     ap.add_argument("--deepcompile", action="store_true",
                     help="engine.compile() with DeepCompile: profiled ZeRO-3 gather schedule (selective gather + prefetch)")
     args = ap.parse_args()
@@ -124,8 +127,11 @@ def main():
                                                                         "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }
-    if args.deepcompile or args.offload_opt_states:
-        ds_config["compile"] = {"deepcompile": bool(args.deepcompile), "offload_opt_states": bool(args.offload_opt_states)}
+    dc_on = args.deepcompile or args.offload_opt_states or args.offload_params_compile is not None
+    if dc_on:
+        ds_config["compile"] = {"deepcompile": bool(args.deepcompile or args.offload_params_compile is not None),
+                                "offload_opt_states": bool(args.offload_opt_states),
+                                "offload_parameters": args.offload_params_compile is not None}
     if args.offload != "none":
         ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True}
         if args.offload_param:
@@ -141,8 +147,9 @@ def main():
     if args.ckpt:
         model.gradient_checkpointing_enable()
     engine, _, _, _ = hds.initialize(model=model, config=ds_config)
-    if args.deepcompile or args.offload_opt_states:
-        engine.compile()  # schedule compiled after the profiled warmup step (compile/backend.py)
+    if dc_on:
+        kw = {} if args.offload_params_compile is None else {"mem_budget_bytes": args.offload_params_compile * 2**30}
+        engine.compile(compile_kwargs=kw)  # schedule compiled after the profiled warmup step (compile/backend.py)
     t_init = time.time() - t_init
     dev = engine.device
     S, mb = args.seq, args.micro_batch
@@ -251,6 +258,11 @@ def main():
         if so is not None:
             out["extra"]["offload_opt_states"] = so.stats()
             out["config"]["offload_opt_states"] = True
+        sched = getattr(engine.optimizer, "dc_schedule", None)
+        if sched is not None and "offload_parameters" in sched.meta:
+            out["extra"]["offload_parameters"] = {k: v for k, v in sched.meta["offload_parameters"].items()
+                                                  if k != "resident"}
+            out["config"]["offload_parameters"] = True
         ac = getattr(engine, "_activation_cache", None)
         if ac is not None:
             out["extra"]["act_cache"] = ac.stats()

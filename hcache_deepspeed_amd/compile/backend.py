@@ -21,7 +21,8 @@ import torch
 import torch.distributed as tdist
 
 from ..utils.logging import log_dist
-from .passes import CompiledSchedule, UnitGraph, compile_schedule, plan_state_offload, plan_state_reload
+from .passes import (CompiledSchedule, UnitGraph, compile_schedule, plan_param_offload, plan_state_offload,
+                     plan_state_reload)
 from .profiler import CommPredictor, UnitProbe, combine, profile_allgather, profile_h2d
 
 
@@ -112,8 +113,21 @@ class DeepCompileBackend:
         self.times["comm_profile"] = time.perf_counter() - t0
         t0 = time.perf_counter()
         self.graph = UnitGraph(fwd, bwd, nbytes, gathered, peak, total)
-        sched = compile_schedule(self.graph, self.predictor, self.margin, self.mem_budget, self.max_buffered,
+        budget, pmeta = self.mem_budget, None
+        if getattr(opt, "param_offload_gpu_step", False):
+            # offload_parameters: the most-fetched shards stay on the device while the headroom allows; a resident
+            # world-1 unit needs no fetch at all, so it leaves the gathered set before the other passes run
+            head = budget if budget is not None else max(0.0, total * (1.0 - self.margin) - peak) if total else 0.0
+            shard = {u.uid: u.shard * esize for u in opt.units if not u.persistent}
+            res, used, pstats = plan_param_offload(self.graph, shard, head)
+            pmeta = dict(pstats, resident=sorted(res))
+            one = {u.uid for u in opt.units if u.world == 1}
+            self.graph = UnitGraph(fwd, bwd, nbytes, gathered - (res & one), peak, total)
+            budget = max(0.0, head - used)
+        sched = compile_schedule(self.graph, self.predictor, self.margin, budget, self.max_buffered,
                                  self.selective)
+        if pmeta is not None:
+            sched.meta["offload_parameters"] = pmeta
         so = getattr(opt, "state_offload", None)
         if so is not None and dev.type == "cuda":
             # offload_adam_states: the reload goes where the remaining backward covers the measured H2D time
@@ -129,6 +143,8 @@ class DeepCompileBackend:
         tdist.broadcast_object_list(obj, src=src, group=group)
         sched = CompiledSchedule.from_dict(obj[0])
         self.times["passes"] = time.perf_counter() - t0
+        if "offload_parameters" in sched.meta:
+            opt.set_param_residency(sched.meta["offload_parameters"]["resident"])
         opt.install_schedule(sched)
         if so is not None and "offload_adam_states" in sched.meta:
             so.reload_pos = sched.meta["offload_adam_states"]["reload_pos"]

@@ -9,6 +9,9 @@ Reference parity:
   * compile/passes/prefetch.py -- reorders all-gathers earlier under a memory limit (``schedule_prefetch``
     below). The reference walks the FX graph backwards and fuses small gathers; fetch units here are already
     flat, coalesced buffers (one all-gather per unit), so the pass only decides WHERE each gather is issued;
+  * compile/passes/offload_parameters.py -- parameter shards on pinned host, fetched (H2D + all-gather) at the
+    positions the prefetch pass plans; ``plan_param_offload`` keeps the most-fetched shards on the device while
+    the HBM budget allows (executed by runtime/zero/optimizer.py ``enable_param_offload``);
   * compile/passes/offload_adam_states.py -- optimizer states to pinned host after the step, back during the
     late backward (``plan_state_reload`` / ``plan_state_offload`` below, executed by
     runtime/zero/state_offload.py). ZeRO-1 needs no schedule here: its flat reduce already runs per unit as each
@@ -89,6 +92,30 @@ def zero3_compile(graph, resident=()):
                 prog.append((phase, k, "release", uid))
                 counts[f"releases_{phase}"] += 1
     return prog, counts
+
+
+def plan_param_offload(graph, shard_bytes, budget):
+    """Parameter offload (reference compile/passes/offload_parameters.py: every gathered parameter is reloaded from
+    the host before its all-gather and offloaded after its last use). The shards live on the host; with HBM to
+    spare, keeping a unit's shard on the device removes its host fetches, so the pass keeps the units with the most
+    fetches per step (forward + backward gathers of the zero3 program), then the smallest, while their shard bytes
+    fit ``budget``. Returns (resident uids, bytes, stats)."""
+    prog, _ = zero3_compile(graph)
+    fetches = defaultdict(int)
+    for _, _, op, uid in prog:
+        if op == "gather":
+            fetches[uid] += 1
+    cands = sorted((uid for uid in shard_bytes if fetches.get(uid)), key=lambda u: (-fetches[u], shard_bytes[u], u))
+    res, used = set(), 0
+    for uid in cands:
+        b = shard_bytes[uid]
+        if used + b <= budget:
+            res.add(uid)
+            used += b
+    off = [uid for uid in cands if uid not in res]
+    return res, used, {"resident_units": len(res), "resident_bytes": int(used), "offloaded_units": len(off),
+                       "offloaded_bytes": int(sum(shard_bytes[u] for u in off)),
+                       "host_fetches_per_step": int(sum(fetches[u] for u in off))}
 
 
 def plan_state_reload(graph, state_bytes, h2d, margin=0.2, mem_limit=None):

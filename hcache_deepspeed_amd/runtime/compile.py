@@ -18,7 +18,9 @@ already a runtime mechanism of the engine, driven by the module-execution trace 
   * offload_opt_states                          -> optimizer states (and the fp32 master) move to pinned host
     right after ``step()`` on a copy stream and come back during the late backward, at the trace position the
     ``plan_state_reload`` pass picks from the profiled step (runtime/zero/state_offload.py);
-  * offload_parameters                          -> ZeRO-Infinity parameter offload (configured at init);
+  * offload_parameters                          -> parameter shards on pinned host (ZeRO-Infinity at init, or
+    switched on here for a GPU-optimizer ZeRO-3 engine): fetches are H2D + all-gather at the planned prefetch
+    positions; the ``plan_param_offload`` pass keeps the most-fetched shards on the device within the HBM budget;
   * double_buffer                               -> RCCL reduce-scatter buckets are already double-buffered per
     unit;
   * symmetric_memory                            -> the ZeRO unit all-gathers / reduce-scatters of intra-node groups
@@ -91,9 +93,15 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
             "offload_opt_states needs the ZeRO optimizer"
         engine.optimizer.enable_state_offload(include_master=bool((compile_kwargs or {}).get("offload_master", True)))
     times["offload_adam_states"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     if cfg.offload_parameters and not engine._config.zero_config.offload_param.enabled:
-        logger.warning("compile: offload_parameters requires zero_optimization.offload_param at initialize(); "
-                       "parameters stay on device")
+        # parameter shards to pinned host, fetched by the (compiled) prefetch schedule; the GPU optimizer step writes
+        # them back per unit (runtime/zero/optimizer.py enable_param_offload, compile/passes.py plan_param_offload)
+        opt = engine.optimizer
+        if opt is None or not hasattr(opt, "enable_param_offload") or not opt.enable_param_offload():
+            logger.warning("compile: offload_parameters needs a ZeRO-3 engine with a fused optimizer and a "
+                           "bf16/fp16 compute dtype; parameters stay on device")
+    times["offload_parameters"] = time.perf_counter() - t0
     if cfg.deepcompile and engine.zero_optimization_stage() == 3:
         # profile-guided gather schedule (compile/backend.py): profiled on a later step, then installed
         from ..compile import DeepCompileBackend

@@ -839,6 +839,9 @@ class ZeroOptimizer:
         if self.nvme_param:
             slot, view, req = self.param_swapper.swap_in(u.store_off, u.shard)
             return _NvmeFetch(self, u, full, slot, view, req)
+        dev = getattr(u, "dev_shard", None)
+        if dev is not None:  # offload_parameters: resident device copy, no PCIe
+            return self._all_gather(full, dev, u.ag_group)
         work, _ = self._h2d_from(u, full, u.shard_tensor)
         return work
 
@@ -852,6 +855,9 @@ class ZeroOptimizer:
             tmp = src.to(self.device)
             return dist.all_gather_into_tensor(full, tmp, group=u.ag_group, async_op=True), None
         s.wait_stream(torch.cuda.current_stream())
+        ready = getattr(u, "lp_ready", None)
+        if ready is not None:
+            s.wait_event(ready)  # offload_parameters: this unit's host shard was written back by the step
         with torch.cuda.stream(s):
             if u.world == 1:
                 full.copy_(src, non_blocking=True)
@@ -888,6 +894,103 @@ class ZeroOptimizer:
             from ...comm.native_rccl import RcclCommunicator
             cache[key] = RcclCommunicator(group)
         return cache[key]
+
+    def enable_param_offload(self):
+        """DeepCompile ``offload_parameters`` on a GPU-optimizer ZeRO-3 engine (reference
+        compile/passes/offload_parameters.py, csrc/includes/deepcompile.h ``DSParam::offload/reload``): the
+        compute-dtype parameter shards move to pinned host memory and every fetch becomes an H2D copy (+ the
+        all-gather) on the parameter stream -- the ZeRO-Infinity fetch path, placed by the compiled prefetch schedule.
+        The fused optimizer step still runs on the device: it writes the updated shards into a transient device
+        buffer that goes back to the host unit by unit, each copy with an event the unit's next fetch waits on
+        (``_publish_lp``). Units the ``plan_param_offload`` pass keeps resident get a device copy of their shard
+        (``set_param_residency``). Returns False when not applicable (not ZeRO-3, parameters already offloaded, fp32
+        master aliasing the shard, generic torch optimizer)."""
+        s = self.store
+        if (self.stage != 3 or self.offload_param or self.kind == "generic" or s.master is None
+                or s.master.data_ptr() == s.lp.data_ptr()):
+            return False
+        cuda = self.device.type == "cuda"
+        if cuda:
+            torch.cuda.synchronize(self.device)
+        host = torch.empty(s.numel, dtype=self.dtype, pin_memory=cuda)
+        host.copy_(s.lp)
+        empty = _empty(self.dtype, self.device)
+        for u in self.units:
+            hs = host[u.store_off:u.store_off + u.shard]
+            if u.persistent and u.world == 1 and u.full is not None:
+                full = torch.empty(u.padded, dtype=self.dtype, device=self.device)  # it aliased the device flat
+                full.copy_(u.full)
+                u.full = full
+                u.bind_params(full)
+            elif not u.persistent and u.world == 1:
+                u.unbind_grads()
+                u.unbind_params(empty)
+                u.full = None
+                u.status = NOT_AVAILABLE
+            u.shard_tensor = hs
+            u.dev_shard = None
+            u.lp_ready = None
+            for p in u.params:
+                p.ds_tensor = hs
+                p.ds_status = u.status
+        s.lp = host
+        self.offload_param = True
+        self.param_offload_gpu_step = True
+        if cuda:
+            self.param_h2d_stream = torch.cuda.Stream(self.device, priority=-1)
+            self._lp_d2h_stream = torch.cuda.Stream(self.device)
+        log_dist(f"offload_parameters: {s.numel * host.element_size() / 2**30:.2f} GiB of parameter shards on the "
+                 f"host", ranks=[0])
+        return True
+
+    def set_param_residency(self, uids):
+        """Keep a device copy of these offloaded units' shards (fetched without PCIe, refreshed by the step on the
+        device); every other offloaded unit drops its copy."""
+        keep = set(uids)
+        for u in self.units:
+            if u.persistent or not getattr(self, "param_offload_gpu_step", False):
+                continue
+            if u.uid in keep and getattr(u, "dev_shard", None) is None:
+                self._lp_wait(u)
+                u.dev_shard = torch.empty(u.shard, dtype=self.dtype, device=self.device)
+                u.dev_shard.copy_(u.shard_tensor)
+            elif u.uid not in keep:
+                u.dev_shard = None
+
+    def _lp_wait(self, u=None):
+        """Host-side wait for the step's parameter write-back (all units, or unit ``u``) before reading the host
+        shards on the CPU."""
+        st = getattr(self, "_lp_d2h_stream", None)
+        if st is None:
+            return
+        ev = getattr(u, "lp_ready", None) if u is not None else None
+        (ev.synchronize() if ev is not None else st.synchronize())
+
+    def _lp_written(self, u):
+        """The host shard of ``u`` was written on the CPU (checkpoint / safe_set): refresh its resident copy."""
+        if getattr(u, "dev_shard", None) is not None:
+            u.dev_shard.copy_(self.store.lp_slice(u))
+
+    def _publish_lp(self, tmp):
+        """offload_parameters step: the updated shards (device buffer ``tmp``) refresh the resident units' device
+        copies (D2D) and go back to the pinned host shards in forward-trace order on the write-back stream, one event
+        per unit; persistent units rebuild their gathered buffer from ``tmp`` in ``_post_step_gather``."""
+        order = list(dict.fromkeys(self._fwd_trace)) + [u.uid for u in self.units]
+        for u in self.units:
+            if getattr(u, "dev_shard", None) is not None:
+                u.dev_shard.copy_(tmp[u.store_off:u.store_off + u.shard])
+        st = getattr(self, "_lp_d2h_stream", None)
+        if st is None:
+            self.store.lp.copy_(tmp)
+            return
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            for uid in dict.fromkeys(order):
+                u = self.units[uid]
+                self.store.lp_slice(u).copy_(tmp[u.store_off:u.store_off + u.shard], non_blocking=True)
+                u.lp_ready = torch.cuda.Event()
+                u.lp_ready.record(st)
+        tmp.record_stream(st)
 
     def enable_symmetric_comm(self, cap_limit_bytes=1 << 30):
         """``compile.symmetric_memory``: unit all-gathers / reduce-scatters of intra-node groups run as one-kernel
@@ -955,9 +1058,15 @@ class ZeroOptimizer:
 
     def _gather(self, u, wait=True):
         if u.status == NOT_AVAILABLE:
-            full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
+            dev = getattr(u, "dev_shard", None)
+            if dev is not None and u.world == 1:
+                full = dev  # resident shard IS the unit: bind it, nothing to fetch
+            else:
+                full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
             u.post_gather = None
-            if self.offload_param:
+            if dev is not None and u.world == 1:
+                u.work = _DoneWork()
+            elif self.offload_param:
                 u.work = self._h2d_gather(u, full)
             elif self.in_backward and getattr(u, "sec", None) is not None:
                 # hpZ: backward re-gather from the secondary (intra-group) partition
@@ -1468,9 +1577,13 @@ class ZeroOptimizer:
             self._generic_opt.step()
             s.lp.copy_(s.master)
         else:
+            lp_flat = s.lp
+            if getattr(self, "param_offload_gpu_step", False):
+                lp_flat = torch.empty(s.numel, dtype=self.dtype, device=self.device)
+                self._step_lp = lp_flat
             for sg in s.segments:
                 g = self._seg_group(sg)
-                p32, gr, lp = s.seg(s.master, sg), s.seg(s.grad, sg), s.seg(s.lp, sg)
+                p32, gr, lp = s.seg(s.master, sg), s.seg(s.grad, sg), s.seg(lp_flat, sg)
                 if self.kind == "adam":
                     fused.adam_flat(p32, gr, s.seg(s.states["exp_avg"], sg), s.seg(s.states["exp_avg_sq"], sg),
                                     g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
@@ -1483,7 +1596,10 @@ class ZeroOptimizer:
                 elif self.kind == "adagrad":
                     fused.adagrad_flat(p32, gr, s.seg(s.states["sum"], sg), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
                                        g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
-        self._post_step_gather()
+        tmp = self.__dict__.pop("_step_lp", None)
+        if tmp is not None:
+            self._publish_lp(tmp)
+        self._post_step_gather(tmp)
         self.zero_grad()
         if self.state_offload is not None:
             self.state_offload.offload()  # D2H overlaps the next forward
@@ -1523,12 +1639,19 @@ class ZeroOptimizer:
             if self.loss_scaler.dynamic:
                 dist.all_reduce(self._inf_buf, op=dist.ReduceOp.MAX, group=self.mp_group)
 
-    def _post_step_gather(self):
-        """ZeRO-1/2: rebuild the persistent full parameters from the updated shards."""
+    def _post_step_gather(self, dev_lp=None):
+        """ZeRO-1/2: rebuild the persistent full parameters from the updated shards (``dev_lp``: the step's device
+        copy of the shards when offload_parameters keeps them on the host)."""
         works = []
         for u in self.units:
             if self.offload_param and u.persistent and u.full is not None:
-                if self.nvme_param:
+                if dev_lp is not None:
+                    src = dev_lp[u.store_off:u.store_off + u.shard]
+                    if u.world == 1:
+                        u.full.copy_(src)
+                    else:
+                        works.append(self._all_gather(u.full, src, u.ag_group))
+                elif self.nvme_param:
                     works.append(self._h2d_gather(u, u.full))
                 elif u.world == 1:
                     u.full.copy_(u.shard_tensor)
@@ -1669,7 +1792,11 @@ class ZeroOptimizer:
         self._post_step_gather()
 
     def _master_to_lp(self):
+        self._lp_wait()
         self.store.lp.copy_(self.store.master)
+        for u in self.units:
+            if getattr(u, "dev_shard", None) is not None:
+                u.dev_shard.copy_(self.store.lp_slice(u))
 
     def refresh_fp32_from_lp(self):
         with torch.no_grad():
@@ -1683,6 +1810,7 @@ class ZeroOptimizer:
             self._lp_to_master()
 
     def _lp_to_master(self):
+        self._lp_wait()
         self.store.master.copy_(self.store.lp)
 
     # ------------------------------------------------------------------------------------

@@ -99,7 +99,9 @@ def _set_full(param, value, key):
             src = src * (z.layout_world_for_avg() * z.loss_scaler.loss_scale)
         buf[lo:hi].copy_(src)
         if key == _FP32:
+            z._lp_wait()
             z.store.lp[lo:hi].copy_(buf[lo:hi])
+            z._lp_written(u)
     if key == _FP32:
         z._post_step_gather()  # collective: every rank refreshes the gathered copies
 
@@ -154,7 +156,9 @@ def _set_local(param, value, key):
     buf = _buffer(z, key)
     buf[lo:hi].copy_(value.reshape(-1).to(buf.dtype))
     if key == _FP32:
+        z._lp_wait()
         z.store.lp[lo:hi].copy_(buf[lo:hi])
+        z._lp_written(u)
 
 
 def safe_get_local_grad(param):

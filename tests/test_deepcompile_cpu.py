@@ -192,3 +192,66 @@ def test_offload_adam_states_keeps_trajectory(stage, world):
     """Optimizer states and the fp32 master offloaded after every step and reloaded in the next backward: the
     training trajectory is bit-identical to keeping them resident (GAS=2: only the boundary step moves them)."""
     run_distributed(_state_offload_run, world, stage, None)
+
+
+def test_param_offload_plan():
+    """offload_parameters pass: units fetched in both phases are kept on the device first, then the smallest, within
+    the budget; units with no fetch are ignored."""
+    from hcache_deepspeed_amd.compile import UnitGraph, plan_param_offload, zero3_compile
+    fwd = [(i, i, 1e-3, 0) for i in range(4)]
+    bwd = [(i, i, 1e-3, 0) for i in (3, 2, 1)]  # unit 0 has no backward (no fetch there)
+    g = UnitGraph(fwd, bwd, {i: 100 for i in range(4)}, {0, 1, 2, 3})
+    assert len(zero3_compile(g)[0]) == 14
+    res, used, st = plan_param_offload(g, {0: 10, 1: 30, 2: 20, 3: 20}, budget=45)
+    assert res == {2, 3} and used == 40
+    assert st["offloaded_units"] == 2 and st["host_fetches_per_step"] == 3  # unit 1 twice, unit 0 once
+    res, used, _ = plan_param_offload(g, {0: 10, 1: 30, 2: 20, 3: 20}, budget=0)
+    assert res == set() and used == 0
+
+
+def _param_offload_run(rank, world, out):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.utils.tensor_fragment import safe_get_full_fp32_param
+    res = {}
+    # (offload_parameters, mem budget of the passes, offload_opt_states too)
+    for mode, (off, budget, states) in {"base": (False, None, False), "all": (True, 0, False),
+                                        "some": (True, 80000, False), "everything": (True, 0, True)}.items():
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(**TINY))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "bf16": {"enabled": True},
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}, "zero_optimization": {"stage": 3},
+               "compile": {"deepcompile": off, "offload_parameters": off, "offload_opt_states": states}}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        if off:
+            eng.compile(compile_kwargs={"mem_budget_bytes": budget, "comm_sizes": [4096, 65536]})
+            assert eng.optimizer.offload_param and eng.optimizer.param_offload_gpu_step
+        g = torch.Generator().manual_seed(5 + rank)
+        losses = []
+        for _ in range(5):
+            x = torch.randint(0, TINY["vocab_size"], (2, 12), generator=g)
+            loss = eng(x, labels=x)
+            eng.backward(loss)
+            eng.step()
+            losses.append(float(loss))
+        z = eng.optimizer
+        if off:
+            meta = z.dc_schedule.meta["offload_parameters"]
+            dev = [u.uid for u in z.units if getattr(u, "dev_shard", None) is not None]
+            assert sorted(dev) == meta["resident"]
+            if budget == 0:
+                assert meta["resident_units"] == 0 and meta["offloaded_units"] > 0
+            else:
+                assert 0 < meta["resident_units"] and meta["offloaded_units"] > 0, meta
+        res[mode] = (losses, [safe_get_full_fp32_param(p).clone() for p in eng.module.parameters()])
+    for mode in ("all", "some", "everything"):
+        assert res[mode][0] == res["base"][0], (mode, res[mode][0], res["base"][0])
+        assert all(torch.equal(a, b) for a, b in zip(res[mode][1], res["base"][1])), mode
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_offload_parameters_keeps_trajectory(world):
+    """compile.offload_parameters on a GPU-optimizer ZeRO-3 engine: shards on the host, fetched by the compiled
+    schedule, some kept on the device by the pass under a budget, combined with optimizer-state offload: the training
+    trajectory and final weights are bit-identical to the resident run."""
+    run_distributed(_param_offload_run, world, None)

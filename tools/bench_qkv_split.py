@@ -38,8 +38,6 @@ def main():
                                                                 for k, v in r.items()}))
 
 
-
-
 def slices():
     """The framework's split forward (two GEMMs into column slices of one output) vs fused, at the bench shape."""
     from hcache_deepspeed_amd.runtime.zero.linear import _split_fwd
@@ -48,7 +46,11 @@ def slices():
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
     ref = F.linear(x, w)
     got = _split_fwd(x, w, 4096)
-    assert torch.equal(ref, got) or (ref.float() - got.float()).abs().max().item() < 1e-2
+    r32 = x[:4096].float() @ w.float().t()  # both must be bf16 roundings of the same product (reduction order aside)
+    e_ref = (ref[:4096].float() - r32).abs().max().item()
+    e_got = (got[:4096].float() - r32).abs().max().item()
+    print(json.dumps({"err_fused": e_ref, "err_split": e_got}), flush=True)
+    assert e_got <= 1.5 * e_ref + 1e-3
     fl = 2 * T * N * K
     r = {"fused_ms": t(lambda: F.linear(x, w)), "split_slices_ms": t(lambda: _split_fwd(x, w, 4096))}
     print(json.dumps({k: round(v, 4) for k, v in r.items()} | {k.replace("_ms", "_PFs"): round(fl / v / 1e12, 3)
