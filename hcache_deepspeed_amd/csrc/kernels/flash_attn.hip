@@ -462,6 +462,228 @@ __global__ __launch_bounds__(512) void attn_fwd_stg_kernel(AttnParams p) {
 }
 
 // =====================================================================================
+// forward, software-pipelined softmax (D = 128, 8 waves, 256 queries per workgroup)
+// =====================================================================================
+// The plain loop is a dependency chain per wave -- S = K.Q^T (16 MFMAs), then the softmax on the VALU, then
+// O += V^T.P (16 MFMAs) -- so a wave's MFMAs and its own softmax never overlap, and the two waves of a SIMD only
+// overlap by chance (PMC: ~37 % MFMA busy). Here iteration kt computes the NEXT tile's scores while this tile's
+// softmax runs: block A issues S_{kt+1} = K_{kt+1}.Q^T with the max / rescale / exponentials of S_kt between its
+// MFMAs (independent work, interleaved by sched_group_barrier, the guide's "fillers beside MFMAs": a 32x32x16
+// MFMA leaves ~24 issue cycles of its 32 for VALU); block B issues O += V_kt^T.P_kt with the row sum and the V^T
+// fragment reads beside it. The K ring runs one tile further ahead than V: at the top of iteration kt the wave
+// retires V_kt and K_{kt+1} (vmcnt(0)), the barrier frees V_{kt-1} / K_kt, and the DMA of V_{kt+1} / K_{kt+2} is
+// issued into those slots -- one barrier per tile. Every wave runs every tile of the workgroup's causal range (a
+// tile fully masked for a wave contributes exp(-inf) = 0), so the loop body has no wave-level branches that would
+// split the interleaved blocks.
+template <int D>
+__global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
+  constexpr int NW = 8, BM = 32 * NW;
+  constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
+  static_assert(D == 128, "software-pipelined forward: head_dim 128");
+  __shared__ __attribute__((aligned(16))) char smem[4 * TL];  // K[2], V[2]
+  int blk, hq, b;
+  lpt_ids(blk, hq, b);
+  int start, len;
+  seq_bounds(p, b, start, len);
+  const int nqb = (len + BM - 1) / BM;
+  const int qb = p.causal ? (gridDim.x - 1 - blk) : blk;
+  if (qb >= nqb || len == 0) return;
+  const int hk = hq / (p.hq / p.hkv);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q0 = qb * BM;
+  const int myq = q0 + 32 * w + (lane & 31);
+  const float c = p.scale * kLog2e;
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half (guide T5)
+
+  bf16x8 qf[KS];
+  {
+    const int qr = myq < len ? myq : len - 1;
+    const bf16* qp = p.q + (int64_t)(start + qr) * p.sq + (int64_t)hq * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+  }
+  int kt_end = (len + BN - 1) / BN;
+  if (p.causal) {
+    const int last = q0 + BM - 1 < len - 1 ? q0 + BM - 1 : len - 1;
+    kt_end = last / BN + 1;
+  }
+  int kt_begin = 0;
+  if (p.window > 0) {
+    const int first = q0 - p.window + 1;
+    kt_begin = first > 0 ? first / BN : 0;
+  }
+  auto rowp = [&](const bf16* base, int64_t stride, int kt) {
+    return [=](int row) {
+      int r = kt * BN + row;
+      r = r < len ? r : len - 1;
+      return base + (int64_t)(start + r) * stride + (int64_t)hk * D;
+    };
+  };
+  const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
+  const uint32_t P0 = rows_lane_off(0), P1 = rows_lane_off(32);
+  uint32_t y0, y1;
+  tr_lane_offs(y0, y1);
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  // prologue: K_0, V_0, K_1 in flight; S_0 once K_0 has landed
+  stage_tile_d<NW, D>(smem + 0, rowp(p.k, p.sk, kt_begin));
+  stage_tile_d<NW, D>(smem + 2 * TL, rowp(p.v, p.sv, kt_begin));
+  if (kt_begin + 1 < kt_end) {
+    stage_tile_d<NW, D>(smem + TL, rowp(p.k, p.sk, kt_begin + 1));
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this wave's 2 K_0 DMAs (issued first) have landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  }
+  __syncthreads();
+  f32x16 sc[2];
+  {
+    bf16x8 kr[2][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kr[0][ks] = read_rows_off_asm(smem, P0, ks);
+      kr[1][ks] = read_rows_off_asm(smem, P1, ks);
+    }
+    lds_wait<0>();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sc[t] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) sc[t] = mfma(kr[t][ks], qf[ks], sc[t]);
+    }
+  }
+
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
+    const char* Kn = smem + (buf ^ 1) * TL;  // K_{kt+1} (stale, unused data on the last tile)
+    const char* Vt = smem + 2 * TL + buf * TL;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V_kt and K_{kt+1} of this wave have landed
+    __syncthreads();                                   // ... of every wave; V_{kt-1} and K_kt are free
+    if (kt + 1 < kt_end) stage_tile_d<NW, D>(smem + 2 * TL + (buf ^ 1) * TL, rowp(p.v, p.sv, kt + 1));
+    if (kt + 2 < kt_end) stage_tile_d<NW, D>(smem + buf * TL, rowp(p.k, p.sk, kt + 2));
+
+    const int k0 = kt * BN;
+    const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
+                           (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) sc[t][r] = -INFINITY;
+    }
+
+    // ---- block A: S_{kt+1} = K_{kt+1}.Q^T beside the max, the rescale factor and exp(S_kt[keys 0..31]) ----
+    // K rows in 4 chunks of 4 k-steps (t = chunk >> 1), double-buffered: 32 registers instead of 64
+    f32x16 sn[2];
+    bf16x8 kr[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kr[0][i] = read_rows_off_asm(Kn, P0, i);
+    float tm0 = -INFINITY, tm1 = -INFINITY;  // two independent max chains
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      tm0 = max3_raw(tm0, sc[0][r], sc[0][r + 1]);
+      tm1 = max3_raw(tm1, sc[1][r], sc[1][r + 1]);
+    }
+    float tmax = fmaxf(tm0, tm1);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
+    const bool move = !__all(tmax <= m + kDeferThr);  // deferred running max (guide T13)
+    const float mnew = move ? fmaxf(m, tmax) : m;
+    const float alpha = move ? ((m == -INFINITY) ? 0.f : fast_exp2(m - mnew)) : 1.f;
+    m = mnew;
+    const float muse = (m == -INFINITY) ? 0.f : m;
+    if (move) {  // before the interleaved blocks: a branch after them would let the compiler sink the exponentials
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    }
+    float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = j >> 1;
+      if (j + 1 < 4) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kr[(j + 1) & 1][i] = read_rows_off_asm(Kn, (j + 1) >> 1 ? P1 : P0, 4 * ((j + 1) & 1) + i);
+        lds_wait<4>();
+      } else {
+        lds_wait<0>();
+      }
+      if ((j & 1) == 0) sn[t] = f32x16{};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sn[t] = mfma(kr[j & 1][i], qf[4 * (j & 1) + i], sn[t]);
+      // fillers: exponentials of 4 scores of keys 0..31 (and their row sum)
+#pragma unroll
+      for (int r = 4 * j; r < 4 * j + 4; ++r) {
+        const float e = fast_exp2(__builtin_fmaf(sc[0][r], c, -muse));
+        sc[0][r] = e;
+        (r & 1 ? rs1 : rs0) += e;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // then fma + exp + add
+      }
+    }
+    bf16x8 pb[4];
+    pb[0] = acc_to_b<0>(sc[0]);
+    pb[1] = acc_to_b<1>(sc[0]);
+
+    // ---- block B: O += V_kt^T.P_kt, key sub-block st outer, with exp(S_kt[keys 32..63]) beside the first half ----
+    bf16x8 vf[2][DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) vf[0][dt] = read_tr_off_asm(Vt, y0, y1, 0, dt);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      if (st + 1 < 4) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) vf[(st + 1) & 1][dt] = read_tr_off_asm(Vt, y0, y1, st + 1, dt);
+        lds_wait<8>();
+      } else {
+        lds_wait<0>();
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(vf[st & 1][dt], pb[st], o[dt]);
+      if (st < 2) {
+#pragma unroll
+        for (int r = 8 * st; r < 8 * st + 8; ++r) {
+          const float e = fast_exp2(__builtin_fmaf(sc[1][r], c, -muse));
+          sc[1][r] = e;
+          (r & 1 ? rs1 : rs0) += e;
+        }
+        if (st == 1) {
+          pb[2] = acc_to_b<0>(sc[1]);
+          pb[3] = acc_to_b<1>(sc[1]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+        }
+      }
+    }
+    float rs = rs0 + rs1;
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    sc[0] = sn[0];
+    sc[1] = sn[1];
+  }
+
+  if (myq < len) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* op = p.o + (int64_t)(start + myq) * p.so + (int64_t)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) store_row_block<D>(op, o[dt], dt, h, inv);
+    if (h == 0 && p.lse) {
+      const float lse = (l > 0.f) ? (m + __log2f(l)) / kLog2e : -INFINITY;
+      p.lse[(int64_t)hq * p.total_tokens + start + myq] = lse;
+    }
+  }
+}
+
+// =====================================================================================
 // backward pre-pass: delta[hq][t] = sum_d dO * O   (16 lanes per row, 4 rows per wave)
 // =====================================================================================
 template <int D>
@@ -1099,9 +1321,9 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_bwd_pipe = 0;
 
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
-// 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max)
+// 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 4) return hipErrorInvalidValue;
+  if (var < 0 || var > 5) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1136,6 +1358,7 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
       if constexpr (D == 128) {  // the A/B variants exist for the training head dim only
         switch (g_fwd_var) {
           case 4: hipLaunchKernelGGL((attn_fwd_stg_kernel<D>), grid, dim3(512), 0, st, p); break;
+          case 5: hipLaunchKernelGGL((attn_fwd_sp_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;

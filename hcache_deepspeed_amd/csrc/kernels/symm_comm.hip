@@ -79,6 +79,14 @@ __device__ __forceinline__ void exchange(const SymmArgs& a) {
   __threadfence_system();
 }
 
+// raw copy of one 8-element vector (16 B for 16-bit types, 32 B for fp32)
+template <typename T>
+__device__ __forceinline__ void copy8(T* dst, const T* src) {
+#pragma unroll
+  for (int j = 0; j < (int)(8 * sizeof(T) / 16); ++j)
+    reinterpret_cast<u32x4*>(dst)[j] = reinterpret_cast<const u32x4*>(src)[j];
+}
+
 __device__ __forceinline__ void block_range(int64_t nvec, int64_t& lo, int64_t& hi) {
   const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
   lo = (int64_t)blockIdx.x * per;
@@ -92,10 +100,7 @@ __global__ __launch_bounds__(kThreads) void symm_allreduce_kernel(SymmArgs a) {
   block_range(a.n / 8, lo, hi);
   const T* in = reinterpret_cast<const T*>(a.in);
   T* mine = reinterpret_cast<T*>(data_ptr(a, a.rank));
-  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(in + 8 * i);
-    *reinterpret_cast<u32x4*>(mine + 8 * i) = v;
-  }
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) copy8(mine + 8 * i, in + 8 * i);
   exchange(a);
   T* out = reinterpret_cast<T*>(a.out);
   for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(kThreads) void symm_reduce_scatter_kernel(SymmArgs 
   for (int s = 0; s < a.world; ++s)
     for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
       const int64_t e = (int64_t)s * a.n + 8 * i;
-      *reinterpret_cast<u32x4*>(mine + e) = *reinterpret_cast<const u32x4*>(in + e);
+      copy8(mine + e, in + e);
     }
   exchange(a);
   T* out = reinterpret_cast<T*>(a.out);

@@ -642,9 +642,11 @@ def test_decode_attention_matches_reference_gpu(D, H, Hkv, S):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [4, 5])
 @pytest.mark.parametrize("case", ["causal", "full", "window", "varlen"])
-def test_flash_fwd_staggered_variant_gpu(case):
-    """Forward variant 4 (staggered wave groups, asm transposed reads) against the fp32 reference."""
+def test_flash_fwd_staggered_variant_gpu(case, variant):
+    """Forward variants 4 (staggered wave groups) and 5 (software-pipelined softmax) against variant 2 and the fp32
+    reference; the backward (which consumes the forward's LSE) must agree too."""
     from hcache_deepspeed_amd.ops import native
     from hcache_deepspeed_amd.ops.attention import flash_attn
     lib = native.kernels()
@@ -654,20 +656,29 @@ def test_flash_fwd_staggered_variant_gpu(case):
     k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
     kw = dict(causal=case != "full", window=100 if case == "window" else 0)
+    do = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
     try:
-        outs = {}
-        for var in (2, 4):
+        outs, grads = {}, {}
+        for var in (2, variant):
             assert lib.hds_attn_fwd_variant(var) == 0
+            qg, kg, vg = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
             if case == "varlen":
                 cu = torch.tensor([0, 333, 2 * S], device="cuda", dtype=torch.int32)
-                outs[var] = flash_attn(q.reshape(-1, Hq, D), k.reshape(-1, Hkv, D), v.reshape(-1, Hkv, D),
-                                       causal=True, cu_seqlens=cu)
+                o = flash_attn(qg.reshape(-1, Hq, D), kg.reshape(-1, Hkv, D), vg.reshape(-1, Hkv, D),
+                               causal=True, cu_seqlens=cu).reshape(B, S, Hq, D)
             else:
-                outs[var] = flash_attn(q, k, v, **kw)
+                o = flash_attn(qg, kg, vg, **kw)
+            o.backward(do)
+            outs[var] = o.detach()
+            grads[var] = (qg.grad, kg.grad, vg.grad)
     finally:
         lib.hds_attn_fwd_variant(2)
-    d = (outs[4].float() - outs[2].float()).abs().max().item()
+    d = (outs[variant].float() - outs[2].float()).abs().max().item()
     assert d < 3e-2, d  # both within bf16 rounding of each other (same math, different schedule)
+    for a, b in zip(grads[variant], grads[2]):
+        rel = ((a.float() - b.float()).norm() / b.float().norm()).item()
+        assert rel < 2e-2, rel
+    outs[4] = outs[variant]
     if case != "varlen":
         qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k.repeat_interleave(4, 2), v.repeat_interleave(4, 2)))
         s = qf @ kf.transpose(-1, -2) / D**0.5

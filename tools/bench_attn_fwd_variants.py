@@ -35,7 +35,7 @@ def main():
     s = s.masked_fill(torch.triu(torch.ones(S, S, device="cuda", dtype=torch.bool), 1), float("-inf"))
     ref = (torch.softmax(s, -1) @ vf).transpose(0, 1)
     base = None
-    for var in (2, 4, 2, 4):
+    for var in (2, 4, 5, 2, 5):
         lib.hds_attn_fwd_variant(var)
         o = flash_attn(q, k, v, causal=True)
         t = timeit(lambda: flash_attn(q, k, v, causal=True))
