@@ -24,6 +24,9 @@
 //   dq    : workgroup = 128 query rows of one (batch, q-head); sweeps key tiles; dQ in
 //           accumulators. Deterministic (no float atomics anywhere).
 // P is recomputed from the forward LSE; delta = rowsum(dO * O) comes from a tiny pre-kernel.
+#include <type_traits>
+#include <utility>
+
 #include "attn_common.h"
 
 using namespace hds;
@@ -465,16 +468,41 @@ __global__ __launch_bounds__(512) void attn_fwd_stg_kernel(AttnParams p) {
 // forward, software-pipelined softmax (D = 128, 8 waves, 256 queries per workgroup)
 // =====================================================================================
 // The plain loop is a dependency chain per wave -- S = K.Q^T (16 MFMAs), then the softmax on the VALU, then
-// O += V^T.P (16 MFMAs) -- so a wave's MFMAs and its own softmax never overlap, and the two waves of a SIMD only
-// overlap by chance (PMC: ~37 % MFMA busy). Here iteration kt computes the NEXT tile's scores while this tile's
-// softmax runs: block A issues S_{kt+1} = K_{kt+1}.Q^T with the max / rescale / exponentials of S_kt between its
-// MFMAs (independent work, interleaved by sched_group_barrier, the guide's "fillers beside MFMAs": a 32x32x16
-// MFMA leaves ~24 issue cycles of its 32 for VALU); block B issues O += V_kt^T.P_kt with the row sum and the V^T
-// fragment reads beside it. The K ring runs one tile further ahead than V: at the top of iteration kt the wave
-// retires V_kt and K_{kt+1} (vmcnt(0)), the barrier frees V_{kt-1} / K_kt, and the DMA of V_{kt+1} / K_{kt+2} is
-// issued into those slots -- one barrier per tile. Every wave runs every tile of the workgroup's causal range (a
-// tile fully masked for a wave contributes exp(-inf) = 0), so the loop body has no wave-level branches that would
-// split the interleaved blocks.
+// O += V^T.P (16 MFMAs) -- so a wave's MFMAs and its own softmax never overlap. Here iteration kt computes the NEXT
+// tile's scores while this tile's softmax runs: block A issues S_{kt+1} = K_{kt+1}.Q^T with the max / rescale /
+// exponentials of S_kt between its MFMAs (independent work, interleaved by sched_group_barrier: a 32x32x16 MFMA
+// leaves ~24 of its 32 issue cycles to VALU); block B issues O += V_kt^T.P_kt with the other half of the
+// exponentials and the row sums beside it. The K ring runs one tile further ahead than V: at the top of iteration kt
+// the wave retires V_kt and K_{kt+1} (vmcnt(0)), the barrier frees V_{kt-1} / K_kt, and the DMA of V_{kt+1} /
+// K_{kt+2} goes into those slots -- one barrier per tile.
+// Fixed per-tile VALU is removed as well (PMC: ~8 VALU per MFMA, the SIMD's issue port being the limit): the loop is
+// unrolled by two so every LDS slot offset is a compile-time ds_read immediate on 16 per-lane address registers
+// computed once (no address VALU per read), and a full tile's LDS-DMA source is a uniform base plus a per-lane
+// 32-bit offset computed once (clamped per-row addressing only on the last, partial tile). Every wave runs every tile
+// of the workgroup's causal range (a fully masked tile contributes exp(-inf) = 0), so the loop body has no
+// wave-level branches that would split the interleaved blocks.
+template <int IMM>
+__device__ __forceinline__ bf16x8 lds_b128(uint32_t a) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(IMM) : "memory");
+  return r;
+}
+template <int IMM>
+__device__ __forceinline__ bf16x8 lds_tr8(uint32_t a0, uint32_t a1) {
+  bf16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(a0), "n"(IMM) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a1), "n"(IMM) : "memory");
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <int... I, typename F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
 template <int D>
 __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   constexpr int NW = 8, BM = 32 * NW;
@@ -520,10 +548,40 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
       return base + (int64_t)(start + r) * stride + (int64_t)hk * D;
     };
   };
+  // LDS-DMA of a full tile: uniform tile base + per-lane byte offset (row 4n + lane/16, swizzled 16-B chunk)
+  int32_t dk[2], dv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 4 * (w * 2 + i) + (lane >> 4);
+    const int ch = (lane & 15) ^ swz(row);
+    dk[i] = (int32_t)(((int64_t)row * p.sk + 8 * ch) * 2);
+    dv[i] = (int32_t)(((int64_t)row * p.sv + 8 * ch) * 2);
+  }
+  auto stage = [&](char* dst, const bf16* base, int64_t stride, const int32_t* off, int kt) {
+    if (kt * BN + BN <= len) {
+      const char* tb = (const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((gbl_void*)(tb + off[i]), (lds_void*)(dst + (w * 2 + i) * 1024), 16, 0, 0);
+    } else {
+      stage_tile_d<NW, D>(dst, rowp(base, stride, kt));
+    }
+  };
   const int wq_lo = q0 + 32 * w, wq_hi = q0 + 32 * w + 31;
-  const uint32_t P0 = rows_lane_off(0), P1 = rows_lane_off(32);
-  uint32_t y0, y1;
-  tr_lane_offs(y0, y1);
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  uint32_t ak[KS], av0[DT], av1[DT];
+  {
+    const uint32_t P0 = rows_lane_off(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) ak[ks] = sbase + (P0 ^ (32u * ks));  // + 8192: rows 32..63 (same swizzle)
+    uint32_t y0, y1;
+    tr_lane_offs(y0, y1);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      av0[dt] = sbase + (y0 ^ (64u * dt));
+      av1[dt] = sbase + (y1 ^ (64u * dt));
+    }
+  }
 
   f32x16 o[DT];
 #pragma unroll
@@ -531,10 +589,10 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   float m = -INFINITY, l = 0.f;
 
   // prologue: K_0, V_0, K_1 in flight; S_0 once K_0 has landed
-  stage_tile_d<NW, D>(smem + 0, rowp(p.k, p.sk, kt_begin));
-  stage_tile_d<NW, D>(smem + 2 * TL, rowp(p.v, p.sv, kt_begin));
+  stage(smem + 0, p.k, p.sk, dk, kt_begin);
+  stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
   if (kt_begin + 1 < kt_end) {
-    stage_tile_d<NW, D>(smem + TL, rowp(p.k, p.sk, kt_begin + 1));
+    stage(smem + TL, p.k, p.sk, dk, kt_begin + 1);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this wave's 2 K_0 DMAs (issued first) have landed
   } else {
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -543,11 +601,11 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   f32x16 sc[2];
   {
     bf16x8 kr[2][KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      kr[0][ks] = read_rows_off_asm(smem, P0, ks);
-      kr[1][ks] = read_rows_off_asm(smem, P1, ks);
-    }
+    static_for<KS>([&](auto KSC) {
+      constexpr int ks = decltype(KSC)::value;
+      kr[0][ks] = lds_b128<0>(ak[ks]);
+      kr[1][ks] = lds_b128<8192>(ak[ks]);
+    });
     lds_wait<0>();
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -557,14 +615,14 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
     }
   }
 
-  for (int kt = kt_begin; kt < kt_end; ++kt) {
-    const int buf = (kt - kt_begin) & 1;
-    const char* Kn = smem + (buf ^ 1) * TL;  // K_{kt+1} (stale, unused data on the last tile)
-    const char* Vt = smem + 2 * TL + buf * TL;
+  auto tile = [&](auto BUFC, int kt) {
+    constexpr int buf = decltype(BUFC)::value;
+    constexpr int KN = (buf ^ 1) * TL;          // K_{kt+1}
+    constexpr int VT = 2 * TL + buf * TL;       // V_kt
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V_kt and K_{kt+1} of this wave have landed
     __syncthreads();                                   // ... of every wave; V_{kt-1} and K_kt are free
-    if (kt + 1 < kt_end) stage_tile_d<NW, D>(smem + 2 * TL + (buf ^ 1) * TL, rowp(p.v, p.sv, kt + 1));
-    if (kt + 2 < kt_end) stage_tile_d<NW, D>(smem + buf * TL, rowp(p.k, p.sk, kt + 2));
+    if (kt + 1 < kt_end) stage(smem + 2 * TL + (buf ^ 1) * TL, p.v, p.sv, dv, kt + 1);
+    if (kt + 2 < kt_end) stage(smem + buf * TL, p.k, p.sk, dk, kt + 2);
 
     const int k0 = kt * BN;
     const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
@@ -576,13 +634,6 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
         for (int r = 0; r < 16; ++r)
           if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) sc[t][r] = -INFINITY;
     }
-
-    // ---- block A: S_{kt+1} = K_{kt+1}.Q^T beside the max, the rescale factor and exp(S_kt[keys 0..31]) ----
-    // K rows in 4 chunks of 4 k-steps (t = chunk >> 1), double-buffered: 32 registers instead of 64
-    f32x16 sn[2];
-    bf16x8 kr[2][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) kr[0][i] = read_rows_off_asm(Kn, P0, i);
     float tm0 = -INFINITY, tm1 = -INFINITY;  // two independent max chains
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
@@ -600,21 +651,30 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
     }
+
+    // ---- block A: S_{kt+1} = K_{kt+1}.Q^T (4 chunks of 4 k-steps, double-buffered) beside exp(S_kt[keys 0..31])
+    f32x16 sn[2];
+    bf16x8 kr[2][4];
     float rs0 = 0.f, rs1 = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = j >> 1;
-      if (j + 1 < 4) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) kr[(j + 1) & 1][i] = read_rows_off_asm(Kn, (j + 1) >> 1 ? P1 : P0, 4 * ((j + 1) & 1) + i);
+    static_for<4>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      kr[0][i] = lds_b128<KN>(ak[i]);
+    });
+    static_for<4>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      constexpr int t = j >> 1;
+      if constexpr (j + 1 < 4) {
+        static_for<4>([&](auto IC) {
+          constexpr int i = decltype(IC)::value;
+          kr[(j + 1) & 1][i] = lds_b128<KN + 8192 * ((j + 1) >> 1)>(ak[4 * ((j + 1) & 1) + i]);
+        });
         lds_wait<4>();
       } else {
         lds_wait<0>();
       }
-      if ((j & 1) == 0) sn[t] = f32x16{};
+      if constexpr ((j & 1) == 0) sn[t] = f32x16{};
 #pragma unroll
       for (int i = 0; i < 4; ++i) sn[t] = mfma(kr[j & 1][i], qf[4 * (j & 1) + i], sn[t]);
-      // fillers: exponentials of 4 scores of keys 0..31 (and their row sum)
 #pragma unroll
       for (int r = 4 * j; r < 4 * j + 4; ++r) {
         const float e = fast_exp2(__builtin_fmaf(sc[0][r], c, -muse));
@@ -626,34 +686,38 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // then fma + exp + add
       }
-    }
+    });
     bf16x8 pb[4];
     pb[0] = acc_to_b<0>(sc[0]);
     pb[1] = acc_to_b<1>(sc[0]);
 
     // ---- block B: O += V_kt^T.P_kt, key sub-block st outer, with exp(S_kt[keys 32..63]) beside the first half ----
     bf16x8 vf[2][DT];
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) vf[0][dt] = read_tr_off_asm(Vt, y0, y1, 0, dt);
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      if (st + 1 < 4) {
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) vf[(st + 1) & 1][dt] = read_tr_off_asm(Vt, y0, y1, st + 1, dt);
+    static_for<DT>([&](auto DC) {
+      constexpr int dt = decltype(DC)::value;
+      vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
+    });
+    static_for<4>([&](auto SC) {
+      constexpr int st = decltype(SC)::value;
+      if constexpr (st + 1 < 4) {
+        static_for<DT>([&](auto DC) {
+          constexpr int dt = decltype(DC)::value;
+          vf[(st + 1) & 1][dt] = lds_tr8<VT + 4096 * (st + 1)>(av0[dt], av1[dt]);
+        });
         lds_wait<8>();
       } else {
         lds_wait<0>();
       }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(vf[st & 1][dt], pb[st], o[dt]);
-      if (st < 2) {
+      if constexpr (st < 2) {
 #pragma unroll
         for (int r = 8 * st; r < 8 * st + 8; ++r) {
           const float e = fast_exp2(__builtin_fmaf(sc[1][r], c, -muse));
           sc[1][r] = e;
           (r & 1 ? rs1 : rs0) += e;
         }
-        if (st == 1) {
+        if constexpr (st == 1) {
           pb[2] = acc_to_b<0>(sc[1]);
           pb[3] = acc_to_b<1>(sc[1]);
         }
@@ -663,13 +727,19 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
           __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
         }
       }
-    }
+    });
     float rs = rs0 + rs1;
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
     sc[0] = sn[0];
     sc[1] = sn[1];
+  };
+  int kt = kt_begin;
+  for (; kt + 1 < kt_end; kt += 2) {
+    tile(std::integral_constant<int, 0>{}, kt);
+    tile(std::integral_constant<int, 1>{}, kt + 1);
   }
+  if (kt < kt_end) tile(std::integral_constant<int, 0>{}, kt);
 
   if (myq < len) {
     const float inv = l > 0.f ? 1.f / l : 0.f;

@@ -18,12 +18,12 @@ def main():
     torch.manual_seed(0)
     with torch.device(dev):
         model = LlamaForCausalLM(llama3_8b()).to(torch.bfloat16).eval()
-    P, steps = 512, 24
+    P, steps = 512, 24  # +3 untimed graph-capture steps per case
     for B in (1, 8):
         for mode in ("graph", "eager"):
-            econf = {"dtype": "bf16", "state_manager": {"max_ragged_batch_size": B * P, "max_context": P + steps + 64,
+            econf = {"dtype": "bf16", "state_manager": {"max_ragged_batch_size": B * P, "max_context": P + steps + 128,
                                                          "kv_block_size": 64, "max_tracked_sequences": 4 * B}}
-            eng = build_engine_from_model(model, econf, device=dev, num_kv_blocks=B * ((P + steps + 63) // 64) + 16)
+            eng = build_engine_from_model(model, econf, device=dev, num_kv_blocks=B * ((P + steps + 127) // 64) + 16)
             if mode == "eager":
                 eng._model.decode_graph_max_batch = 0
             g = torch.Generator().manual_seed(1)
@@ -31,6 +31,10 @@ def main():
             logits, _ = eng.put(uids, [torch.randint(0, 128256, (P, ), generator=g) for _ in range(B)],
                                 capture_latents=False)
             nxt = logits.argmax(-1).cpu()
+            for _ in range(3):  # untimed: the decode graph for this batch size is captured here
+                logits, _ = eng.put(uids, [nxt[i:i + 1] for i in range(B)], capture_latents=False)
+                nxt = logits.argmax(-1).cpu()
+            torch.cuda.synchronize()
             m = eng._model
             orig_fwd, orig_graph = m.forward, m.forward_decode_graph
             acc = {"fwd_host_ms": 0.0, "fwd_gpu_ms": 0.0}
