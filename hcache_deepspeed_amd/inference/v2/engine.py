@@ -116,8 +116,11 @@ class InferenceEngineV2:
 
     # ------------------------------------------------------------------------------------------
     def put(self, batch_uids: Iterable[int], batch_tokens: Iterable[torch.Tensor], do_checks: bool = True,
-            capture_latents: bool = True) -> Tuple[torch.Tensor, List[Optional[torch.Tensor]]]:
-        """One ragged forward. Returns logits [n_seqs, V] and, per sequence, its latents [L, n_tokens, W] (host)."""
+            capture_latents: bool = True, sync_latents: bool = True) -> Tuple[torch.Tensor, List[Optional[torch.Tensor]]]:
+        """One ragged forward. Returns logits [n_seqs, V] and, per sequence, its latents [L, n_tokens, W] (host).
+        ``sync_latents=False``: the host does not wait for the latent copies (no per-forward synchronize, reference
+        engine_v2.py:131-189 keeps its host free the same way); call ``wait_latents()`` (or check
+        ``latents_ready()``) before reading them -- ``restore_kv`` / ``evict`` wait on their own."""
         batch_uids = list(batch_uids)
         batch_tokens = [t if isinstance(t, torch.Tensor) else torch.tensor(t) for t in batch_tokens]
         if do_checks:
@@ -135,7 +138,8 @@ class InferenceEngineV2:
         if self._model.decode_graph_eligible(batch, capture_latents):
             logits, latents = self._model.forward_decode_graph(batch), None  # HIP-graph decode step
         else:
-            logits, latents = self._model.forward(batch, capture_latents=capture_latents)
+            logits, latents = self._model.forward(batch, capture_latents=capture_latents, sync_latents=sync_latents)
+            self._latent_event = getattr(self._model, "latent_event", None)
         split = []
         for (q0, n, _) in batch.seq_meta_host:
             split.append(latents[:, q0:q0 + n] if latents is not None else None)
@@ -143,9 +147,21 @@ class InferenceEngineV2:
             sm.get_sequence(uid).post_forward()
         return logits, split
 
+    def latents_ready(self) -> bool:
+        ev = getattr(self, "_latent_event", None)
+        return ev is None or ev.query()
+
+    def wait_latents(self):
+        """Block until the latents returned by the last ``put(..., sync_latents=False)`` are on the host."""
+        ev = getattr(self, "_latent_event", None)
+        if ev is not None:
+            ev.synchronize()
+            self._latent_event = None
+
     def restore_kv(self, batch_uids: Iterable[int], batch_tokens: Iterable[torch.Tensor],
                    batch_latents: Iterable[Optional[torch.Tensor]]):
         """Rebuild the KV cache of previously-evicted sequences from their host latents (HCache)."""
+        self.wait_latents()
         sm, batch = self._state_manager, self._batch
         batch.clear()
         lat, restored = [], []
@@ -171,6 +187,7 @@ class InferenceEngineV2:
     def evict(self, uid):
         """Free a sequence's KV blocks but keep tracking it (its tokens/latents live on the host)."""
         seq = self._state_manager.get_sequence(uid)
+        self.wait_latents()
         if seq is not None:
             self._state_manager.free_kv(seq)
             seq.seen_tokens = 0

@@ -298,8 +298,10 @@ class RaggedTransformer:
         return g.out.clone()
 
     @torch.no_grad()
-    def forward(self, batch, capture_latents=True):
-        """Returns (logits [n_seqs, V], latents host [L, T, H] or [L, T, 2*n_kv*D] or None)."""
+    def forward(self, batch, capture_latents=True, sync_latents=True):
+        """Returns (logits [n_seqs, V], latents host [L, T, H] or [L, T, 2*n_kv*D] or None). With
+        ``sync_latents=False`` the host does not wait for the latent D2H copies: ``self.latent_event`` (HIP event on
+        the copy stream) marks when the returned host tensor is complete."""
         spec = self.spec
         self._prep(batch)
         T = batch.current_tokens
@@ -330,7 +332,8 @@ class RaggedTransformer:
                 h = self._allreduce(self._mlp(L, x2))
         logits = self.unembed_mod(h, residual, batch, self.lm_head, self.lm_head_b, self.final_w, self.final_b,
                                   spec.norm_eps, self.tp_group, self.vocab)
-        if events:
+        self.latent_event = events[-1] if events else None
+        if events and sync_latents:
             events[-1].synchronize()
         return logits, lat
 

@@ -30,7 +30,7 @@ def _devices():
     return devs
 
 
-def _run_consistency(device, dtype, latent_mode, tol):
+def _run_consistency(device, dtype, latent_mode, tol, sync_latents=True):
     m = _model(device, dtype)
     eng = build_engine_from_model(m, {"latent_mode": latent_mode, "dtype": {torch.float32: "fp32",
                                                                           torch.bfloat16: "bf16"}[dtype],
@@ -43,7 +43,7 @@ def _run_consistency(device, dtype, latent_mode, tol):
     full1 = _full_logits(m, torch.cat([p1, cont]).to(device))
     full2 = _full_logits(m, p2.to(device))
     # ragged prefill of two sequences
-    logits, lats = eng.put([1, 2], [p1, p2])
+    logits, lats = eng.put([1, 2], [p1, p2], sync_latents=sync_latents)  # async: evict / restore_kv wait
     assert logits.shape == (2, 211)
     assert torch.allclose(logits[0].float(), full1[69], atol=tol, rtol=tol)
     assert torch.allclose(logits[1].float(), full2[-1], atol=tol, rtol=tol)
@@ -68,14 +68,16 @@ def _run_consistency(device, dtype, latent_mode, tol):
 @pytest.mark.parametrize("latent_mode", ["hidden", "kv"])
 def test_hcache_consistency_cpu(latent_mode):
     _run_consistency("cpu", torch.float32, latent_mode, 2e-4)
+    _run_consistency("cpu", torch.float32, latent_mode, 2e-4, sync_latents=False)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sync_latents", [True, False])
 @pytest.mark.parametrize("latent_mode", ["hidden", "kv"])
-def test_hcache_consistency_gpu(latent_mode):
+def test_hcache_consistency_gpu(latent_mode, sync_latents):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_consistency("cuda", torch.bfloat16, latent_mode, 6e-2)
+    _run_consistency("cuda", torch.bfloat16, latent_mode, 6e-2, sync_latents)
 
 
 @pytest.mark.gpu
