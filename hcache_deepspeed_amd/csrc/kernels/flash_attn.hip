@@ -503,7 +503,7 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
-template <int D>
+template <int D, bool FASTDMA = true>
 __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   constexpr int NW = 8, BM = 32 * NW;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
@@ -558,7 +558,7 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
     dv[i] = (int32_t)(((int64_t)row * p.sv + 8 * ch) * 2);
   }
   auto stage = [&](char* dst, const bf16* base, int64_t stride, const int32_t* off, int kt) {
-    if (kt * BN + BN <= len) {
+    if (FASTDMA && kt * BN + BN <= len) {
       const char* tb = (const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -1393,7 +1393,7 @@ int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_b
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
 // 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 5) return hipErrorInvalidValue;
+  if (var < 0 || var > 6) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1429,6 +1429,7 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
         switch (g_fwd_var) {
           case 4: hipLaunchKernelGGL((attn_fwd_stg_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 5: hipLaunchKernelGGL((attn_fwd_sp_kernel<D>), grid, dim3(512), 0, st, p); break;
+          case 6: hipLaunchKernelGGL((attn_fwd_sp_kernel<D, false>), grid, dim3(512), 0, st, p); break;
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;
