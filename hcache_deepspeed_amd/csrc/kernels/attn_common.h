@@ -137,6 +137,26 @@ __device__ __forceinline__ void lds_wait() {
   __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs that consume the asm reads behind the wait (guide rule 18)
 }
 
+// lds_wait<N>() that also TIES the fragments the retired reads produced: they are in/out operands of the
+// s_waitcnt, so no use of them (an MFMA) can be placed above it. An inline-asm LDS read hands its destination
+// registers to the compiler as if the data were already there; the sched_barrier in lds_wait stops only the machine
+// scheduler, not IR-level motion of an MFMA (no memory effects) above an asm statement it has no data dependency on.
+template <int N>
+__device__ __forceinline__ void lds_wait_tie(bf16x8& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void lds_wait_tie(bf16x8& a, bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void lds_wait_tie(bf16x8& a, bf16x8& b, bf16x8& c, bf16x8& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // B-operand fragment for k-step (s & 1) of a 32-row accumulator tile: registers 8*(s&1) .. +7.
 template <int HALF>
 __device__ __forceinline__ bf16x8 acc_to_b(const f32x16& acc) {

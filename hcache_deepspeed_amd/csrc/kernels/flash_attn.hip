@@ -267,9 +267,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
           if (dt + 1 < DT) {
 #pragma unroll
             for (int st = 0; st < 4; ++st) vf[(dt + 1) & 1][st] = tr_d_asm(Vt, st, dt + 1);
-            lds_wait<8>();
+            lds_wait_tie<8>(vf[dt & 1][0], vf[dt & 1][1], vf[dt & 1][2], vf[dt & 1][3]);
           } else {
-            lds_wait<0>();
+            lds_wait_tie<0>(vf[dt & 1][0], vf[dt & 1][1], vf[dt & 1][2], vf[dt & 1][3]);
           }
 #pragma unroll
           for (int st = 0; st < 4; ++st) o[dt] = mfma(vf[dt & 1][st], pb[st], o[dt]);
@@ -439,9 +439,10 @@ __global__ __launch_bounds__(512) void attn_fwd_stg_kernel(AttnParams p) {
         if (dt + 1 < DT) {
 #pragma unroll
           for (int st = 0; st < 4; ++st) vf[(dt + 1) & 1][st] = read_tr_asm(Vt, st, dt + 1);
-          lds_wait<8>();  // block dt's 8 reads are done, block dt+1's may still fly
+          // block dt's 8 reads are done, block dt+1's may still fly
+          lds_wait_tie<8>(vf[dt & 1][0], vf[dt & 1][1], vf[dt & 1][2], vf[dt & 1][3]);
         } else {
-          lds_wait<0>();
+          lds_wait_tie<0>(vf[dt & 1][0], vf[dt & 1][1], vf[dt & 1][2], vf[dt & 1][3]);
         }
 #pragma unroll
         for (int st = 0; st < 4; ++st) o[dt] = mfma(vf[dt & 1][st], pb[st], o[dt]);
@@ -606,7 +607,11 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
       kr[0][ks] = lds_b128<0>(ak[ks]);
       kr[1][ks] = lds_b128<8192>(ak[ks]);
     });
-    lds_wait<0>();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      lds_wait_tie<0>(kr[t][0], kr[t][1], kr[t][2], kr[t][3]);
+      lds_wait_tie<0>(kr[t][4], kr[t][5], kr[t][6], kr[t][7]);
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       sc[t] = f32x16{};
@@ -668,9 +673,9 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
           constexpr int i = decltype(IC)::value;
           kr[(j + 1) & 1][i] = lds_b128<KN + 8192 * ((j + 1) >> 1)>(ak[4 * ((j + 1) & 1) + i]);
         });
-        lds_wait<4>();
+        lds_wait_tie<4>(kr[j & 1][0], kr[j & 1][1], kr[j & 1][2], kr[j & 1][3]);
       } else {
-        lds_wait<0>();
+        lds_wait_tie<0>(kr[j & 1][0], kr[j & 1][1], kr[j & 1][2], kr[j & 1][3]);
       }
       if constexpr ((j & 1) == 0) sn[t] = f32x16{};
 #pragma unroll
@@ -704,9 +709,9 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
           constexpr int dt = decltype(DC)::value;
           vf[(st + 1) & 1][dt] = lds_tr8<VT + 4096 * (st + 1)>(av0[dt], av1[dt]);
         });
-        lds_wait<8>();
+        lds_wait_tie<8>(vf[st & 1][0], vf[st & 1][1], vf[st & 1][2], vf[st & 1][3]);
       } else {
-        lds_wait<0>();
+        lds_wait_tie<0>(vf[st & 1][0], vf[st & 1][1], vf[st & 1][2], vf[st & 1][3]);
       }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(vf[st & 1][dt], pb[st], o[dt]);
@@ -1051,11 +1056,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
         for (int j = 0; j < 2 * KS; ++j) {
           if (j + 2 < 2 * KS) {
             ld(j + 2);
-            lds_wait<4>();
+            lds_wait_tie<4>(fa[j % 3], fb[j % 3]);
           } else if (j + 1 < 2 * KS) {
-            lds_wait<2>();
+            lds_wait_tie<2>(fa[j % 3], fb[j % 3]);
           } else {
-            lds_wait<0>();
+            lds_wait_tie<0>(fa[j % 3], fb[j % 3]);
           }
           if (j < KS)
             sacc = mfma(fa[j % 3], fb[j % 3], sacc);
@@ -1096,11 +1101,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
         for (int j = 0; j < 4 * DT; ++j) {
           if (j + 2 < 4 * DT) {
             ldt(j + 2);
-            lds_wait<4>();
+            lds_wait_tie<4>(ft[j % 3]);
           } else if (j + 1 < 4 * DT) {
-            lds_wait<2>();
+            lds_wait_tie<2>(ft[j % 3]);
           } else {
-            lds_wait<0>();
+            lds_wait_tie<0>(ft[j % 3]);
           }
           const int dt = j >> 2;
           switch (j & 3) {
@@ -1255,11 +1260,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
         for (int j = 0; j < 32; ++j) {
           if (j + 2 < 32) {
             ld(j + 2);
-            lds_wait<2>();
+            lds_wait_tie<2>(fa[j % 3]);
           } else if (j + 1 < 32) {
-            lds_wait<1>();
+            lds_wait_tie<1>(fa[j % 3]);
           } else {
-            lds_wait<0>();
+            lds_wait_tie<0>(fa[j % 3]);
           }
           const int t = j >> 4, which = (j >> 3) & 1, ks = j & 7;
           if (which)
@@ -1322,11 +1327,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
         for (int j = 0; j < 4 * DT; ++j) {
           if (j + 2 < 4 * DT) {
             ldt(j + 2);
-            lds_wait<4>();
+            lds_wait_tie<4>(ft[j % 3]);
           } else if (j + 1 < 4 * DT) {
-            lds_wait<2>();
+            lds_wait_tie<2>(ft[j % 3]);
           } else {
-            lds_wait<0>();
+            lds_wait_tie<0>(ft[j % 3]);
           }
           dq[j >> 2] = mfma(ft[j % 3], sb[j & 3], dq[j >> 2]);
         }

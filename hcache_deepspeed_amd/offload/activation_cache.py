@@ -26,6 +26,14 @@ allocation; from then on only the *earliest* layers 0..k-1 are spilled, with k t
 ``peak_all + resident_bytes(k..)`` under the budget (``plan_offload``). Early layers are spilled because their
 D2H has the whole remaining forward to drain and their H2D the whole remaining backward to prefetch. A runtime
 guard still spills any tensor that would push the allocation past the budget.
+
+Two corrections keep the budgeted cache off the critical path:
+* the calibration peak over-states the all-spilled peak (spilled tensors still waiting for their D2H hold HBM
+  inside the copy window), so after each planned step the forward/backward turn-around peak is compared with the
+  budget and the latest spilled layers whose bytes fit in the slack are kept resident from then on (closed loop);
+* in backward the spilled layers are prefetched as far ahead as the HBM the backward has already freed allows
+  (bounded by the budget), not only ``prefetch_layers`` ahead: the H2D of the spilled prefix then overlaps the
+  backward of the resident layers instead of bunching up at the end of the step.
 """
 import contextlib
 import os
@@ -101,6 +109,9 @@ class HostActivationCache:
         self.host_capped_bytes = 0
         self._capped_this_step = 0
         self._attached = []
+        self._cal_bytes = {}  # per-layer eligible bytes measured by the calibration step
+        self._turn_peak = None  # max allocation at the forward/backward turn-around of the last step
+        self.plan_adjustments = 0
 
     @classmethod
     def from_config(cls, cfg, device):
@@ -144,12 +155,21 @@ class HostActivationCache:
                 self.plan = calibrated_plan(self.layer_bytes, peak + self._capped_this_step, self._capped_this_step,
                                             self.budget)
                 self._calibrating = False
+                self._cal_bytes = dict(self.layer_bytes)
                 log_dist(f"host activation cache: spilling {len(self.plan)} of {self.n_layers} layers (peak when spilling all {peak / 2**30:.1f} GiB, budget "
                          f"{self.budget / 2**30:.1f} GiB, {self._capped_this_step / 2**30:.1f} GiB kept by the host cap)",
                          ranks=[0])
             elif self.plan is None:
                 self._calibrating = True
-                torch.cuda.reset_peak_memory_stats(self.device)
+            elif self._turn_peak is not None:
+                n0 = len(self.plan)
+                self.plan = refine_plan(self.plan, self._cal_bytes, self._turn_peak, self.budget)
+                if len(self.plan) != n0:
+                    self.plan_adjustments += 1
+                    log_dist(f"host activation cache: turn-around peak {self._turn_peak / 2**30:.1f} GiB of "
+                             f"{self.budget / 2**30:.1f} GiB -> spilling {len(self.plan)} layers", ranks=[0])
+            self._turn_peak = None
+            torch.cuda.reset_peak_memory_stats(self.device)
         self.cur_layer = -1
         for lst in self.by_layer.values():  # a forward whose backward never ran: return its host buffers
             for o in lst:
@@ -230,6 +250,8 @@ class HostActivationCache:
     _DEBUG = os.environ.get("HDS_ACT_CACHE_DEBUG") == "1"
 
     def _prefetch_before(self, layer):
+        if self._turn_peak is None and self.device.type == "cuda":
+            self._turn_peak = torch.cuda.max_memory_allocated(self.device)  # first unpack of the step
         for j in range(1, self.prefetch_layers + 1):
             lst = self.by_layer.get(layer - j, ())
             if self._DEBUG and lst and lst[0].dev is None:
@@ -238,6 +260,17 @@ class HostActivationCache:
                       file=sys.stderr, flush=True)
             for o in lst:
                 self._prefetch(o)
+        if self.budget is not None and self.device.type == "cuda":
+            # further ahead, while the HBM the backward has already freed covers the next spilled layer
+            for lj in sorted((k for k in self.by_layer if k < layer - self.prefetch_layers), reverse=True):
+                need = sum(o.host.numel() * o.host.element_size() for o in self.by_layer[lj]
+                           if o.dev is None and o.host is not None)
+                if need == 0:
+                    continue
+                if torch.cuda.memory_allocated(self.device) + need > self.budget:
+                    break
+                for o in self.by_layer[lj]:
+                    self._prefetch(o)
 
     def _unpack(self, s):
         if isinstance(s, _Tagged):
@@ -265,6 +298,23 @@ class HostActivationCache:
                 "spilled_layers": None if self.plan is None else len(self.plan), "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits}
+
+
+def refine_plan(plan, layer_bytes, turn_peak, budget, margin=1 << 30):
+    """Closed-loop correction of a spill plan (a prefix {0..k-1}) from the turn-around peak of a step that ran it:
+    the latest spilled layers whose bytes fit in ``budget - margin - turn_peak`` stay resident from now on; a peak
+    over the budget spills the next layer as well."""
+    spilled = sorted(plan)
+    slack = budget - margin - turn_peak
+    if slack < 0:
+        nxt = (spilled[-1] + 1) if spilled else min(layer_bytes, default=None)
+        if nxt is not None and nxt in layer_bytes:
+            return set(spilled) | {nxt}
+        return set(spilled)
+    while spilled and layer_bytes.get(spilled[-1], 0) <= slack:
+        slack -= layer_bytes.get(spilled[-1], 0)
+        spilled.pop()
+    return set(spilled)
 
 
 def calibrated_plan(layer_bytes, measured_peak, host_capped_bytes, budget):

@@ -211,3 +211,16 @@ def test_pipelined_swapper_overlap_order(tmp_path):
     m = sw.read_full("m")
     for i, (lo, hi) in enumerate(bounds):
         assert torch.all(m[lo:hi] == i)
+
+
+def test_refine_plan_closed_loop():
+    """The turn-around peak of a planned step corrects the plan: slack keeps the latest spilled layers resident,
+    an over-budget peak spills the next layer too."""
+    from hcache_deepspeed_amd.offload.activation_cache import refine_plan
+    lb = {i: 10 for i in range(8)}
+    G = 1 << 30
+    assert refine_plan({0, 1, 2, 3, 4}, lb, turn_peak=100, budget=125 + G) == {0, 1, 2}  # 25 B slack: 2 layers
+    assert refine_plan({0, 1, 2}, lb, turn_peak=100, budget=105 + G) == {0, 1, 2}        # 5 B: nothing fits
+    assert refine_plan({0, 1, 2}, lb, turn_peak=100, budget=95 + G) == {0, 1, 2, 3}      # over budget
+    assert refine_plan(set(), lb, turn_peak=100, budget=95 + G) == {0}
+    assert refine_plan({0, 1}, lb, turn_peak=0, budget=1000 + G) == set()
