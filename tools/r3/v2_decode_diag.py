@@ -19,8 +19,11 @@ def main():
     with torch.device(dev):
         model = LlamaForCausalLM(llama3_8b()).to(torch.bfloat16).eval()
     P, steps = 512, 24  # +3 untimed graph-capture steps per case
-    for B in (1, 8):
-        for mode in ("graph", "eager"):
+    cases = [(1, "graph"), (1, "eager"), (8, "graph"), (8, "eager")]
+    if len(sys.argv) > 1:  # e.g. "1:graph,8:graph"
+        cases = [(int(c.split(":")[0]), c.split(":")[1]) for c in sys.argv[1].split(",")]
+    for B, mode in cases:
+        if True:
             econf = {"dtype": "bf16", "state_manager": {"max_ragged_batch_size": B * P, "max_context": P + steps + 128,
                                                          "kv_block_size": 64, "max_tracked_sequences": 4 * B}}
             eng = build_engine_from_model(model, econf, device=dev, num_kv_blocks=B * ((P + steps + 127) // 64) + 16)
