@@ -104,6 +104,20 @@ __device__ __forceinline__ void lpt_ids(int& blk, int& head, int& b) {
   b = rem / heads;
 }
 
+// The per-element mask as an interval test (two compares, no branches): the keys a query may see, or the queries
+// that may see a key, form [lo, hi] (empty when lo > hi). Same predicate as masked() below.
+__device__ __forceinline__ void key_span(const AttnParams& p, int qi, int len, int& lo, int& hi) {
+  lo = p.window > 0 ? max(0, qi - p.window + 1) : 0;
+  hi = p.causal ? min(qi, len - 1) : len - 1;
+  if (qi >= len) lo = 1, hi = 0;
+}
+__device__ __forceinline__ void query_span(const AttnParams& p, int kj, int len, int& lo, int& hi) {
+  lo = p.causal ? kj : 0;
+  hi = p.window > 0 ? min(len - 1, kj + p.window - 1) : len - 1;
+  if (kj >= len) lo = 1, hi = 0;
+}
+__device__ __forceinline__ bool outside(int i, int lo, int hi) { return i < lo || i > hi; }
+
 __device__ __forceinline__ bool masked(const AttnParams& p, int qi, int kj, int len) {
   if (kj >= len || qi >= len) return true;
   if (p.causal && kj > qi) return true;
@@ -136,6 +150,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   const int q0 = qb * BM;
   const int myq = q0 + 32 * w + (lane & 31);
   const float c = p.scale * kLog2e;
+  int klo, khi;
+  key_span(p, myq, len, klo, khi);
 
   // Q fragments (B operand of S^T = K.Q^T): Q[myq][16ks + 8h .. +7]
   bf16x8 qf[KS];
@@ -218,7 +234,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         if (need_mask) {
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) s[t][r] = -INFINITY;
+            if (outside(k0 + 32 * t + acc_row(r, h), klo, khi)) s[t][r] = -INFINITY;
         }
 #pragma unroll
         for (int r = 0; r < 16; r += 2) tmax = max3_raw(tmax, s[t][r], s[t][r + 1]);
@@ -327,6 +343,8 @@ __global__ __launch_bounds__(512) void attn_fwd_stg_kernel(AttnParams p) {
   const int q0 = qb * BM;
   const int myq = q0 + 32 * w + (lane & 31);
   const float c = p.scale * kLog2e;
+  int klo, khi;
+  key_span(p, myq, len, klo, khi);
 
   bf16x8 qf[KS];
   {
@@ -397,7 +415,7 @@ __global__ __launch_bounds__(512) void attn_fwd_stg_kernel(AttnParams p) {
         if (need_mask) {
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) s[t][r] = -INFINITY;
+            if (outside(k0 + 32 * t + acc_row(r, h), klo, khi)) s[t][r] = -INFINITY;
         }
 #pragma unroll
         for (int r = 0; r < 16; r += 2) tmax = max3_raw(tmax, s[t][r], s[t][r + 1]);
@@ -523,6 +541,8 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   const int q0 = qb * BM;
   const int myq = q0 + 32 * w + (lane & 31);
   const float c = p.scale * kLog2e;
+  int klo, khi;
+  key_span(p, myq, len, klo, khi);
   if (w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half (guide T5)
 
   bf16x8 qf[KS];
@@ -637,7 +657,7 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (masked(p, myq, k0 + 32 * t + acc_row(r, h), len)) sc[t][r] = -INFINITY;
+          if (outside(k0 + 32 * t + acc_row(r, h), klo, khi)) sc[t][r] = -INFINITY;
     }
     float tm0 = -INFINITY, tm1 = -INFINITY;  // two independent max chains
 #pragma unroll
@@ -808,6 +828,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int kw0 = kb * BK + 32 * w;      // this wave's first key
   const int myk = kw0 + (lane & 31);
+  int qlo, qhi;
+  query_span(p, myk, len, qlo, qhi);
   const float c = p.scale * kLog2e;
 
   // K and V fragments (B operands): K[myk][16ks + 8h ..]
@@ -898,7 +920,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
           const int qr = 32 * sub + acc_row(r, h);
           const int qi = qbase + qr;
           float pr = fast_exp2(sacc[r] * c - Lt[qr] * kLog2e);
-          if (masked(p, qi, myk, len)) pr = 0.f;
+          if (outside(qi, qlo, qhi)) pr = 0.f;
           sacc[r] = pr;
           dpacc[r] = pr * (dpacc[r] - Dt[qr]);
         }
@@ -963,6 +985,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
   const int kg = w & 3, qh = w >> 2;
   const int kw0 = kb * BK + 32 * kg;  // this wave's first key
   const int myk = kw0 + (lane & 31);
+  int qlo, qhi;
+  query_span(p, myk, len, qlo, qhi);
   const float c = p.scale * kLog2e;
   const char* Kw = Kt + (kg >> 1) * 16384;
   const char* Vw = Vt + (kg >> 1) * 16384;
@@ -1084,7 +1108,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
           float x = sacc[r] * c - l4[j] * kLog2e;
           if constexpr (EVO) x += evo_bias(p, b, hk, qt * BN + qr0 + j, myk) * kLog2e;
           float pr = fast_exp2(x);
-          if ((EVO || need_mask) && masked(p, qt * BN + qr0 + j, myk, len)) pr = 0.f;
+          if constexpr (EVO) {
+            if (masked(p, qt * BN + qr0 + j, myk, len)) pr = 0.f;
+          } else {
+            if (need_mask && outside(qt * BN + qr0 + j, qlo, qhi)) pr = 0.f;
+          }
           sacc[r] = pr;
           dpacc[r] = pr * (dpacc[r] - d4[j]);
         }
@@ -1179,6 +1207,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   const int q0 = qb * BM;
   const int myq = q0 + 32 * w + (lane & 31);
   const float c = p.scale * kLog2e;
+  int klo, khi;
+  key_span(p, myq, len, klo, khi);
   const int qr = myq < len ? myq : len - 1;
 
   bf16x8 qf[KS], df[KS];
@@ -1294,7 +1324,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
           float x = s[t][r] * c - lse2;
           if constexpr (EVO) x += evo_bias(p, b, hq, myq, key) * kLog2e;
           float pr = fast_exp2(x);
-          const bool off = masked(p, myq, key, len);
+          const bool off = EVO ? masked(p, myq, key, len) : outside(key, klo, khi);
           if ((EVO || need_mask) && off) pr = 0.f;
           s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
           if constexpr (EVO) {
