@@ -250,6 +250,164 @@ __global__ __launch_bounds__(64 * NW) void paged_attn_kernel(PagedParams p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// decode-only batches: split-K ("flash decoding") over the paged cache
+// ------------------------------------------------------------------------------------------
+// One new token per sequence: the atom kernel above would run one 4-wave workgroup per (sequence, kv head) --
+// 8 workgroups for a single Llama-3-8B sequence, each walking the whole context on a mostly empty 128-row MFMA tile
+// (35 us per layer at 540 keys, profiles/r3). Decode is a K/V stream, so this kernel is built like decode_attn.hip:
+// grid (splits, Hkv, n_seqs), a workgroup serves all G query heads of its kv head from ONE read of its key range,
+// 16-B loads with LPK = D / 8 lanes per key, online softmax in registers, lane groups and waves merged by
+// max / rescale, splits merged by a combine kernel through fp32 partials. The key range comes from the device-side
+// sequence metadata (seen + 1 keys), so one launch shape serves every step of a HIP-graph decode.
+constexpr int kDecGMax = 8;
+
+struct PagedDecodeParams {
+  const bf16* q;  // [T, Hq, D] rows with token stride sq
+  int64_t sq;
+  const bf16* cache;  // [num_blocks, block_size, 2, Hkv, D]
+  bf16* o;            // [T, Hq, D]
+  float* part_o;      // [n_seqs, Hq, splits, D]
+  float* part_ml;     // [n_seqs, Hq, splits, 2]
+  const int* seq_meta;  // [n_seqs][3] = {q_start, n_new (1), seen}
+  const int* block_tables;
+  int max_blocks, block_size, hq, hkv, splits;
+  float scale;
+  int window;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void paged_decode_kernel(PagedDecodeParams p) {
+  constexpr int LPK = D / 8, KPW = 64 / LPK;
+  __shared__ float red[4][kDecGMax][2 + D];
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int G = p.hq / p.hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kl = lane / LPK, c = lane % LPK;
+  const int q_start = p.seq_meta[3 * b], ctx = p.seq_meta[3 * b + 2] + 1;
+  const int jb = p.window > 0 ? max(0, ctx - p.window) : 0;
+  const int kps = (ctx + p.splits - 1) / p.splits;
+  const int j0 = split * kps, j1 = min(ctx, j0 + kps);
+  const int* table = p.block_tables + (int64_t)b * p.max_blocks;
+  const int64_t kv_row = 2LL * p.hkv * D;
+
+  float qv[kDecGMax][8];
+#pragma unroll
+  for (int g = 0; g < kDecGMax; ++g) {
+    if (g < G) {
+      Vec8<bf16>::load(p.q + (int64_t)q_start * p.sq + (int64_t)(hk * G + g) * D + c * 8, qv[g]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qv[g][e] *= p.scale;
+    }
+  }
+  float m[kDecGMax], l[kDecGMax], acc[kDecGMax][8];
+#pragma unroll
+  for (int g = 0; g < kDecGMax; ++g) {
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[g][e] = 0.f;
+  }
+  for (int j = j0 + w * KPW + kl; j - kl < j1; j += 4 * KPW) {
+    const bool ok = j < j1 && j >= jb;
+    float kv[8] = {}, vv[8] = {};
+    if (ok) {
+      const int blk = table[j / p.block_size];
+      const bf16* kb = p.cache + ((int64_t)blk * p.block_size + j % p.block_size) * kv_row + (int64_t)hk * D + c * 8;
+      Vec8<bf16>::load(kb, kv);
+      Vec8<bf16>::load(kb + (int64_t)p.hkv * D, vv);
+    }
+#pragma unroll
+    for (int g = 0; g < kDecGMax; ++g) {
+      if (g >= G) break;
+      float sc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sc += qv[g][e] * kv[e];
+#pragma unroll
+      for (int off = LPK / 2; off >= 1; off >>= 1) sc += __shfl_xor(sc, off, 64);
+      sc = ok ? sc : -INFINITY;
+      const float mn = fmaxf(m[g], sc);
+      const bool none = mn == -INFINITY;
+      const float a = none ? 1.f : __expf(m[g] - mn), e_s = none ? 0.f : __expf(sc - mn);
+      l[g] = l[g] * a + e_s;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[g][e] = acc[g][e] * a + e_s * vv[e];
+      m[g] = mn;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < kDecGMax; ++g) {
+    if (g >= G) break;
+#pragma unroll
+    for (int off = LPK; off < 64; off <<= 1) {
+      const float mo = __shfl_xor(m[g], off, 64), lo = __shfl_xor(l[g], off, 64);
+      const float mn = fmaxf(m[g], mo);
+      const float a = mn == -INFINITY ? 0.f : __expf(m[g] - mn), ao = mn == -INFINITY ? 0.f : __expf(mo - mn);
+      l[g] = l[g] * a + lo * ao;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[g][e] = acc[g][e] * a + __shfl_xor(acc[g][e], off, 64) * ao;
+      m[g] = mn;
+    }
+  }
+  if (kl == 0) {
+#pragma unroll
+    for (int g = 0; g < kDecGMax; ++g) {
+      if (g >= G) break;
+      if (c == 0) {
+        red[w][g][0] = m[g];
+        red[w][g][1] = l[g];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[w][g][2 + c * 8 + e] = acc[g][e];
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < G * LPK; t += 256) {
+    const int g = t / LPK, cc = t % LPK;
+    float mm = -INFINITY;
+    for (int ww = 0; ww < 4; ++ww) mm = fmaxf(mm, red[ww][g][0]);
+    float ll = 0.f, oo[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ww = 0; ww < 4; ++ww) {
+      const float a = mm == -INFINITY ? 0.f : __expf(red[ww][g][0] - mm);
+      ll += red[ww][g][1] * a;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) oo[e] += red[ww][g][2 + cc * 8 + e] * a;
+    }
+    const int h = hk * G + g;
+    if (p.splits == 1) {
+      const float inv = ll > 0.f ? 1.f / ll : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) oo[e] *= inv;
+      Vec8<bf16>::store(p.o + ((int64_t)q_start * p.hq + h) * D + cc * 8, oo);
+    } else {
+      float* po = p.part_o + (((int64_t)b * p.hq + h) * p.splits + split) * D + cc * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) po[e] = oo[e];
+      if (cc == 0) {
+        float* pm = p.part_ml + (((int64_t)b * p.hq + h) * p.splits + split) * 2;
+        pm[0] = mm;
+        pm[1] = ll;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void paged_decode_combine_kernel(PagedDecodeParams p) {
+  const int bh = blockIdx.x, b = bh / p.hq, h = bh % p.hq;
+  const float* pm = p.part_ml + (int64_t)bh * p.splits * 2;
+  float mm = -INFINITY;
+  for (int s = 0; s < p.splits; ++s) mm = fmaxf(mm, pm[2 * s]);
+  const int d = threadIdx.x;
+  float ll = 0.f, oo = 0.f;
+  for (int s = 0; s < p.splits; ++s) {
+    const float a = mm == -INFINITY ? 0.f : __expf(pm[2 * s] - mm);
+    ll += pm[2 * s + 1] * a;
+    oo += p.part_o[((int64_t)bh * p.splits + s) * D + d] * a;
+  }
+  p.o[((int64_t)p.seq_meta[3 * b] * p.hq + h) * D + d] = (bf16)(ll > 0.f ? oo / ll : 0.f);
+}
+
 }  // namespace
 
 #define HDS_PAGED_DIMS(X) X(32) X(48) X(64) X(80) X(96) X(112) X(128) X(160) X(192) X(256)
@@ -296,3 +454,42 @@ HDS_EXPORT int hds_paged_attn(const void* q, int64_t sq, const void* cache, void
 }
 
 HDS_EXPORT int hds_paged_rows_per_atom() { return 128; }
+
+// decode-only batches (every sequence has exactly one new token)
+HDS_EXPORT int hds_paged_decode_supported(int head_dim, int G) {
+  return (head_dim == 64 || head_dim == 128 || head_dim == 256) && G >= 1 && G <= kDecGMax;
+}
+
+// key splits for n_seqs sequences of at most max_ctx keys: >= 2 workgroups per CU overall, >= 32 keys per split
+HDS_EXPORT int hds_paged_decode_splits(int n_seqs, int hkv, int max_ctx) {
+  const int groups = n_seqs * hkv;
+  int splits = (512 + groups - 1) / groups;
+  const int by_len = (max_ctx + 31) / 32;
+  splits = splits < by_len ? splits : by_len;
+  return splits < 1 ? 1 : (splits > 64 ? 64 : splits);
+}
+
+HDS_EXPORT int hds_paged_decode(const void* q, int64_t sq, const void* cache, void* o, float* part_o, float* part_ml,
+                                const int* seq_meta, const int* block_tables, int max_blocks, int block_size,
+                                int n_seqs, int hq, int hkv, int head_dim, int splits, float scale, int window,
+                                hipStream_t st) {
+  if (n_seqs <= 0) return 0;
+  if (hq % hkv || !hds_paged_decode_supported(head_dim, hq / hkv) || splits < 1 ||
+      (splits > 1 && (!part_o || !part_ml)))
+    return hipErrorInvalidValue;
+  PagedDecodeParams p{(const bf16*)q, sq, (const bf16*)cache, (bf16*)o, part_o, part_ml, seq_meta, block_tables,
+                      max_blocks, block_size, hq, hkv, splits, scale, window};
+  const dim3 grid(splits, hkv, n_seqs);
+  switch (head_dim) {
+#define HDS_DEC(d)                                                                                            \
+  case d:                                                                                                     \
+    hipLaunchKernelGGL(paged_decode_kernel<d>, grid, dim3(256), 0, st, p);                                    \
+    if (splits > 1) hipLaunchKernelGGL(paged_decode_combine_kernel<d>, dim3(n_seqs * hq), dim3(d), 0, st, p); \
+    break;
+    HDS_DEC(64)
+    HDS_DEC(128)
+    HDS_DEC(256)
+#undef HDS_DEC
+  }
+  return hipGetLastError();
+}

@@ -58,7 +58,8 @@ class DSDenseBlockedAttention(DSSelfAttentionBase):
         kv_rope_scatter(qkv, cache, batch.tok_seq, batch.tok_pos, batch.block_tables, cos, sin, nq, nkv,
                         do_rope=c.positional_embedding_type != "none" and cos is not None, rotary_dim=c.rotary_dim)
         o = paged_attention(qkv[:, :nq], cache, batch.atoms, batch.n_atoms, batch.seq_meta, batch.block_tables, nq,
-                            nkv, c.scale_factor, c.sliding_window, batch.seq_meta_host, batch.tables_host)
+                            nkv, c.scale_factor, c.sliding_window, batch.seq_meta_host, batch.tables_host,
+                            decode=T == batch.current_sequences)
         return o.reshape(T, nq * D)
 
 

@@ -88,6 +88,9 @@ _KERNEL_SIGS = {
     "hds_grouped_gemm": "ppppp" + "iiiiii" + "s",
     "hds_evoformer_fwd": "ppppp" + "i" + "pp" + "iiiii" + "f" + "s",
     "hds_nhwc_bias_add": "i" + "ppppp" + "l" + "ii" + "s",
+    "hds_paged_decode_supported": "ii",
+    "hds_paged_decode_splits": "iii",
+    "hds_paged_decode": "p" + "l" + "pppp" + "pp" + "iiiiiiii" + "f" + "i" + "s",
     "hds_symm_header_bytes": "",
     "hds_symm_alloc": "lpp",
     "hds_symm_open": "pp",
@@ -143,6 +146,8 @@ def load_kernels(build_if_missing=True):
         _bind(lib, _KERNEL_SIGS)
         # FlashAttention backward with LDS reads pipelined two MFMAs ahead (csrc/kernels/flash_attn.hip PIPE)
         lib.hds_attn_bwd_pipe(int(os.environ.get("HDS_ATTN_BWD_PIPE", "1")))
+        # FlashAttention forward variant (csrc/kernels/flash_attn.hip hds_attn_fwd_variant; 5 = software-pipelined)
+        lib.hds_attn_fwd_variant(int(os.environ.get("HDS_ATTN_FWD_VAR", "2")))
         _klib = lib
         return _klib
 

@@ -76,18 +76,34 @@ def build_atoms(seq_meta_host, n_q, n_kv):
 
 
 def paged_attention(q, cache, atoms, n_atoms, seq_meta, block_tables, n_q, n_kv, scale, window=0,
-                    seq_meta_host=None, block_tables_host=None):
-    """q: [T, n_q, D] (token-strided view ok). Returns o [T, n_q, D]."""
+                    seq_meta_host=None, block_tables_host=None, decode=False):
+    """q: [T, n_q, D] (token-strided view ok). Returns o [T, n_q, D]. ``decode``: every sequence of the batch has
+    exactly one new token (T == n_seqs) -- the split-K paged decode kernel runs instead of the atom kernel; its key
+    splits are sized from the cache capacity (block table width x block size), so one launch shape serves every
+    step of a HIP-graph decode."""
     T, _, D = q.shape
     o = torch.empty(T, n_q, D, device=q.device, dtype=q.dtype)
     if native.use_native(q):
         if not kernel_head_dim_ok(D) or q.dtype != torch.bfloat16:
             raise NotImplementedError(f"paged_attention: head_dim {D} / {q.dtype} has no HIP kernel")
+        lib = native.kernels()
+        if decode and lib.hds_paged_decode_supported(D, n_q // n_kv):
+            n_seqs = T
+            splits = lib.hds_paged_decode_splits(n_seqs, n_kv, block_tables.shape[1] * cache.shape[1])
+            part_o = part_ml = None
+            if splits > 1:
+                part_o = torch.empty(n_seqs * n_q * splits * D, device=q.device, dtype=torch.float32)
+                part_ml = torch.empty(n_seqs * n_q * splits * 2, device=q.device, dtype=torch.float32)
+            native.check(
+                lib.hds_paged_decode(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(), native.ptr(part_o),
+                                     native.ptr(part_ml), seq_meta.data_ptr(), block_tables.data_ptr(),
+                                     block_tables.shape[1], cache.shape[1], n_seqs, n_q, n_kv, D, splits, float(scale),
+                                     int(window), native.stream()), "paged_decode")
+            return o
         native.check(
-            native.kernels().hds_paged_attn(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(),
-                                            atoms.data_ptr(), n_atoms, seq_meta.data_ptr(), block_tables.data_ptr(),
-                                            block_tables.shape[1], cache.shape[1], n_q, n_kv, D, float(scale),
-                                            int(window), native.stream()), "paged_attn")
+            lib.hds_paged_attn(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(), atoms.data_ptr(), n_atoms,
+                               seq_meta.data_ptr(), block_tables.data_ptr(), block_tables.shape[1], cache.shape[1],
+                               n_q, n_kv, D, float(scale), int(window), native.stream()), "paged_attn")
         return o
     meta = seq_meta_host if seq_meta_host is not None else seq_meta.tolist()
     tables = block_tables_host if block_tables_host is not None else block_tables

@@ -401,6 +401,28 @@ def test_paged_attention_matches_reference(lens, seen, D):
     assert _rel(o.cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("D,G", [(128, 4), (64, 8), (256, 2), (128, 1)])
+@pytest.mark.parametrize("seen,window", [([100, 5, 700, 0], 0), ([1000, 33, 64, 63], 0), ([300, 2000, 7, 90], 50)])
+def test_paged_decode_matches_reference(seen, window, D, G):
+    """Split-K paged decode (one new token per sequence) against the torch reference over the same block tables,
+    incl. sliding window, a first-token sequence (seen 0) and splits that get no keys."""
+    from hcache_deepspeed_amd.ops.paged import build_atoms, paged_attention
+    Hkv = 2
+    Hq = Hkv * G
+    lens = [1] * len(seen)
+    cache, tab, metas, T, _ = _paged_setup(lens, seen, D=D)
+    q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16)
+    atoms, n = build_atoms(metas, Hq, Hkv)
+    meta = torch.tensor(metas, dtype=torch.int32)
+    o = paged_attention(q, cache, atoms.cuda(), n, meta.cuda(), tab.cuda(), Hq, Hkv, 1 / math.sqrt(D), window,
+                        decode=True)
+    o_atom = paged_attention(q, cache, atoms.cuda(), n, meta.cuda(), tab.cuda(), Hq, Hkv, 1 / math.sqrt(D), window)
+    ref = paged_attention(q.cpu().float(), cache.cpu().float(), atoms, n, meta, tab, Hq, Hkv, 1 / math.sqrt(D), window,
+                          seq_meta_host=metas, block_tables_host=tab)
+    assert _rel(o.cpu(), ref) < 1e-2
+    assert _rel(o.cpu(), o_atom.cpu()) < 1e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_moe_dispatch_combine_fwd_bwd(dtype):
     from hcache_deepspeed_amd.ops import moe as M
