@@ -90,7 +90,7 @@ _KERNEL_SIGS = {
     "hds_nhwc_bias_add": "i" + "ppppp" + "l" + "ii" + "s",
     "hds_paged_decode_supported": "ii",
     "hds_paged_decode_splits": "iii",
-    "hds_paged_decode": "p" + "l" + "pppp" + "pp" + "iiiiiiii" + "f" + "i" + "s",
+    "hds_paged_decode": "p" + "l" + "pppp" + "pp" + "iiiiiii" + "f" + "i" + "s",
     "hds_symm_header_bytes": "",
     "hds_symm_alloc": "lpp",
     "hds_symm_open": "pp",

@@ -1,0 +1,53 @@
+"""The ctypes signatures in ops/native.py against the HDS_EXPORT definitions in csrc/kernels/*.hip: same
+argument count and compatible kinds (pointer / 32-bit int / 64-bit int / float / stream), so a signature typo fails
+here instead of as a TypeError (or a silently mis-passed argument) on the GPU."""
+import glob
+import os
+import re
+
+from hcache_deepspeed_amd.ops import native
+
+KDIR = os.path.join(os.path.dirname(native.__file__), "..", "csrc", "kernels")
+
+
+def _exports():
+    out = {}
+    for path in glob.glob(os.path.join(KDIR, "*.hip")):
+        src = open(path).read()
+        for m in re.finditer(r"HDS_EXPORT\s+[\w\s\*]+?\b(hds_\w+)\s*\(([^)]*)\)", src):
+            out[m.group(1)] = [a.strip() for a in m.group(2).replace("\n", " ").split(",") if a.strip()]
+    return out
+
+
+def _kind(decl):
+    d = re.sub(r"\s+", " ", decl)
+    if "*" in d or d.startswith("hipStream_t"):
+        return "ps"
+    if re.match(r"(const )?(int64_t|long|size_t)\b", d):
+        return "l"
+    if re.match(r"(const )?float\b", d):
+        return "f"
+    if re.match(r"(const )?(uint32_t|unsigned)\b", d):
+        return "u"
+    if re.match(r"(const )?(int|bool)\b", d):
+        return "i"
+    return "?"
+
+
+def test_kernel_signatures_match_exports():
+    ex = _exports()
+    bad = []
+    for name, spec in native._KERNEL_SIGS.items():
+        if name not in ex:
+            bad.append(f"{name}: no HDS_EXPORT definition")
+            continue
+        args = ex[name]
+        if len(args) != len(spec):
+            bad.append(f"{name}: {len(spec)} ctypes args vs {len(args)} in the source")
+            continue
+        for i, (c, a) in enumerate(zip(spec, args)):
+            k = _kind(a)
+            ok = (c in "ps" and k == "ps") or (c == k) or (c == "i" and k == "u")
+            if not ok:
+                bad.append(f"{name} arg {i}: '{c}' vs `{a}`")
+    assert not bad, "\n".join(bad)
