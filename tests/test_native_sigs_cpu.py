@@ -51,3 +51,18 @@ def test_kernel_signatures_match_exports():
             if not ok:
                 bad.append(f"{name} arg {i}: '{c}' vs `{a}`")
     assert not bad, "\n".join(bad)
+
+
+def test_host_signatures_match_exports():
+    from hcache_deepspeed_amd.ops import host_sigs
+    hdir = os.path.join(os.path.dirname(native.__file__), "..", "csrc", "host")
+    ex = {}
+    for path in glob.glob(os.path.join(hdir, "*.cpp")):
+        src = open(path).read()
+        for m in re.finditer(r"(?:HDS_EXPORT|HDS_HOST_EXPORT|extern \"C\")\s+[\w\s\*]+?\b(hds_\w+)\s*\(([^)]*)\)", src):
+            ex[m.group(1)] = [a.strip() for a in m.group(2).replace("\n", " ").split(",")
+                              if a.strip() and a.strip() != "void"]
+    bad = [f"{n}: {len(a)} ctypes args vs {len(ex[n])} in the source" for n, (_, a) in host_sigs.SIGS.items()
+           if n in ex and len(a) != len(ex[n])]
+    missing = [n for n in host_sigs.SIGS if n not in ex]
+    assert not bad and not missing, (bad, missing)
