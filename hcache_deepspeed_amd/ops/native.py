@@ -147,7 +147,7 @@ def load_kernels(build_if_missing=True):
         # FlashAttention backward with LDS reads pipelined two MFMAs ahead (csrc/kernels/flash_attn.hip PIPE)
         lib.hds_attn_bwd_pipe(int(os.environ.get("HDS_ATTN_BWD_PIPE", "1")))
         # FlashAttention forward variant (csrc/kernels/flash_attn.hip hds_attn_fwd_variant; 5 = software-pipelined)
-        lib.hds_attn_fwd_variant(int(os.environ.get("HDS_ATTN_FWD_VAR", "2")))
+        lib.hds_attn_fwd_variant(int(os.environ.get("HDS_ATTN_FWD_VAR", "5")))
         _klib = lib
         return _klib
 
