@@ -63,6 +63,10 @@ def main():
     ap.add_argument("--offload-params-compile", type=float, default=None, metavar="BUDGET_GIB",
                     help="DeepCompile offload_parameters on the GPU-optimizer engine; the pass keeps shards on the "
                          "device within BUDGET_GIB of HBM (0: every shard on the host)")
+    ap.add_argument("--reuse-distance", default="auto",
+                    help="ZeRO-3 stage3_max_reuse_distance in elements; 'auto' = every parameter at N > 1 (units stay "
+                         "gathered from their forward to their backward: one all-gather per unit per step instead of "
+                         "two; HBM allows it at every dp for Llama-3-8B), 0 = release after the forward")
     ap.add_argument("--deepcompile", action="store_true",
                     help="engine.compile() with DeepCompile: profiled ZeRO-3 gather schedule (selective gather + prefetch)")
     args = ap.parse_args()
@@ -127,6 +131,14 @@ def main():
                                                                         "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }
+    if args.zero == 3:
+        rd = args.reuse_distance
+        if rd == "auto":
+            npar = (cfg_model.num_params() if hasattr(cfg_model, "num_params") else
+                    cfg_model.active_params() if hasattr(cfg_model, "active_params") else 0)
+            rd = int(4 * npar) if world > 1 else 0
+        if int(rd) > 0:
+            ds_config["zero_optimization"]["stage3_max_reuse_distance"] = int(rd)
     dc_on = args.deepcompile or args.offload_opt_states or args.offload_params_compile is not None
     if dc_on:
         ds_config["compile"] = {"deepcompile": bool(args.deepcompile or args.offload_params_compile is not None),
@@ -245,6 +257,7 @@ def main():
                        "host_act_cache": bool(args.host_act_cache), "offload": args.offload,
                        "global_batch": world * mb * args.gas, "seq_len": S,
                        "parallelism": f"zero{args.zero}-dp{world}", "micro_batch_per_gpu": mb, "gas": args.gas,
+                       "stage3_max_reuse_distance": ds_config["zero_optimization"].get("stage3_max_reuse_distance"),
                        "activation_checkpointing": bool(args.ckpt), "deepcompile": bool(args.deepcompile)},
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
                       "final_loss": round(float(loss.item()), 4), "peak_mem_gib": round(mem, 1),
