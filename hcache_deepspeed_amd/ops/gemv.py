@@ -6,15 +6,19 @@ import torch.nn.functional as F
 
 from . import native
 
-# Weight sizes (elements) that take the GEMV, from profiles/gemv_bench_r2.jsonl: at M = 1 the GEMV streams
-# 3.6-6.6 TB/s and beats hipBLASLt up to the 59M-element down projection (qkv 3.5x, o 2.1x, down 1.1x; gate_up 0.96x);
-# its dot products make it VALU-bound as M grows (M = 4: qkv 1.4x, down 0.73x; M = 8: o 1.36x, qkv 0.98x), so the
-# limit halves at M > 1 and again at M > 4.
-MAX_GEMV_NUMEL = int(__import__("os").environ.get("HDS_GEMV_MAX_NUMEL", str(64 * 1024 * 1024)))
+# Weight sizes (elements) that take the GEMV. At M = 1 every size does: in a real decode step (weights streamed from
+# HBM, not re-read from the 256 MB MALL as in a micro-benchmark loop) the GEMV beats hipBLASLt's small-M GEMM on the
+# gate_up projection and the LM head as well -- Llama-3-8B v2 decode 234.8 vs 211.0 tok/s at B = 1, same box
+# (profiles/r3/v2_decode_gemv_rule_r3.jsonl). Its dot products make it VALU-bound as M grows (M = 4: qkv 1.4x,
+# down 0.73x; M = 8: o 1.36x, qkv 0.98x, gate_up a loss in decode: 1124 vs 1462 tok/s at B = 8), so beyond one row
+# the limit is 32M elements up to M = 4 and 16M up to M = 8 (profiles/gemv_bench_r2.jsonl).
+_os = __import__("os")
+MAX_GEMV_NUMEL_M1 = int(_os.environ.get("HDS_GEMV_MAX_NUMEL_M1", str(1 << 40)))
+MAX_GEMV_NUMEL = int(_os.environ.get("HDS_GEMV_MAX_NUMEL", str(64 * 1024 * 1024)))
 
 
 def max_numel(M):
-    return MAX_GEMV_NUMEL >> (0 if M == 1 else (1 if M <= 4 else 2))
+    return MAX_GEMV_NUMEL_M1 if M == 1 else MAX_GEMV_NUMEL >> (1 if M <= 4 else 2)
 
 
 def gemv_ok(x2, w, b=None):
