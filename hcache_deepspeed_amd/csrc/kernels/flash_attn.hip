@@ -1110,12 +1110,15 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
           float pr = fast_exp2(x);
           if constexpr (EVO) {
             if (masked(p, qt * BN + qr0 + j, myk, len)) pr = 0.f;
-          } else {
-            if (need_mask && outside(qt * BN + qr0 + j, qlo, qhi)) pr = 0.f;
           }
           sacc[r] = pr;
           dpacc[r] = pr * (dpacc[r] - d4[j]);
         }
+      }
+      if (!EVO && need_mask) {  // wave-uniform branch: interior tiles run no mask VALU at all
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (outside(qt * BN + 32 * qh + acc_row(r, h), qlo, qhi)) sacc[r] = dpacc[r] = 0.f;
       }
       const bf16x8 p0 = acc_to_b<0>(sacc), p1 = acc_to_b<1>(sacc);
       const bf16x8 s0 = acc_to_b<0>(dpacc), s1 = acc_to_b<1>(dpacc);
@@ -1324,15 +1327,24 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
           float x = s[t][r] * c - lse2;
           if constexpr (EVO) x += evo_bias(p, b, hq, myq, key) * kLog2e;
           float pr = fast_exp2(x);
-          const bool off = EVO ? masked(p, myq, key, len) : outside(key, klo, khi);
-          if ((EVO || need_mask) && off) pr = 0.f;
-          s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
           if constexpr (EVO) {
+            const bool off = masked(p, myq, key, len);
+            if (off) pr = 0.f;
+            s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
             // pair-bias gradient, summed over the N rows of the MSA (float atomics into [B][H][L][L])
             if (p.db2 && !off)
               atomicAdd(p.db2 + ((int64_t)((b / p.evo_n) * p.hq + hq) * len + myq) * len + key, s[t][r]);
+          } else {
+            s[t][r] = pr * (dp[t][r] - dlt);  // dS^T
           }
         }
+      if (!EVO && need_mask) {  // wave-uniform branch: interior tiles run no mask VALU at all
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (outside(k0 + 32 * t + acc_row(r, h), klo, khi)) s[t][r] = 0.f;
+      }
       if constexpr (EVO) {
         if (p.db1) {  // mask-bias gradient: sum over this wave's 32 queries, then over heads by atomics
 #pragma unroll
