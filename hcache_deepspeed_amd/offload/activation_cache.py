@@ -267,8 +267,8 @@ class HostActivationCache:
                            if o.dev is None and o.host is not None)
                 if need == 0:
                     continue
-                if torch.cuda.memory_allocated(self.device) + need > self.budget - (2 << 30):
-                    break  # 2 GiB of headroom for the backward's own transients
+                if torch.cuda.memory_allocated(self.device) + need > self.budget:
+                    break
                 for o in self.by_layer[lj]:
                     self._prefetch(o)
 
