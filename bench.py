@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--layers", type=int, default=0, help="debug only: override layer count (result is marked invalid)")
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
+    ap.add_argument("--act-cache-policy", default="budget", choices=["budget", "recompute", "all"],
+                    help="host activation cache: spill the over-budget layers (budget), recompute them (recompute), "
+                         "or spill every eligible layer (all)")
     ap.add_argument("--act-cache-budget-gib", type=float, default=0.0,
                     help="host activation cache: HBM budget the planner keeps activations under (0: 92%% of HBM)")
     ap.add_argument("--host-act-cache", action="store_true",
@@ -127,7 +130,7 @@ def main():
                                                    "weight_decay": 0.1}},
         "gradient_clipping": 1.0,
         "zero_optimization": {"stage": args.zero},
-        "mi355x": {"zero3_prefetch_depth": args.prefetch, "comm_stats": world > 1, "host_act_cache": {"enabled": bool(args.host_act_cache),
+        "mi355x": {"zero3_prefetch_depth": args.prefetch, "comm_stats": world > 1, "host_act_cache": {"enabled": bool(args.host_act_cache), "policy": args.act_cache_policy,
                                                                         "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }

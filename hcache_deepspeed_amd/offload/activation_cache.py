@@ -27,6 +27,11 @@ allocation; from then on only the *earliest* layers 0..k-1 are spilled, with k t
 D2H has the whole remaining forward to drain and their H2D the whole remaining backward to prefetch. A runtime
 guard still spills any tensor that would push the allocation past the budget.
 
+``policy="recompute"`` plans the same over-budget layers but recomputes them in backward (non-reentrant activation
+checkpointing of just those blocks) instead of spilling them: when PCIe cannot hide the spill (at 32k tokens a
+Llama-3-8B layer moves ~3.5 GB each way, ~61 ms per direction against ~27 ms to recompute its forward), selective
+recomputation is the cheaper way to meet the budget; the closed-loop refinement below applies to either set.
+
 Two corrections keep the budgeted cache off the critical path:
 * the calibration peak over-states the all-spilled peak (spilled tensors still waiting for their D2H hold HBM
   inside the copy window), so after each planned step the forward/backward turn-around peak is compared with the
@@ -66,8 +71,10 @@ class _Tagged:
 class HostActivationCache:
 
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
-                 gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None):
+                 gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None, recompute=False):
         self.device = device
+        self.policy_recompute = bool(recompute)
+        self.recompute = set()  # blocks whose forward is checkpointed (policy "recompute")
         # D2H copy window: spilled bytes the host may have queued on the copy stream and not yet seen copied.
         # Autograd runs far ahead of the GPU on the host, and a spilled tensor's HBM is recycled only once its D2H
         # drained (record_stream) -- with PCIe slower than a layer's forward the backlog grows layer by layer. Left
@@ -116,7 +123,7 @@ class HostActivationCache:
     @classmethod
     def from_config(cls, cfg, device):
         budget = None
-        if getattr(cfg, "policy", "budget") == "budget" and device.type == "cuda":
+        if getattr(cfg, "policy", "budget") in ("budget", "recompute") and device.type == "cuda":
             gib = float(getattr(cfg, "gpu_budget_gib", 0.0) or 0.0)
             total = torch.cuda.get_device_properties(device).total_memory
             budget = int(gib * 2**30) if gib > 0 else int(0.92 * total)
@@ -127,7 +134,8 @@ class HostActivationCache:
         wgib = float(getattr(cfg, "copy_window_gib", 0.0) or 0.0)
         return cls(device, min_bytes=1 << 20, min_layers_resident=cfg.min_layers_resident,
                    prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget,
-                   host_budget_bytes=int(hgib * 2**30), copy_window_bytes=int(wgib * 2**30) if wgib > 0 else None)
+                   host_budget_bytes=int(hgib * 2**30), copy_window_bytes=int(wgib * 2**30) if wgib > 0 else None,
+                   recompute=getattr(cfg, "policy", "budget") == "recompute")
 
     # ---------------------------------------------------------------------------------------
     def attach(self, model):
@@ -139,7 +147,19 @@ class HostActivationCache:
         self.n_layers = len(blocks)
         for i, b in enumerate(blocks):
             self._attached.append(b.register_forward_pre_hook(lambda mod, args, i=i: self._enter(i)))
+            if self.policy_recompute:
+                b.forward = self._recompute_wrapper(b.forward, i)
         return self
+
+    def _recompute_wrapper(self, fwd, i):
+        from ..runtime.activation_checkpointing import checkpointing as ck
+
+        def run(*args, **kwargs):
+            if i in self.recompute and torch.is_grad_enabled():
+                return ck.checkpoint(fwd, *args, **kwargs)
+            return fwd(*args, **kwargs)
+
+        return run
 
     def _enter(self, i):
         if torch.is_grad_enabled():
@@ -156,18 +176,25 @@ class HostActivationCache:
                                             self.budget)
                 self._calibrating = False
                 self._cal_bytes = dict(self.layer_bytes)
+                if self.policy_recompute:  # the same over-budget layers, recomputed instead of spilled
+                    self.recompute, self.plan = set(self.plan), set()
                 log_dist(f"host activation cache: spilling {len(self.plan)} of {self.n_layers} layers (peak when spilling all {peak / 2**30:.1f} GiB, budget "
                          f"{self.budget / 2**30:.1f} GiB, {self._capped_this_step / 2**30:.1f} GiB kept by the host cap)",
                          ranks=[0])
             elif self.plan is None:
                 self._calibrating = True
             elif self._turn_peak is not None:
-                n0 = len(self.plan)
-                self.plan = refine_plan(self.plan, self._cal_bytes, self._turn_peak, self.budget)
-                if len(self.plan) != n0:
+                cur = self.recompute if self.policy_recompute else self.plan
+                new = refine_plan(cur, self._cal_bytes, self._turn_peak, self.budget)
+                if new != cur:
                     self.plan_adjustments += 1
+                    if self.policy_recompute:
+                        self.recompute = new
+                    else:
+                        self.plan = new
                     log_dist(f"host activation cache: turn-around peak {self._turn_peak / 2**30:.1f} GiB of "
-                             f"{self.budget / 2**30:.1f} GiB -> spilling {len(self.plan)} layers", ranks=[0])
+                             f"{self.budget / 2**30:.1f} GiB -> {'recomputing' if self.policy_recompute else 'spilling'} "
+                             f"{len(new)} layers", ranks=[0])
             self._turn_peak = None
             torch.cuda.reset_peak_memory_stats(self.device)
         self.cur_layer = -1
@@ -295,7 +322,8 @@ class HostActivationCache:
 
     def stats(self):
         return {"bytes_offloaded": self.bytes_offloaded, "pinned_pool_bytes": self.pool.bytes_allocated,
-                "spilled_layers": None if self.plan is None else len(self.plan), "late_unpacks": self.late_unpacks,
+                "spilled_layers": None if self.plan is None else len(self.plan),
+                "recomputed_layers": len(self.recompute), "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits}
 

@@ -167,7 +167,9 @@ class HostActCacheConfig:
     slots: int = 8
     slot_mb: int = 512
     min_layers_resident: int = 2
-    policy: str = "budget"  # "budget": spill only what exceeds gpu_budget_gib; "all": spill every eligible layer
+    # "budget": spill only what exceeds gpu_budget_gib; "recompute": checkpoint those layers instead of spilling;
+    # "all": spill every eligible layer
+    policy: str = "budget"
     gpu_budget_gib: float = 0.0  # 0: 92% of device memory
     prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block
     host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: min(40% of host RAM, 160 GiB))

@@ -224,3 +224,46 @@ def test_refine_plan_closed_loop():
     assert refine_plan({0, 1, 2}, lb, turn_peak=100, budget=95 + G) == {0, 1, 2, 3}      # over budget
     assert refine_plan(set(), lb, turn_peak=100, budget=95 + G) == {0}
     assert refine_plan({0, 1}, lb, turn_peak=0, budget=1000 + G) == set()
+
+
+def test_recompute_policy_wraps_planned_blocks():
+    """policy "recompute": the planned blocks run under activation checkpointing (same outputs and gradients,
+    no saved activations of their internals), the others are untouched."""
+    import torch.nn as nn
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    torch.manual_seed(0)
+    blocks = nn.ModuleList([nn.Sequential(nn.Linear(16, 16), nn.GELU(), nn.Linear(16, 16)) for _ in range(4)])
+    model = nn.Module()
+    model.blocks = blocks
+
+    def run(m, x):
+        for b in m.blocks:
+            x = x + b(x)
+        return x.square().sum()
+
+    x = torch.randn(8, 16, requires_grad=True)
+    ref = run(model, x)
+    ref.backward()
+    gref = [p.grad.clone() for p in model.parameters()]
+    for p in model.parameters():
+        p.grad = None
+    cache = HostActivationCache(torch.device("cpu"), recompute=True).attach(model)
+    cache.recompute = {0, 2}
+    calls = []
+    import hcache_deepspeed_amd.runtime.activation_checkpointing.checkpointing as ck
+    real = ck.checkpoint
+
+    def spy(fn, *a, **k):
+        calls.append(fn)
+        return real(fn, *a, **k)
+
+    ck.checkpoint = spy
+    try:
+        out = run(model, x.detach().requires_grad_(True))
+        out.backward()
+    finally:
+        ck.checkpoint = real
+    assert len(calls) == 2
+    torch.testing.assert_close(out, ref)
+    for p, g in zip(model.parameters(), gref):
+        torch.testing.assert_close(p.grad, g)

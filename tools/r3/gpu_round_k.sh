@@ -1,0 +1,13 @@
+# GPU: FA backward mask branch (flash tests + timing), headline bench, 32k budget with the recompute policy
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out/rk
+T="python -u -m pytest -x -v --timeout 150 --timeout-method thread"
+timeout -k 10 300 $T tests/test_kernels_gpu.py -k "flash or attn or evoformer" > gpurun_out/rk/flash_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u tools/r3/fa_bench.py > gpurun_out/rk/fa_bench.log 2>&1 || exit 1
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > gpurun_out/rk/bench.log 2>&1 || exit 1
+B="python -u bench.py --seq 32768 --micro-batch 1 --steps 4 --warmup 3"
+timeout -k 10 500 $B --host-act-cache --act-cache-policy recompute --act-cache-budget-gib 230 > gpurun_out/rk/ac32k_b230_recompute.log 2>&1 || exit 1
+timeout -k 10 500 $B --host-act-cache --act-cache-budget-gib 230 > gpurun_out/rk/ac32k_b230.log 2>&1 || exit 1
+timeout -k 10 500 $B --ckpt > gpurun_out/rk/ckpt32k.log 2>&1 || exit 1
