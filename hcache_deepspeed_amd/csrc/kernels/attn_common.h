@@ -122,6 +122,24 @@ __device__ __forceinline__ bf16x8 read_tr_off_asm(const char* tile, uint32_t y0,
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// Reads on a pre-added base b = tile + lane offset: with 1 KiB-aligned LDS allocations every tile base has bits 0-9
+// clear, so the k-step / column-block XOR (bits 5-7) commutes with the add -- ONE v_xor per read (none for k-step /
+// column block 0), and slot / sub-block offsets ride in the ds_read immediate (OFF).
+template <int OFF>
+__device__ __forceinline__ bf16x8 rows_x(uint32_t b, int ks) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(b ^ (32u * (uint32_t)ks)), "n"(OFF) : "memory");
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ bf16x8 tr_x(uint32_t b0, uint32_t b1, int dt) {
+  bf16x4 lo, hi;
+  const uint32_t x = 64u * (uint32_t)dt;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(b0 ^ x), "n"(OFF) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(b1 ^ x), "n"(OFF) : "memory");
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // row fragment (read_rows) issued as inline asm, retired by lds_wait<N>() like read_tr_asm
 __device__ __forceinline__ bf16x8 read_rows_asm(const char* lds_tile, int row0, int ks) {
   const int lane = threadIdx.x & 63;

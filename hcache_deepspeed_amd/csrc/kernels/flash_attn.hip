@@ -968,7 +968,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT;
   static_assert(D <= 128, "split dK/dV kernel keeps 8 tiles in LDS: head_dim <= 128");
   // LDS: K (2 x 16K), V (2 x 16K), Q[2] (16K each), dO[2] (16K each), lse[2][64], delta[2][64]
-  __shared__ __attribute__((aligned(16))) char smem[8 * 16384 + 4 * 256];
+  __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 4 * 256];  // 1 KiB: rows_x / tr_x bases
   char* const Kt = smem;
   char* const Vt = smem + 2 * 16384;
   char* const Qbase = smem + 4 * 16384;
@@ -1069,10 +1069,17 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
       if constexpr (PIPE != 0 && D == 128) {
         bf16x8 fa[3], fb[3];
+        // O tile = Q tile + 2 slots, V = K + 2 slots: immediates on one base register each
+        const uint32_t bq = (uint32_t)(uintptr_t)Qt + pq, bk = (uint32_t)(uintptr_t)Kw + pk;
         auto ld = [&](int j) {
           const int ks = j % KS;
-          fa[j % 3] = read_rows_off_asm(j < KS ? Qt : Ot, pq, ks);
-          fb[j % 3] = read_rows_off_asm(j < KS ? Kw : Vw, pk, ks);
+          if (j < KS) {
+            fa[j % 3] = rows_x<0>(bq, ks);
+            fb[j % 3] = rows_x<0>(bk, ks);
+          } else {
+            fa[j % 3] = rows_x<2 * 16384>(bq, ks);
+            fb[j % 3] = rows_x<2 * 16384>(bk, ks);
+          }
         };
         ld(0);
         ld(1);
@@ -1125,7 +1132,17 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
       if constexpr (PIPE != 0 && D == 128) {
         // j = 4 dt + r: r 0/1 -> dV with dO^T halves, r 2/3 -> dK with Q^T halves
         bf16x8 ft[3];
-        auto ldt = [&](int j) { ft[j % 3] = read_tr_off_asm((j & 3) < 2 ? Ot : Qt, ty0, ty1, 2 * qh + (j & 1), j >> 2); };
+        // k-step s = 2 qh + (j & 1): the qh part in the base, the (j & 1) part and the O slot in the immediate
+        const uint32_t b0 = (uint32_t)(uintptr_t)Qt + 8192u * qh + ty0, b1 = (uint32_t)(uintptr_t)Qt + 8192u * qh + ty1;
+        auto ldt = [&](int j) {
+          const int dt = j >> 2;
+          switch (j & 3) {
+            case 0: ft[j % 3] = tr_x<2 * 16384>(b0, b1, dt); break;         // dO^T, k-step 2 qh
+            case 1: ft[j % 3] = tr_x<2 * 16384 + 4096>(b0, b1, dt); break;  // dO^T, k-step 2 qh + 1
+            case 2: ft[j % 3] = tr_x<0>(b0, b1, dt); break;                 // Q^T
+            default: ft[j % 3] = tr_x<4096>(b0, b1, dt); break;
+          }
+        };
         ldt(0);
         ldt(1);
 #pragma unroll
@@ -1197,7 +1214,7 @@ template <int D, int NW, int PRIO, bool EVO = false, int PIPE = 0>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 32 * NW;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TL];  // K[2], V[2]
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TL];  // K[2], V[2]; 1 KiB: rows_x / tr_x bases
   int blk, hq, b;
   lpt_ids(blk, hq, b);
   int start, len;
@@ -1283,9 +1300,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
         // j = 16 t + 8 which + ks: which 0 -> S (K rows x Q), 1 -> dP (V rows x dO)
         s[0] = s[1] = dp[0] = dp[1] = f32x16{};
         bf16x8 fa[3];
+        const uint32_t bk = (uint32_t)(uintptr_t)Kt + pr0;  // V = K + 2 slots, rows 32.. = +8192: immediates
         auto ld = [&](int j) {
           const int t = j >> 4, which = (j >> 3) & 1, ks = j & 7;
-          fa[j % 3] = read_rows_off_asm(which ? Vt : Kt, t ? pr1 : pr0, ks);
+          if (which == 0)
+            fa[j % 3] = t ? rows_x<8192>(bk, ks) : rows_x<0>(bk, ks);
+          else
+            fa[j % 3] = t ? rows_x<2 * TL + 8192>(bk, ks) : rows_x<2 * TL>(bk, ks);
         };
         ld(0);
         ld(1);
@@ -1362,7 +1383,16 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
       const bf16x8 sb[4] = {acc_to_b<0>(s[0]), acc_to_b<1>(s[0]), acc_to_b<0>(s[1]), acc_to_b<1>(s[1])};
       if constexpr (PIPE != 0 && D == 128 && !EVO) {
         bf16x8 ft[3];
-        auto ldt = [&](int j) { ft[j % 3] = read_tr_off_asm(Kt, ty0, ty1, j & 3, j >> 2); };
+        const uint32_t b0 = (uint32_t)(uintptr_t)Kt + ty0, b1 = (uint32_t)(uintptr_t)Kt + ty1;
+        auto ldt = [&](int j) {
+          const int dt = j >> 2;
+          switch (j & 3) {  // k-step s = j & 3 in the immediate
+            case 0: ft[j % 3] = tr_x<0>(b0, b1, dt); break;
+            case 1: ft[j % 3] = tr_x<4096>(b0, b1, dt); break;
+            case 2: ft[j % 3] = tr_x<8192>(b0, b1, dt); break;
+            default: ft[j % 3] = tr_x<12288>(b0, b1, dt); break;
+          }
+        };
         ldt(0);
         ldt(1);
 #pragma unroll
