@@ -209,6 +209,9 @@ class HostActivationCache:
         self._capped_this_step = 0
         with torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack):
             yield
+        if self.device.type == "cuda" and self._turn_peak is None:
+            # end of the forward: every saved activation is alive -- the turn-around peak the plan refinement uses
+            self._turn_peak = torch.cuda.max_memory_allocated(self.device)
 
     # ---------------------------------------------------------------------------------------
     def _window(self, q, nbytes):
