@@ -42,7 +42,7 @@ def _staged(fn_name):
     return call
 
 
-def _run(rank, world, d, steps=3):
+def _run(rank, world, d, steps=3, symmetric=False):
     import hcache_deepspeed_amd as hds
     import hcache_deepspeed_amd.comm as hcomm
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
@@ -59,7 +59,13 @@ def _run(rank, world, d, steps=3):
     cfg = {"train_micro_batch_size_per_gpu": mb, "bf16": {"enabled": True}, "gradient_clipping": 1.0,
            "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "zero_optimization": {"stage": 3},
            "mi355x": {"comm_stats": True}}
+    if symmetric:
+        cfg["compile"] = {"symmetric_memory": True}
     eng, _, _, _ = hds.initialize(model=m, config=cfg)
+    if symmetric:
+        eng.compile()
+        if world > 1 and on_gpu:
+            assert getattr(eng.optimizer, "_symm", None), "symmetric-memory collectives not enabled"
     assert eng.device.type == ("cuda" if on_gpu else "cpu")
     z = eng.optimizer
     if world > 1:
@@ -80,10 +86,15 @@ def _run(rank, world, d, steps=3):
         assert summ["collectives"]["all_gather"]["count"] > 0
         assert summ["collectives"]["reduce_scatter"]["count"] > 0
     full = {n: safe_get_full_fp32_param(p).float().cpu() for n, p in eng.module.named_parameters()}
+    if symmetric and world > 1 and on_gpu:
+        calls = {k: sum(sm.calls[k] for sm in z._symm.values()) for k in ("all_gather", "reduce_scatter")}
+        assert calls["all_gather"] > 0 and calls["reduce_scatter"] > 0, calls
+        assert all(sm.error() == 0 for sm in z._symm.values())
     ls = torch.tensor(losses)
     torch.distributed.all_reduce(ls)
     if rank == 0:
-        torch.save({"losses": (ls / world).tolist(), "weights": full}, os.path.join(d, f"w{world}.pt"))
+        tag = "s" if symmetric else ""
+        torch.save({"losses": (ls / world).tolist(), "weights": full}, os.path.join(d, f"w{world}{tag}.pt"))
 
 
 def test_zero3_partitioned_device_path_world2_matches_world1(tmp_path):
@@ -92,6 +103,22 @@ def test_zero3_partitioned_device_path_world2_matches_world1(tmp_path):
     run_distributed(_run, 2, d)
     a = torch.load(os.path.join(d, "w1.pt"), weights_only=True)
     b = torch.load(os.path.join(d, "w2.pt"), weights_only=True)
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert abs(la - lb) <= 2e-2 * abs(la), (a["losses"], b["losses"])
+    for n, w in a["weights"].items():
+        rel = float((b["weights"][n] - w).norm() / w.norm().clamp_min(1e-12))
+        assert rel < 2e-2, (n, rel)
+
+
+def test_zero3_symmetric_memory_world2_matches_world1(tmp_path):
+    """compile.symmetric_memory at world 2 on one MI355X: the unit all-gathers and reduce-scatters run as the
+    one-kernel symmetric-memory collectives (IPC-mapped buffers of the other process), and training follows the
+    world-1 run like the RCCL/gloo path does."""
+    d = str(tmp_path)
+    run_distributed(_run, 1, d)
+    run_distributed(_run, 2, d, 3, True)
+    a = torch.load(os.path.join(d, "w1.pt"), weights_only=True)
+    b = torch.load(os.path.join(d, "w2s.pt"), weights_only=True)
     for la, lb in zip(a["losses"], b["losses"]):
         assert abs(la - lb) <= 2e-2 * abs(la), (a["losses"], b["losses"])
     for n, w in a["weights"].items():
