@@ -121,6 +121,7 @@ class _FusedLinearCEFn(torch.autograd.Function):
         want_dw = need_grad and weight.requires_grad
         dw = None  # fp32 accumulator: the first chunk's GEMM writes it (beta = 0), no zero-fill pass
         native_path = native.use_native(hidden)
+        wcache = {}  # the LM-head weight transposed once for every chunk's dgrad (NT layout)
         for s in range(0, T, chunk_rows):
             e = min(T, s + chunk_rows)
             hc = hidden[s:e]
@@ -142,7 +143,7 @@ class _FusedLinearCEFn(torch.autograd.Function):
                 if dh is not None:
                     if dl.is_cuda:
                         from .gemm import dgrad
-                        dgrad(dl, weight, out=dh[s:e])
+                        dgrad(dl, weight, out=dh[s:e], cache=wcache)
                     else:
                         torch.mm(dl, weight, out=dh[s:e])
                 if want_dw:
@@ -157,6 +158,7 @@ class _FusedLinearCEFn(torch.autograd.Function):
                     else:
                         _addmm_f32_(dw, dl.t(), hc)
             del logits
+        del wcache
         ctx.save_for_backward(dh, dw)
         ctx.wdtype = weight.dtype
         ctx.weight = weight  # the Parameter object: its gradient may be written in place (ZeRO)

@@ -58,21 +58,26 @@ def gemm_nt(a, b, out=None, alpha=1.0, accumulate=False, variant=None):
 # ----------------------------------------------------------------------------------------------------------------
 # weight-gradient GEMM layout: dW[N, K] (+)= dY[T, N]^T X[T, K]
 # ----------------------------------------------------------------------------------------------------------------
-def transpose2d(x):
+_TRANSPOSE_VAR = int(os.environ.get("HDS_TRANSPOSE_VAR", "2"))  # 1: 64x64 tile, 2-B LDS ops; 2: 64x128, 8/16-B
+
+
+def transpose2d(x, variant=None):
     """[R, C] (unit last stride) -> contiguous [C, R]; HIP LDS-tiled kernel for bf16 on the GPU."""
     R, C = x.shape
     if not (native.use_native(x) and x.dtype == torch.bfloat16 and x.stride(1) == 1 and R % 8 == 0
-            and x.stride(0) % 8 == 0):
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0):
         return x.t().contiguous()
     out = torch.empty(C, R, dtype=x.dtype, device=x.device)
-    native.check(native.kernels().hds_transpose_bf16(x.data_ptr(), out.data_ptr(), R, C, x.stride(0),
-                                                     native.stream()), "transpose_bf16")
+    var = _TRANSPOSE_VAR if variant is None else int(variant)
+    native.check(native.kernels().hds_transpose_bf16_var(x.data_ptr(), out.data_ptr(), R, C, x.stride(0), var,
+                                                         native.stream()), "transpose_bf16")
     return out
 
 
 _WGRAD_LAYOUT = os.environ.get("HDS_WGRAD_LAYOUT", "auto")  # auto | direct | nt | direct_sk2 | nt_sk2
 _WGRAD_CHOICE = {}
 _SPLITK = os.environ.get("HDS_WGRAD_SPLITK", "0") == "1"  # two-stream split-K candidates in the timed choice
+_B2 = os.environ.get("HDS_WGRAD_B2", "0") == "1"  # batched two-half split-K candidates in the timed choice
 
 
 def _mm_into(out, a, bt, accumulate):
@@ -98,18 +103,38 @@ def _side_stream(dev):
     return s
 
 
+def _bmm_halves(out, a, bt, accumulate):
+    """out (+)= a[N, T] @ bt[T, K] as ONE batched GEMM over the two halves of the token (reduction) dimension into
+    fp32 partials [2, N, K], then one add. Batch 2 doubles the output-tile count of the grid (qkv: 384 -> 768 tiles of
+    256^2 = 3 full waves on 256 CUs instead of 1.5; down: 896 -> 1792 = 7 instead of 3.5) without a second stream."""
+    N, T = a.shape
+    K = bt.shape[1]
+    h = T // 2
+    A = a.as_strided((2, N, h), (h * a.stride(1), a.stride(0), a.stride(1)), a.storage_offset())
+    B = bt.as_strided((2, h, K), (h * bt.stride(0), bt.stride(0), bt.stride(1)), bt.storage_offset())
+    part = torch.bmm(A, B, out_dtype=torch.float32) if out.is_cuda else torch.bmm(A.float(), B.float())
+    if accumulate:
+        out.add_(part[0] + part[1])
+    else:
+        torch.add(part[0], part[1], out=out)
+
+
 def _wgrad_run(layout, dy2, x2, out, accumulate):
     """``layout``: "direct" (TN as autograd issues it), "nt" (HIP transposes + the NT GEMM), or either with "_sk2":
     the token (reduction) dimension split in two halves run as CONCURRENT GEMMs on two streams, the second into a
-    scratch buffer added at the join. A projection with few output tiles (qkv: 24 x 16 tiles of 256 = 1.5 waves on
-    256 CUs; down: 3.5 waves) otherwise idles part of the chip in its last wave; two half-K GEMMs in flight fill it."""
-    base, sk2 = layout.split("_")[0], layout.endswith("_sk2")
+    scratch buffer added at the join, or with "_b2": the two halves as one batched GEMM (``_bmm_halves``). A
+    projection with few output tiles (qkv: 24 x 16 tiles of 256 = 1.5 waves on 256 CUs; down: 3.5 waves) otherwise
+    idles part of the chip in its last wave; two half-K GEMMs in flight fill it."""
+    base, sk2, b2 = layout.split("_")[0], layout.endswith("_sk2"), layout.endswith("_b2")
     if base == "nt":  # hipBLASLt's NT form on transposed copies (the forward GEMM's fast layout)
         a, bt = transpose2d(dy2), transpose2d(x2).t()
         split_a, split_b = (lambda t, lo, hi: t[:, lo:hi]), (lambda t, lo, hi: t[lo:hi])
     else:
         a, bt = dy2.t(), x2
         split_a, split_b = (lambda t, lo, hi: t[:, lo:hi]), (lambda t, lo, hi: t[lo:hi])
+    if b2 and a.shape[1] % 2 == 0:
+        _bmm_halves(out, a, bt, accumulate)
+        return
     if not sk2 or not out.is_cuda:
         _mm_into(out, a, bt, accumulate)
         return
@@ -153,7 +178,8 @@ def wgrad(dy2, x2, out, accumulate=False):
             key = (tuple(dy2.shape), tuple(x2.shape), out.dtype, bool(accumulate))
             layout = _WGRAD_CHOICE.get(key)
             if layout is None:
-                cands = ("direct", "nt", "direct_sk2", "nt_sk2") if _SPLITK else ("direct", "nt")
+                cands = ("direct", "nt") + (("direct_b2", "nt_b2") if _B2 else ()) + (
+                    ("direct_sk2", "nt_sk2") if _SPLITK else ())
                 times = {c: _time_layout(c, dy2, x2, out, accumulate) for c in cands}
                 layout = min(times, key=times.get)
                 if layout != "direct" and times[layout] > 0.97 * times["direct"]:
@@ -170,17 +196,25 @@ _DGRAD_LAYOUT = os.environ.get("HDS_DGRAD_LAYOUT", "auto")  # auto | direct | nt
 _DGRAD_CHOICE = {}
 
 
-def _dgrad_run(layout, dy2, w, out):
-    b = transpose2d(w).t() if layout == "nt" else w  # nt: dY @ (W^T)^T, hipBLASLt's NT form
+def _dgrad_run(layout, dy2, w, out, cache=None):
+    if layout == "nt":  # nt: dY @ (W^T)^T, hipBLASLt's NT form
+        b = cache.get("wt") if cache is not None else None
+        if b is None:
+            b = transpose2d(w).t()
+            if cache is not None:
+                cache["wt"] = b
+    else:
+        b = w
     if out is None:
         return torch.mm(dy2, b)
     return torch.mm(dy2, b, out=out)
 
 
-def dgrad(dy2, w, out=None):
+def dgrad(dy2, w, out=None, cache=None):
     """dy2[T, N] @ w[N, K] with the faster of the NN GEMM autograd issues and a HIP transpose of the (small) weight +
     the NT GEMM, timed once per shape under ``HDS_DGRAD_LAYOUT=auto`` (the NT form ran 1.51-1.59 PF/s against
-    1.32-1.39 for NN at the bench shapes, profiles/gemm_layouts_r1.log)."""
+    1.32-1.39 for NN at the bench shapes, profiles/gemm_layouts_r1.log). ``cache``: a dict the caller keeps for the
+    calls that share ``w`` (the fused CE's per-chunk LM-head dgrads): the transposed weight is made once."""
     layout = _DGRAD_LAYOUT
     if layout == "auto":
         if not (dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy2.stride(1) == 1
@@ -201,4 +235,4 @@ def dgrad(dy2, w, out=None):
                     times[cand] = e0.elapsed_time(e1)
                 layout = "nt" if times["nt"] < 0.97 * times["direct"] else "direct"
                 _DGRAD_CHOICE[key] = layout
-    return _dgrad_run(layout, dy2, w, out)
+    return _dgrad_run(layout, dy2, w, out, cache)

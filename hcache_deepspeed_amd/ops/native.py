@@ -63,6 +63,7 @@ _KERNEL_SIGS = {
     "hds_dequant_minifloat": "i" + "ppp" + "l" + "iii" + "s",
     "hds_fp6_gemv": "pppp" + "iiiiii" + "s",
     "hds_transpose_bf16": "pp" + "ii" + "l" + "s",
+    "hds_transpose_bf16_var": "pp" + "ii" + "l" + "i" + "s",
     "hds_gemv_bf16_supported": "iii",
     "hds_gemv_bf16": "pppp" + "iii" + "ll" + "s",
     "hds_wmix_splits": "iii",

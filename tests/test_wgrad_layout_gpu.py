@@ -5,15 +5,17 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (1000, 136, 136), (4096, 520, 1024), (8, 7, 8)])
-def test_transpose_matches_torch(R, C, ld):
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (1000, 136, 136), (4096, 520, 1024), (8, 7, 8), (64, 128, 128),
+                                    (200, 260, 264), (72, 129, 136), (4096, 4096, 4096)])
+def test_transpose_matches_torch(R, C, ld, variant):
     from hcache_deepspeed_amd.ops.gemm import transpose2d
     base = torch.randn(R, ld, device="cuda", dtype=torch.bfloat16)
     x = base[:, :C]
-    assert torch.equal(transpose2d(x), x.t().contiguous())
+    assert torch.equal(transpose2d(x, variant=variant), x.t().contiguous())
 
 
-@pytest.mark.parametrize("layout", ["direct", "nt", "direct_sk2", "nt_sk2", "auto"])
+@pytest.mark.parametrize("layout", ["direct", "nt", "direct_sk2", "nt_sk2", "direct_b2", "nt_b2", "auto"])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
 def test_wgrad_layouts_match(layout, out_dtype, monkeypatch):
     from hcache_deepspeed_amd.ops import gemm
@@ -39,6 +41,9 @@ def test_dgrad_layouts_match(layout, monkeypatch):
     ref = dy.float() @ w.float()
     got = gemm.dgrad(dy, w)
     assert (got.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    cache = {}
+    for _ in range(2):  # the second call reuses the cached transposed weight
+        assert torch.equal(gemm.dgrad(dy, w, cache=cache), got)
     out = torch.empty(1024, 512, device="cuda", dtype=torch.bfloat16)
     gemm.dgrad(dy, w, out=out)
     assert torch.equal(out, got)

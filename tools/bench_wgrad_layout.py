@@ -57,9 +57,12 @@ def splitk():
         out = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
         fl = 2 * T * N * K
         res = {}
-        for lay in ("direct", "nt", "direct_sk2", "nt_sk2"):
+        ref = torch.mm(dy.t().float(), x.float())
+        lays = ("direct", "nt", "direct_b2", "nt_b2") + (("direct_sk2", "nt_sk2") if "--streams" in sys.argv else ())
+        for lay in lays:
             ts = t(lambda: gemm._wgrad_run(lay, dy, x, out, False))
-            res[lay] = (round(ts * 1e3, 3), round(fl / ts / 1e15, 3))
+            err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+            res[lay] = (round(ts * 1e3, 3), round(fl / ts / 1e15, 3), round(err, 5))
         print(name, json.dumps(res), flush=True)
 
 
