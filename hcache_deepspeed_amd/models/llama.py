@@ -208,7 +208,11 @@ class LlamaMLP(nn.Module):
         if self.fpdt_chunks > 1:
             from ..parallel.fpdt import fpdt_gated_ffn
             return fpdt_gated_ffn(x, self.gate_up_proj.weight, self.down_proj.weight, self.fpdt_chunks, self.act)
-        return self.down_proj(glu(self.gate_up_proj(x), self.act))
+        # ZeRO linears on both sides: the SwiGLU kernels also write the transposes the two weight gradients read
+        # (runtime/zero/linear.py), instead of separate HBM transposes in the backward
+        t = (torch.is_grad_enabled() and getattr(self.down_proj, "_hds_mel", False)
+             and getattr(self.gate_up_proj, "_hds_mel", False))
+        return self.down_proj(glu(self.gate_up_proj(x), self.act, transposed=t))
 
 
 class LlamaDecoderLayer(nn.Module):

@@ -29,13 +29,31 @@ def _ref_act(x, a):
     return x
 
 
+def _t_ok(gu):
+    """The transposed-output kernels' contract: bf16 on the GPU, rows and I multiples of 8, 16-B aligned."""
+    I = gu.shape[-1] // 2
+    rows = gu.numel() // max(1, 2 * I)
+    return (native.use_native(gu) and gu.dtype == torch.bfloat16 and gu.is_contiguous() and rows % 8 == 0
+            and I % 8 == 0 and rows > 0 and gu.data_ptr() % 16 == 0)
+
+
 class _GLUFn(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, gu, act):
+    def forward(ctx, gu, act, transposed=False):
         I = gu.shape[-1] // 2
         ctx.act = act
         ctx.save_for_backward(gu)
+        ctx.transposed = bool(transposed) and _t_ok(gu)
+        if ctx.transposed:
+            rows = gu.numel() // (2 * I)
+            y = torch.empty(rows, I, device=gu.device, dtype=gu.dtype)
+            yt = torch.empty(I, rows, device=gu.device, dtype=gu.dtype)
+            native.check(native.kernels().hds_glu_fwd_t(act, gu.data_ptr(), y.data_ptr(), yt.data_ptr(), rows, I,
+                                                        native.stream()), "glu_fwd_t")
+            out = y.view(*gu.shape[:-1], I)
+            out._hds_t = yt  # the consumer may save this [I, rows] copy instead of out (runtime/zero/linear.py)
+            return out
         if native.use_native(gu):
             gu2 = gu.reshape(-1, 2 * I).contiguous()
             y = torch.empty(gu2.shape[0], I, device=gu.device, dtype=gu.dtype)
@@ -49,28 +67,45 @@ class _GLUFn(torch.autograd.Function):
     def backward(ctx, dy):
         (gu, ) = ctx.saved_tensors
         I = gu.shape[-1] // 2
+        if ctx.transposed and dy.dtype == gu.dtype:
+            from .gemm import wants_transposed_dy
+            if wants_transposed_dy(2 * I):
+                rows = gu.numel() // (2 * I)
+                d = dy.reshape(rows, I).contiguous()
+                dgu = torch.empty(rows, 2 * I, device=gu.device, dtype=gu.dtype)
+                dgut = torch.empty(2 * I, rows, device=gu.device, dtype=gu.dtype)
+                native.check(native.kernels().hds_glu_bwd_t(ctx.act, d.data_ptr(), gu.data_ptr(), dgu.data_ptr(),
+                                                            dgut.data_ptr(), rows, I, native.stream()), "glu_bwd_t")
+                r = dgu.view(gu.shape)
+                r._hds_t = dgut  # the gate|up projection's weight gradient reads this [2I, rows] copy (NT form)
+                return r, None, None
         if native.use_native(gu):
             gu2 = gu.reshape(-1, 2 * I).contiguous()
             dgu = torch.empty_like(gu2)
             native.check(native.kernels().hds_glu_bwd(native.dt(gu), ctx.act, dy.reshape(-1, I).contiguous().data_ptr(),
                                                       gu2.data_ptr(), dgu.data_ptr(), gu2.shape[0], I,
                                                       native.stream()), "glu_bwd")
-            return dgu.view(gu.shape), None
+            return dgu.view(gu.shape), None, None
         with torch.enable_grad():
             g = gu.detach().float().requires_grad_(True)
             a, u = g.split(I, dim=-1)
             y = _ref_act(a, ctx.act) * u
             (dg, ) = torch.autograd.grad(y, g, dy.float())
-        return dg.to(gu.dtype), None
+        return dg.to(gu.dtype), None, None
 
 
-def glu(gu, act="silu"):
-    """act(gu[..., :I]) * gu[..., I:] for the fused gate|up projection output."""
-    return _GLUFn.apply(gu, act_code(act))
+def glu(gu, act="silu", transposed=False):
+    """act(gu[..., :I]) * gu[..., I:] for the fused gate|up projection output.
+
+    ``transposed=True`` (bf16 on the GPU, rows % 8 == 0): the kernel also writes the output's transpose [I, rows]
+    and attaches it as ``out._hds_t``; a ZeRO linear consuming ``out`` saves that copy instead of ``out`` for its
+    weight gradient (hipBLASLt's NT form needs the token dimension contiguous). The backward likewise hands the
+    gate|up projection the transpose of d(gate|up). Both replace a separate HBM transpose pass in the backward."""
+    return _GLUFn.apply(gu, act_code(act), bool(transposed))
 
 
 def swiglu(gu):
-    return _GLUFn.apply(gu, SILU)
+    return _GLUFn.apply(gu, SILU, False)
 
 
 class _BiasActFn(torch.autograd.Function):

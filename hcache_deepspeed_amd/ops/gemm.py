@@ -58,7 +58,9 @@ def gemm_nt(a, b, out=None, alpha=1.0, accumulate=False, variant=None):
 # ----------------------------------------------------------------------------------------------------------------
 # weight-gradient GEMM layout: dW[N, K] (+)= dY[T, N]^T X[T, K]
 # ----------------------------------------------------------------------------------------------------------------
-_TRANSPOSE_VAR = int(os.environ.get("HDS_TRANSPOSE_VAR", "2"))  # 1: 64x64 tile, 2-B LDS ops; 2: 64x128, 8/16-B
+# 1: 64x64 tile, 2-B LDS ops; 2: 64x128, 8/16-B LDS ops -- the same ~4.5-5 TB/s at the step's shapes
+# (profiles/r3/transpose_bench_r3.log): HBM read/write mix, not LDS, bounds both
+_TRANSPOSE_VAR = int(os.environ.get("HDS_TRANSPOSE_VAR", "1"))
 
 
 def transpose2d(x, variant=None):
@@ -77,7 +79,7 @@ def transpose2d(x, variant=None):
 _WGRAD_LAYOUT = os.environ.get("HDS_WGRAD_LAYOUT", "auto")  # auto | direct | nt | direct_sk2 | nt_sk2
 _WGRAD_CHOICE = {}
 _SPLITK = os.environ.get("HDS_WGRAD_SPLITK", "0") == "1"  # two-stream split-K candidates in the timed choice
-_B2 = os.environ.get("HDS_WGRAD_B2", "0") == "1"  # batched two-half split-K candidates in the timed choice
+_B2 = os.environ.get("HDS_WGRAD_B2", "1") == "1"  # batched two-half split-K candidates in the timed choice
 
 
 def _mm_into(out, a, bt, accumulate):
@@ -119,19 +121,21 @@ def _bmm_halves(out, a, bt, accumulate):
         torch.add(part[0], part[1], out=out)
 
 
-def _wgrad_run(layout, dy2, x2, out, accumulate):
+def _wgrad_run(layout, dy2, x2, out, accumulate, dyt=None, xt=None):
     """``layout``: "direct" (TN as autograd issues it), "nt" (HIP transposes + the NT GEMM), or either with "_sk2":
     the token (reduction) dimension split in two halves run as CONCURRENT GEMMs on two streams, the second into a
     scratch buffer added at the join, or with "_b2": the two halves as one batched GEMM (``_bmm_halves``). A
     projection with few output tiles (qkv: 24 x 16 tiles of 256 = 1.5 waves on 256 CUs; down: 3.5 waves) otherwise
-    idles part of the chip in its last wave; two half-K GEMMs in flight fill it."""
+    idles part of the chip in its last wave; two half-K GEMMs in flight fill it. ``dyt`` / ``xt``: transposes the
+    producer already wrote ([N, T] / [K, T]); the "nt" forms use them instead of transposing (``x2`` may then be
+    None)."""
     base, sk2, b2 = layout.split("_")[0], layout.endswith("_sk2"), layout.endswith("_b2")
     if base == "nt":  # hipBLASLt's NT form on transposed copies (the forward GEMM's fast layout)
-        a, bt = transpose2d(dy2), transpose2d(x2).t()
-        split_a, split_b = (lambda t, lo, hi: t[:, lo:hi]), (lambda t, lo, hi: t[lo:hi])
+        a = dyt if dyt is not None else transpose2d(dy2)
+        bt = (xt if xt is not None else transpose2d(x2)).t()
     else:
         a, bt = dy2.t(), x2
-        split_a, split_b = (lambda t, lo, hi: t[:, lo:hi]), (lambda t, lo, hi: t[lo:hi])
+    split_a, split_b = (lambda t, lo, hi: t[:, lo:hi]), (lambda t, lo, hi: t[lo:hi])
     if b2 and a.shape[1] % 2 == 0:
         _bmm_halves(out, a, bt, accumulate)
         return
@@ -153,39 +157,71 @@ def _wgrad_run(layout, dy2, x2, out, accumulate):
     out.add_(tmp)
 
 
-def _time_layout(layout, dy2, x2, out, accumulate):
+def _time_layout(layout, dy2, x2, out, accumulate, dyt=None, xt=None, reps=2):
     scratch = torch.zeros_like(out)
-    _wgrad_run(layout, dy2, x2, scratch, accumulate)  # warm (hipBLASLt solution lookup, allocator)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    _wgrad_run(layout, dy2, x2, scratch, accumulate)
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1)
+    _wgrad_run(layout, dy2, x2, scratch, accumulate, dyt, xt)  # warm (hipBLASLt solution lookup, allocator)
+    best = float("inf")
+    for _ in range(reps):  # min of reps: one timed run mis-picked the down-projection layout in situ
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _wgrad_run(layout, dy2, x2, scratch, accumulate, dyt, xt)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    return best
 
 
-def wgrad(dy2, x2, out, accumulate=False):
-    """out[N, K] (+)= dy2[T, N]^T @ x2[T, K] with the faster of two layouts for this shape: the TN GEMM autograd
-    issues (``direct``) or two HBM-rate HIP transposes + the NT GEMM (``nt``). ``HDS_WGRAD_LAYOUT=auto`` times both
-    once per (shape, dtype, accumulate) on the first call (profiles/wgrad_layout_r2.log: NT runs 1.44-1.47 PF/s
-    where TN runs 0.94-1.10 at the o / gate_up shapes, and no faster at qkv / down)."""
+def _b2_useful(N, K):
+    """A two-half batched GEMM only pays when the 256 x 256 output-tile grid leaves the last wave of 256 CUs about
+    half empty (qkv 1.5 waves, down 3.5; not gate_up 7 or o 1)."""
+    tiles = -(-N // 256) * -(-K // 256)
+    frac = (tiles % 256) / 256
+    return _B2 and 0.2 < frac < 0.8
+
+
+_NT_BY_N = {}  # dy columns -> True if the timed choice for that gradient width was an "nt" form
+
+
+def wants_transposed_dy(n):
+    """Should a producer of a [T, n] output gradient also write its transpose (ops/activations.glu)? Yes until a
+    weight gradient of that width has chosen a non-NT layout."""
+    return _NT_BY_N.get(int(n), True)
+
+
+def wgrad(dy2, x2, out, accumulate=False, dyt=None, xt=None):
+    """out[N, K] (+)= dy2[T, N]^T @ x2[T, K] with the fastest layout for this shape: the TN GEMM autograd issues
+    (``direct``), two HBM-rate HIP transposes + the NT GEMM (``nt``), or either as one batched GEMM over the two
+    token halves (``_b2``, shapes whose tile grid ends in a half-empty wave). ``HDS_WGRAD_LAYOUT=auto`` times the
+    candidates once per (shape, dtype, accumulate, pre-transposed operands) on the first call
+    (profiles/wgrad_layout_r2.log: NT runs 1.44-1.47 PF/s where TN runs 0.94-1.10 at the o / gate_up shapes).
+    ``dyt`` [N, T] / ``xt`` [K, T]: transposes the producers already wrote (glu, runtime/zero/linear.py); with
+    ``x2`` None only the NT forms are possible."""
     layout = _WGRAD_LAYOUT
+    T, N = dy2.shape
+    K = xt.shape[0] if x2 is None else x2.shape[1]
     if layout == "auto":
-        if not (dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
-                and dy2.stride(1) == 1 and x2.stride(1) == 1):
-            layout = "direct"
+        if not (dy2.is_cuda and dy2.dtype == torch.bfloat16 and (x2 is None or x2.dtype == torch.bfloat16)
+                and dy2.stride(1) == 1 and (x2 is None or x2.stride(1) == 1)):
+            layout = "direct" if x2 is not None else "nt"
         else:
-            key = (tuple(dy2.shape), tuple(x2.shape), out.dtype, bool(accumulate))
+            key = (tuple(dy2.shape), K, out.dtype, bool(accumulate), x2 is None, dyt is not None)
             layout = _WGRAD_CHOICE.get(key)
             if layout is None:
-                cands = ("direct", "nt") + (("direct_b2", "nt_b2") if _B2 else ()) + (
-                    ("direct_sk2", "nt_sk2") if _SPLITK else ())
-                times = {c: _time_layout(c, dy2, x2, out, accumulate) for c in cands}
+                b2 = ("_b2", ) if _b2_useful(N, K) else ()
+                if x2 is None:
+                    cands = ("nt", ) + tuple("nt" + x for x in b2)
+                else:
+                    cands = ("direct", "nt") + tuple(c + x for x in b2 for c in ("direct", "nt")) + (
+                        ("direct_sk2", "nt_sk2") if _SPLITK else ())
+                times = {c: _time_layout(c, dy2, x2, out, accumulate, dyt, xt) for c in cands}
                 layout = min(times, key=times.get)
-                if layout != "direct" and times[layout] > 0.97 * times["direct"]:
+                if x2 is not None and layout != "direct" and times[layout] > 0.97 * times["direct"]:
                     layout = "direct"  # within noise: keep the plain form
                 _WGRAD_CHOICE[key] = layout
-    _wgrad_run(layout, dy2, x2, out, accumulate)
+                _NT_BY_N[N] = layout.startswith("nt")
+    elif x2 is None and not layout.startswith("nt"):
+        layout = "nt"
+    _wgrad_run(layout, dy2, x2, out, accumulate, dyt, xt)
     return out
 
 

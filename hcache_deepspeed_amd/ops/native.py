@@ -26,6 +26,8 @@ _KERNEL_SIGS = {
     "hds_rope": "ii" + "pppp" + "l" + "iii" + "l" + "ii" + "f" + "s",
     "hds_glu_fwd": "iipplis",
     "hds_glu_bwd": "iippplis",
+    "hds_glu_fwd_t": "i" + "ppp" + "ii" + "s",
+    "hds_glu_bwd_t": "i" + "pppp" + "ii" + "s",
     "hds_bias_act_fwd": "iippplis",
     "hds_bias_act_bwd": "iipppplis",
     "hds_adam_flat": "ii" + "ppppp" + "l" + "f" * 7 + "i" + "f" + "pp" + "s",

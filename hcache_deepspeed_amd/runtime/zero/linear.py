@@ -109,7 +109,12 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias=None):
-        ctx.save_for_backward(x)
+        # a producer that also wrote x's transpose ([K, tokens], ops/activations.glu transposed=True) lets the
+        # weight gradient run hipBLASLt's NT form without transposing x in the backward: save that copy, not x
+        xt = getattr(x, "_hds_t", None)
+        ctx.x_t = (xt is not None and xt.dim() == 2 and xt.shape[0] == x.shape[-1] and xt.dtype == x.dtype
+                   and xt.shape[1] * xt.shape[0] == x.numel())
+        ctx.save_for_backward(xt if ctx.x_t else x)
         ctx.weight = weight
         ctx.has_bias = bias is not None
         return _linear_fwd(x, weight, bias)
@@ -117,6 +122,12 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (x, ) = ctx.saved_tensors
+        xt = None
+        if ctx.x_t:
+            xt, x = x, None
+        dyt = getattr(dy, "_hds_t", None)  # the output gradient's transpose, when its producer wrote one
+        if dyt is not None and (dyt.dim() != 2 or dyt.shape[0] != dy.shape[-1] or dyt.dtype != dy.dtype):
+            dyt = None
         w = ctx.weight
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -127,14 +138,15 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
                 dx = dy.matmul(w.to(dy.dtype))
         if ctx.needs_input_grad[1]:
             dy2 = dy.reshape(-1, dy.shape[-1])
-            x2 = x.reshape(-1, x.shape[-1]).to(dy.dtype)
+            x2 = x.reshape(-1, x.shape[-1]).to(dy.dtype) if x is not None else None
+            xt2 = xt.to(dy.dtype) if xt is not None else None
 
             def gemm(out, accumulate):
                 from ...ops.gemm import wgrad
-                wgrad(dy2, x2, out, accumulate)
+                wgrad(dy2, x2, out, accumulate, dyt=dyt, xt=xt2)
 
             if not write_weight_grad(w, gemm):
-                dw = dy2.t().matmul(x2)
+                dw = dy2.t().matmul(x2) if x2 is not None else dy2.t().matmul(xt2.t())
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0)
         return dx, dw, db

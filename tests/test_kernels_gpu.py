@@ -95,10 +95,10 @@ def test_rope_inplace_and_inverse(interleaved):
     assert _rel(x, ref) < 2e-2
 
 
+@pytest.mark.parametrize("T,I", [(333, 1024), (7, 8), (3, 24), (130, 2056)])
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh", "relu"])
-def test_glu(act):
+def test_glu(act, T, I):
     from hcache_deepspeed_amd.ops.activations import glu, _ref_act, act_code
-    T, I = 333, 1024
     gu = torch.randn(T, 2 * I, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     y = glu(gu, act)
     gr = gu.detach().float().requires_grad_(True)

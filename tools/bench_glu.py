@@ -35,6 +35,11 @@ def main():
     dt = native.dt(gu)
     fwd = timeit(lambda: lib.hds_glu_fwd(dt, 0, gu.data_ptr(), y.data_ptr(), T, I, st))
     bwd = timeit(lambda: lib.hds_glu_bwd(dt, 0, dy.data_ptr(), gu.data_ptr(), dgu.data_ptr(), T, I, st))
+    yt = torch.empty(I, T, device="cuda", dtype=torch.bfloat16)
+    dgut = torch.empty(2 * I, T, device="cuda", dtype=torch.bfloat16)
+    fwd_t = timeit(lambda: lib.hds_glu_fwd_t(0, gu.data_ptr(), y.data_ptr(), yt.data_ptr(), T, I, st))
+    bwd_t = timeit(lambda: lib.hds_glu_bwd_t(0, dy.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dgut.data_ptr(), T, I,
+                                             st))
     # numerics vs fp32 torch
     g, u = gu.float().chunk(2, -1)
     ref = torch.nn.functional.silu(g) * u
@@ -45,6 +50,9 @@ def main():
     el = T * I * 2
     print(json.dumps({"T": T, "I": I, "glu_fwd_us": round(fwd, 1), "glu_fwd_TBps": round(3 * el / fwd / 1e6, 2),
                       "glu_bwd_us": round(bwd, 1), "glu_bwd_TBps": round(5 * el / bwd / 1e6, 2),
+                      "glu_fwd_t_us": round(fwd_t, 1), "glu_fwd_t_TBps": round(4 * el / fwd_t / 1e6, 2),
+                      "glu_bwd_t_us": round(bwd_t, 1), "glu_bwd_t_TBps": round(7 * el / bwd_t / 1e6, 2),
+                      "variant": os.environ.get("HDS_GLU_VAR", "2"),
                       "rel_err_fwd": err_f, "rel_err_bwd_dgate": err_b}))
 
 

@@ -15,7 +15,7 @@ GLUE = ("transpose", "FillFunctor", "copyBuffer", "copy_kernel", "CUDAFunctor_ad
 
 
 def short(n):
-    n = n.split("(")[0]
+    n = n.replace("(anonymous namespace)::", "").split("(")[0]
     return n[:60]
 
 
