@@ -32,6 +32,8 @@ HOST_LIB = os.path.join(LIB_DIR, "libhds_host.so")
 
 HIPCC_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=fast",
                "-fno-gpu-rdc", "-Wno-unused-result"]
+# per-source extra flags (part of the content hash)
+FILE_FLAGS = {}
 HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include",
               "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
@@ -65,34 +67,40 @@ def _stamp_ok(lib, digest):
     return os.path.exists(lib) and os.path.exists(st) and open(st).read().strip() == digest
 
 
-def build_kernels(force=False, jobs=None, verbose=False):
+def build_kernels(force=False, jobs=None, verbose=False, file_flags=None, out=None):
+    """``file_flags`` / ``out``: an A/B build with different per-source flags into another path (loaded with
+    HDS_KERNEL_LIB=<out>); the default build uses FILE_FLAGS into _lib/libhds_kernels.so."""
+    file_flags = FILE_FLAGS if file_flags is None else file_flags
+    lib_path = out or KERNEL_LIB
     srcs = _sources("kernels", (".hip",))
     hdrs = _sources("kernels", (".h",))
-    digest = _digest(srcs + hdrs, HIPCC_FLAGS)
-    if not force and _stamp_ok(KERNEL_LIB, digest):
-        return KERNEL_LIB
-    os.makedirs(BUILD_DIR, exist_ok=True)
-    os.makedirs(LIB_DIR, exist_ok=True)
+    digest = _digest(srcs + hdrs, HIPCC_FLAGS + sorted(f"{k}:{' '.join(v)}" for k, v in file_flags.items()))
+    if not force and _stamp_ok(lib_path, digest):
+        return lib_path
+    bdir = BUILD_DIR if out is None else BUILD_DIR + "_ab"
+    os.makedirs(bdir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     objs = []
 
     def one(src):
-        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
-        _run([hipcc, *HIPCC_FLAGS, "-I", os.path.join(CSRC, "kernels"), "-c", src, "-o", obj])
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")
+        extra = file_flags.get(os.path.basename(src), [])
+        _run([hipcc, *HIPCC_FLAGS, *extra, "-I", os.path.join(CSRC, "kernels"), "-c", src, "-o", obj])
         return obj
 
     jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))
     with _cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(one, srcs))
-    tmp = KERNEL_LIB + ".tmp"
+    tmp = lib_path + ".tmp"
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
           f"-Wl,-rpath,{ROCM}/lib"])
-    os.replace(tmp, KERNEL_LIB)
-    with open(KERNEL_LIB + ".sha256", "w") as f:
+    os.replace(tmp, lib_path)
+    with open(lib_path + ".sha256", "w") as f:
         f.write(digest)
     if verbose:
-        print(f"[hds build] {KERNEL_LIB} ({len(srcs)} kernel sources)", file=sys.stderr)
-    return KERNEL_LIB
+        print(f"[hds build] {lib_path} ({len(srcs)} kernel sources)", file=sys.stderr)
+    return lib_path
 
 
 def build_host(force=False, verbose=False):

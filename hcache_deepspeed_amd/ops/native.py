@@ -136,8 +136,8 @@ def load_kernels(build_if_missing=True):
     with _lock:
         if _klib is not None:
             return _klib
-        path = _build.KERNEL_LIB
-        if build_if_missing and os.environ.get("HDS_NO_BUILD", "0") != "1":
+        path = os.environ.get("HDS_KERNEL_LIB") or _build.KERNEL_LIB  # override: an A/B build (ops/build.py)
+        if build_if_missing and os.environ.get("HDS_NO_BUILD", "0") != "1" and not os.environ.get("HDS_KERNEL_LIB"):
             try:
                 path = _build.build_kernels()
             except Exception:
