@@ -949,6 +949,27 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(AttnParams p) {
   }
 }
 
+// PIPE >= 2 (head_dim 128, 8 waves): a FULL 64-row tile's LDS-DMA from a wave-uniform tile base plus per-lane 32-bit
+// byte offsets computed once per kernel (row 4n + lane/16 of piece n = 2w + i, swizzled 16-B chunk) -- the generic
+// stage_tile_d recomputes a clamped 64-bit row address per lane and piece on every tile (~2 VALU per MFMA of the
+// backward loops). Partial tiles (the sequence end) keep the clamped path.
+__device__ __forceinline__ void dma_offs8(int64_t stride, int32_t (&off)[2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 4 * (2 * w + i) + (lane >> 4);
+    const int ch = (lane & 15) ^ swz(row);
+    off[i] = (int32_t)(((int64_t)row * stride + 8 * ch) * 2);
+  }
+}
+__device__ __forceinline__ void stage_full8(char* tile, const bf16* tile_base, const int32_t (&off)[2]) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    __builtin_amdgcn_global_load_lds((gbl_void*)((const char*)tile_base + off[i]), (lds_void*)(tile + (2 * w + i) * 1024),
+                                     16, 0, 0);
+}
+
 // =====================================================================================
 // backward dK/dV, 8 waves, K/V resident in LDS (2 waves per SIMD)
 // =====================================================================================
@@ -1026,9 +1047,26 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
   const int nqt = qt_end - qt_begin;
   const int total = nqt * G;
 
+  int32_t oq[2] = {0, 0}, odo[2] = {0, 0};
+  if constexpr (PIPE >= 2 && D == 128) {
+    dma_offs8(p.sq, oq);
+    dma_offs8(p.sdo, odo);
+  }
   auto stage = [&](int it, int buf) {
     const int g = it / nqt, qt = qt_begin + it % nqt;
     const int hq = hk * G + g;
+    if constexpr (PIPE >= 2 && D == 128) {
+      if (qt * BN + BN <= len && p.sq < (1 << 24) && p.sdo < (1 << 24)) {  // 32-bit lane offsets
+        const int64_t r0 = start + qt * BN;
+        stage_full8(Qbase + buf * 16384, p.q + r0 * p.sq + (int64_t)hq * D, oq);
+        stage_full8(Obase + buf * 16384, p.dout + r0 * p.sdo + (int64_t)hq * D, odo);
+        if (w < 2) {
+          const float* src = (w == 0 ? p.lse : p.delta) + (int64_t)hq * p.total_tokens + r0 + lane;
+          __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(LDbase + buf * 64 + w * 128), 4, 0, 0);
+        }
+        return;
+      }
+    }
     stage_tile_d<8, D>(Qbase + buf * 16384, [=](int row) {
       int r = qt * BN + row;
       r = r < len ? r : len - 1;
@@ -1067,7 +1105,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_split_kernel(AttnParams p) 
     if (!skip) {
       const bool need_mask = (p.causal && q0 < kw0 + 31) || p.window > 0 || q0 + 32 > len || kw0 + 32 > len;
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
-      if constexpr (PIPE != 0 && D == 128) {
+      if constexpr (PIPE != 0 && D == 128) {  // (PIPE 2: same loop, fast staging above)
         bf16x8 fa[3], fb[3];
         // O tile = Q tile + 2 slots, V = K + 2 slots: immediates on one base register each
         const uint32_t bq = (uint32_t)(uintptr_t)Qt + pq, bk = (uint32_t)(uintptr_t)Kw + pk;
@@ -1276,6 +1314,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
   uint32_t ty0, ty1;
   tr_lane_offs(ty0, ty1);
 
+  int32_t okk[2] = {0, 0}, ovv[2] = {0, 0};
+  if constexpr (PIPE >= 2 && D == 128 && NW == 8) {
+    dma_offs8(p.sk, okk);
+    dma_offs8(p.sv, ovv);
+  }
   stage_tile_d<NW, D>(smem + 0, kptr(kt_begin));
   stage_tile_d<NW, D>(smem + 2 * TL, vptr(kt_begin));
   __syncthreads();
@@ -1287,8 +1330,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(AttnParams p) {
     const char* Kt = smem + buf * TL;
     const char* Vt = smem + 2 * TL + buf * TL;
     if (kt + 1 < kt_end) {
-      stage_tile_d<NW, D>(smem + (buf ^ 1) * TL, kptr(kt + 1));
-      stage_tile_d<NW, D>(smem + 2 * TL + (buf ^ 1) * TL, vptr(kt + 1));
+      if (PIPE >= 2 && D == 128 && NW == 8 && (kt + 1) * BN + BN <= len && p.sk < (1 << 24) && p.sv < (1 << 24)) {
+        const int64_t r0 = start + (kt + 1) * BN;
+        stage_full8(smem + (buf ^ 1) * TL, p.k + r0 * p.sk + (int64_t)hk * D, okk);
+        stage_full8(smem + 2 * TL + (buf ^ 1) * TL, p.v + r0 * p.sv + (int64_t)hk * D, ovv);
+      } else {
+        stage_tile_d<NW, D>(smem + (buf ^ 1) * TL, kptr(kt + 1));
+        stage_tile_d<NW, D>(smem + 2 * TL + (buf ^ 1) * TL, vptr(kt + 1));
+      }
     }
     const int k0 = kt * BN;
     bool skip = (k0 >= len) || (wq_lo >= len);
@@ -1477,7 +1526,7 @@ HDS_EXPORT int hds_attn_fwd_variant(int var) {
 
 // backward: dK/dV kernel with LDS reads pipelined two MFMAs ahead (0 / 1; head_dim 128)
 HDS_EXPORT int hds_attn_bwd_pipe(int on) {
-  g_bwd_pipe = on ? 1 : 0;
+  g_bwd_pipe = on < 0 ? 0 : (on > 2 ? 2 : on);  // 2: + uniform-base LDS-DMA staging of full tiles
   return 0;
 }
 
@@ -1531,7 +1580,9 @@ int launch_bwd(const AttnParams& p, int batch, int max_len, int total_tokens, in
   if constexpr (D <= 128) {
     if (g_dkdv_nw == 8) {
       const dim3 grid((max_len + 127) / 128, hkv, batch);
-      if (g_bwd_pipe && D == 128)
+      if (g_bwd_pipe == 2 && D == 128)
+        hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 1, false, 2>), grid, dim3(512), 0, st, p);
+      else if (g_bwd_pipe && D == 128)
         hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 1, false, 1>), grid, dim3(512), 0, st, p);
       else if (g_bwd_prio)
         hipLaunchKernelGGL((attn_bwd_dkdv_split_kernel<D, 1>), grid, dim3(512), 0, st, p);
@@ -1559,7 +1610,9 @@ int launch_bwd(const AttnParams& p, int batch, int max_len, int total_tokens, in
   if constexpr (D <= 128) {
     if (g_dq_nw == 8) {
       const dim3 grid((max_len + 255) / 256, hq, batch);
-      if (g_bwd_pipe && D == 128)
+      if (g_bwd_pipe == 2 && D == 128)
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 1, false, 2>), grid, dim3(512), 0, st, p);
+      else if (g_bwd_pipe && D == 128)
         hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 1, false, 1>), grid, dim3(512), 0, st, p);
       else if (g_bwd_prio)
         hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 1>), grid, dim3(512), 0, st, p);

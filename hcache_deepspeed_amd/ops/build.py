@@ -32,8 +32,11 @@ HOST_LIB = os.path.join(LIB_DIR, "libhds_host.so")
 
 HIPCC_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=fast",
                "-fno-gpu-rdc", "-Wno-unused-result"]
-# per-source extra flags (part of the content hash)
-FILE_FLAGS = {}
+# per-source extra flags (part of the content hash). FlashAttention without SLP vectorization: hipcc otherwise packs
+# adjacent scalar f32 muls / adds of the softmax into v_pk_mul_f32 / v_pk_add_f32, which cost MORE issue cycles than
+# two scalar ops beside the MFMAs (MI355X_MICROARCH "price of one filler"): backward 4.10 -> 3.84 ms, headline
+# 24,121 -> 24,440 tok/s on the same box (profiles/r3/fa_noslp_ab_r3p.txt)
+FILE_FLAGS = {"flash_attn.hip": ["-fno-slp-vectorize"]}
 HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include",
               "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
