@@ -49,9 +49,10 @@ def main():
     ap.add_argument("--layers", type=int, default=0, help="debug only: override layer count (result is marked invalid)")
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
-    ap.add_argument("--act-cache-policy", default="budget", choices=["budget", "recompute", "all"],
+    ap.add_argument("--act-cache-policy", default="budget", choices=["budget", "recompute", "all", "ckpt_offload"],
                     help="host activation cache: spill the over-budget layers (budget), recompute them (recompute), "
-                         "or spill every eligible layer (all)")
+                         "spill every eligible layer (all), or checkpoint every block and spill its inputs "
+                         "(ckpt_offload, long context)")
     ap.add_argument("--act-cache-budget-gib", type=float, default=0.0,
                     help="host activation cache: HBM budget the planner keeps activations under (0: 92%% of HBM)")
     ap.add_argument("--host-act-cache", action="store_true",

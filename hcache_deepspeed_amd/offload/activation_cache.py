@@ -27,6 +27,11 @@ allocation; from then on only the *earliest* layers 0..k-1 are spilled, with k t
 D2H has the whole remaining forward to drain and their H2D the whole remaining backward to prefetch. A runtime
 guard still spills any tensor that would push the allocation past the budget.
 
+``policy="ckpt_offload"`` checkpoints EVERY block (``checkpoint_saved_inputs``: its differentiable inputs are saved
+through ``save_for_backward``, so the pack hook below sees them) and spills those inputs -- the residual stream, two
+[tokens, hidden] tensors per block -- with no budget: the long-context mode, where even the checkpoints exceed HBM
+(Llama-3-8B at 256k tokens: 4.3 GB per block, 137 GB for 32 blocks, against ~95 s of compute per step).
+
 ``policy="recompute"`` plans the same over-budget layers but recomputes them in backward (non-reentrant activation
 checkpointing of just those blocks) instead of spilling them: when PCIe cannot hide the spill (at 32k tokens a
 Llama-3-8B layer moves ~3.5 GB each way, ~61 ms per direction against ~27 ms to recompute its forward), selective
@@ -71,9 +76,11 @@ class _Tagged:
 class HostActivationCache:
 
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
-                 gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None, recompute=False):
+                 gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None, recompute=False,
+                 ckpt_offload=False):
         self.device = device
         self.policy_recompute = bool(recompute)
+        self.ckpt_offload = bool(ckpt_offload)
         self.recompute = set()  # blocks whose forward is checkpointed (policy "recompute")
         # D2H copy window: spilled bytes the host may have queued on the copy stream and not yet seen copied.
         # Autograd runs far ahead of the GPU on the host, and a spilled tensor's HBM is recycled only once its D2H
@@ -135,7 +142,8 @@ class HostActivationCache:
         return cls(device, min_bytes=1 << 20, min_layers_resident=cfg.min_layers_resident,
                    prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget,
                    host_budget_bytes=int(hgib * 2**30), copy_window_bytes=int(wgib * 2**30) if wgib > 0 else None,
-                   recompute=getattr(cfg, "policy", "budget") == "recompute")
+                   recompute=getattr(cfg, "policy", "budget") == "recompute",
+                   ckpt_offload=getattr(cfg, "policy", "budget") == "ckpt_offload")
 
     # ---------------------------------------------------------------------------------------
     def attach(self, model):
@@ -149,7 +157,20 @@ class HostActivationCache:
             self._attached.append(b.register_forward_pre_hook(lambda mod, args, i=i: self._enter(i)))
             if self.policy_recompute:
                 b.forward = self._recompute_wrapper(b.forward, i)
+            elif self.ckpt_offload:
+                b.forward = self._ckpt_offload_wrapper(b.forward)
         return self
+
+    @staticmethod
+    def _ckpt_offload_wrapper(fwd):
+        from ..runtime.activation_checkpointing import checkpointing as ck
+
+        def run(*args, **kwargs):
+            if torch.is_grad_enabled() and not kwargs:
+                return ck.checkpoint_saved_inputs(fwd, *args)
+            return fwd(*args, **kwargs)
+
+        return run
 
     def _recompute_wrapper(self, fwd, i):
         from ..runtime.activation_checkpointing import checkpointing as ck
@@ -326,7 +347,8 @@ class HostActivationCache:
     def stats(self):
         return {"bytes_offloaded": self.bytes_offloaded, "pinned_pool_bytes": self.pool.bytes_allocated,
                 "spilled_layers": None if self.plan is None else len(self.plan),
-                "recomputed_layers": len(self.recompute), "late_unpacks": self.late_unpacks,
+                "recomputed_layers": self.n_layers if self.ckpt_offload else len(self.recompute),
+                "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits}
 

@@ -147,8 +147,9 @@ def load_kernels(build_if_missing=True):
             return None
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         _bind(lib, _KERNEL_SIGS)
-        # FlashAttention backward with LDS reads pipelined two MFMAs ahead (csrc/kernels/flash_attn.hip PIPE)
-        lib.hds_attn_bwd_pipe(int(os.environ.get("HDS_ATTN_BWD_PIPE", "1")))
+        # FlashAttention backward with LDS reads pipelined two MFMAs ahead (csrc/kernels/flash_attn.hip PIPE; 2 = + uniform-
+        # base LDS-DMA staging of full tiles: 3.80 vs 3.85 ms, profiles/r3/fa_bwd_pipe2_r3q.txt)
+        lib.hds_attn_bwd_pipe(int(os.environ.get("HDS_ATTN_BWD_PIPE", "2")))
         # FlashAttention forward variant (csrc/kernels/flash_attn.hip hds_attn_fwd_variant; 5 = software-pipelined)
         lib.hds_attn_fwd_variant(int(os.environ.get("HDS_ATTN_FWD_VAR", "5")))
         _klib = lib

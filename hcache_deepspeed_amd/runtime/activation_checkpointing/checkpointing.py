@@ -76,6 +76,52 @@ def checkpoint(function, *args, **kwargs):
 non_reentrant_checkpoint = checkpoint
 
 
+class _SavedInputCheckpoint(torch.autograd.Function):
+    """Checkpoint whose differentiable inputs go through ``ctx.save_for_backward`` -- and therefore through any
+    enclosing ``saved_tensors_hooks``, e.g. the host activation cache, which can then spill them to host memory and
+    prefetch them for the backward (torch's non-reentrant checkpoint keeps its inputs in a closure, invisible to
+    such hooks). Reference: the reentrant ``CheckpointFunction`` with ``cpu_checkpointing``
+    (runtime/activation_checkpointing/checkpointing.py:474-486), here asynchronous via the cache's copy stream."""
+
+    @staticmethod
+    def forward(ctx, run, n_out_hint, *args):
+        ctx.run = run
+        ctx.grad_idx = [i for i, a in enumerate(args) if torch.is_tensor(a) and a.requires_grad]
+        ctx.others = [None if i in ctx.grad_idx else a for i, a in enumerate(args)]
+        ctx.save_for_backward(*[args[i] for i in ctx.grad_idx])
+        ctx.cpu_rng = torch.get_rng_state()
+        ctx.dev_rng = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
+        with torch.no_grad():
+            out = run(*args)
+        ctx.tuple_out = isinstance(out, tuple)
+        return out
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        saved = ctx.saved_tensors
+        args = list(ctx.others)
+        for i, t in zip(ctx.grad_idx, saved):
+            args[i] = t.detach().requires_grad_(True)
+        devs = [torch.cuda.current_device()] if ctx.dev_rng is not None else []
+        with torch.random.fork_rng(devices=devs):
+            torch.set_rng_state(ctx.cpu_rng)
+            if ctx.dev_rng is not None:
+                torch.cuda.set_rng_state(ctx.dev_rng)
+            with torch.enable_grad():
+                out = ctx.run(*args)
+        outs = out if ctx.tuple_out else (out, )
+        pairs = [(o, g) for o, g in zip(outs, gouts) if torch.is_tensor(o) and o.requires_grad and g is not None]
+        if pairs:
+            torch.autograd.backward([o for o, _ in pairs], [g for _, g in pairs])
+        return (None, None) + tuple(args[i].grad if i in ctx.grad_idx else None for i in range(len(args)))
+
+
+def checkpoint_saved_inputs(function, *args):
+    """Recompute ``function(*args)`` in backward; its differentiable tensor inputs are saved through
+    ``save_for_backward`` (host-cache visible, see ``_SavedInputCheckpoint``). Positional arguments only."""
+    return _SavedInputCheckpoint.apply(function, 0, *args)
+
+
 # ---------------------------------------------------------------------------------------------
 # model-parallel RNG (reference :124-247): dropout masks identical across TP ranks for replicated
 # regions and different for partitioned regions.

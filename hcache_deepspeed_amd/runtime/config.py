@@ -168,7 +168,8 @@ class HostActCacheConfig:
     slot_mb: int = 512
     min_layers_resident: int = 2
     # "budget": spill only what exceeds gpu_budget_gib; "recompute": checkpoint those layers instead of spilling;
-    # "all": spill every eligible layer
+    # "all": spill every eligible layer; "ckpt_offload": checkpoint EVERY block and spill its inputs (the only
+    # tensors a checkpointed block keeps) -- long context, where even the checkpoints do not fit in HBM
     policy: str = "budget"
     gpu_budget_gib: float = 0.0  # 0: 92% of device memory
     prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block

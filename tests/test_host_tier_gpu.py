@@ -56,6 +56,32 @@ def test_host_activation_cache_matches_resident():
         assert rel < 2e-2, (n, rel)
 
 
+def test_ckpt_offload_policy_matches_resident():
+    """policy "ckpt_offload": every block recomputed in backward from inputs that were spilled to pinned host memory
+    and prefetched back; gradients match the resident run at bf16 resolution."""
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(num_hidden_layers=6)).cuda().to(torch.bfloat16)
+    x = torch.randint(0, 512, (2, 512), device="cuda")
+    loss = m(x, labels=x)
+    loss.backward()
+    ref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    for p in m.parameters():
+        p.grad = None
+    cache = HostActivationCache(torch.device("cuda"), min_bytes=1 << 16, min_layers_resident=1,
+                                ckpt_offload=True).attach(m)
+    with cache.forward_context():
+        loss2 = m(x, labels=x)
+    loss2.backward()
+    st = cache.stats()
+    assert st["bytes_offloaded"] > 0 and st["recomputed_layers"] == 6
+    assert torch.allclose(loss, loss2)
+    for n, p in m.named_parameters():
+        rel = ((p.grad.float() - ref[n].float()).norm() / (ref[n].float().norm() + 1e-12)).item()
+        assert rel < 2e-2, (n, rel)
+
+
 def test_engine_with_host_activation_cache():
     import hcache_deepspeed_amd as hds
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny

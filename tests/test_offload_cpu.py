@@ -267,3 +267,56 @@ def test_recompute_policy_wraps_planned_blocks():
     torch.testing.assert_close(out, ref)
     for p, g in zip(model.parameters(), gref):
         torch.testing.assert_close(p.grad, g)
+
+
+def test_ckpt_offload_policy_checkpoints_every_block_with_hook_visible_inputs():
+    """policy "ckpt_offload": every block is recomputed in backward (same outputs / gradients), and the only tensors
+    a block saves are its differentiable INPUTS, passed through save_for_backward -- so an enclosing
+    saved_tensors_hooks (the cache's pack hook) sees exactly one input per block."""
+    import torch.nn as nn
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    torch.manual_seed(0)
+
+    class Block(nn.Module):
+
+        def __init__(self):
+            super().__init__()
+            self.f = nn.Sequential(nn.Linear(16, 32), nn.GELU(), nn.Dropout(0.3), nn.Linear(32, 16))
+
+        def forward(self, x, scale):
+            return x + scale * self.f(x)
+
+    model = nn.Module()
+    model.blocks = nn.ModuleList([Block() for _ in range(4)])
+
+    def run(m, x):
+        for b in m.blocks:
+            x = b(x, 0.5)
+        return x.square().sum()
+
+    x = torch.randn(8, 16, requires_grad=True)
+    torch.manual_seed(1)
+    ref = run(model, x)
+    ref.backward()
+    gref = [p.grad.clone() for p in model.parameters()]
+    gx = x.grad.clone()
+    for p in model.parameters():
+        p.grad = None
+    HostActivationCache(torch.device("cpu"), ckpt_offload=True).attach(model)
+    packed = []
+
+    def pack(t):
+        packed.append(tuple(t.shape))
+        return t
+
+    x2 = x.detach().requires_grad_(True)
+    torch.manual_seed(1)  # dropout masks: the recompute replays the forward's RNG state
+    with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
+        out = run(model, x2)
+    out.backward()
+    torch.testing.assert_close(out, ref)
+    torch.testing.assert_close(x2.grad, gx)
+    for p, g in zip(model.parameters(), gref):
+        torch.testing.assert_close(p.grad, g)
+    # one saved input per block + square()'s input: no internal activation of any block was saved
+    assert packed.count((8, 16)) == 5 and len(packed) == 5, packed
