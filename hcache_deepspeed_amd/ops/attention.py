@@ -101,7 +101,7 @@ def _native_fwd(q, k, v, o, lse, causal, scale, cu, B, seq_len, max_len, window,
 
 def _native_bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, cu, B, seq_len, max_len, window, seq_lens=None):
     T, Hq, D = q.shape
-    delta = torch.empty(Hq, T, device=q.device, dtype=torch.float32)
+    delta = torch.empty(2, Hq, T, device=q.device, dtype=torch.float32)  # rowsum(dO * O), lse * log2(e)
     strides = _strides8(q, k, v, o, do, dq, dk, dv)
     native.check(
         native.kernels().hds_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
