@@ -155,3 +155,28 @@ def test_split_column_forward_matches_fused_linear():
     x = torch.randn(33, 64)
     w = torch.randn(6144, 64)
     torch.testing.assert_close(_split_fwd(x, w, 4096), F.linear(x, w))
+
+
+def test_wgrad_pretransposed_and_b2_forms_cpu():
+    """ops/gemm.wgrad reference forms on CPU: pre-transposed operands (x2 None -> NT form) and the batched two-half
+    split-K path give dY^T X; the b2 heuristic picks only grids that end in a half-empty wave of 256 CUs."""
+    from hcache_deepspeed_amd.ops import gemm
+    torch.manual_seed(0)
+    dy = torch.randn(64, 24)
+    x = torch.randn(64, 16)
+    ref = dy.t() @ x
+    for lay in ("direct", "nt", "direct_b2", "nt_b2"):
+        out = torch.zeros(24, 16)
+        gemm._wgrad_run(lay, dy, x, out, False)
+        torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    out = torch.zeros(24, 16)
+    gemm._wgrad_run("nt", dy, None, out, False, dyt=dy.t().contiguous(), xt=x.t().contiguous())
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    out2 = torch.zeros(24, 16)
+    gemm.wgrad(dy, None, out2, xt=x.t().contiguous())
+    torch.testing.assert_close(out2, ref, rtol=1e-4, atol=1e-4)
+    if gemm._B2:
+        assert gemm._b2_useful(4096, 14336)       # down: 896 tiles = 3.5 waves
+        assert gemm._b2_useful(6144, 4096)        # qkv: 384 tiles = 1.5 waves
+        assert not gemm._b2_useful(28672, 4096)   # gate_up: 7 full waves
+        assert not gemm._b2_useful(4096, 4096)    # o: 1 full wave
