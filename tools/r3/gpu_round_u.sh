@@ -10,3 +10,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 python tools/r3/glue_census.py gpurun_out/ru/prof > gpurun_out/ru/glue_census.txt 2>&1
 python tools/r3/trace_step_stats.py gpurun_out/ru/prof > gpurun_out/ru/step_stats.txt 2>&1
 find gpurun_out/ru/prof -name "*kernel_trace.csv" -size +20M -delete
+B="python -u bench.py --seq 32768 --micro-batch 1 --steps 4 --warmup 4"
+timeout -k 10 500 $B --host-act-cache > gpurun_out/ru/ac32k.log 2>&1 || exit 1
+timeout -k 10 500 $B --host-act-cache --act-cache-policy recompute > gpurun_out/ru/ac32k_recompute.log 2>&1 || exit 1
+timeout -k 10 500 $B --ckpt > gpurun_out/ru/ckpt32k.log 2>&1 || exit 1
