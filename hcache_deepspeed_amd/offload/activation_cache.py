@@ -222,8 +222,8 @@ class HostActivationCache:
         for lst in self.by_layer.values():  # a forward whose backward never ran: return its host buffers
             for o in lst:
                 if o.host is not None:
+                    self.host_in_use -= PinnedPool.nbytes_of(o.host)
                     self.pool.put(o.host)
-                    self.host_in_use -= o.host.numel() * o.host.element_size()
                     o.host = None
         self.by_layer = {}
         self.layer_bytes = {}
@@ -274,7 +274,7 @@ class HostActivationCache:
             s.d2h_done.record(self.stream)
         self._d2h_q.append((s.d2h_done, nbytes))
         self.bytes_offloaded += src.numel() * src.element_size()
-        self.host_in_use += src.numel() * src.element_size()
+        self.host_in_use += PinnedPool.nbytes_of(s.host)  # the pinned bucket, not just the tensor
         self.by_layer.setdefault(s.layer, []).append(s)
         return s
 
@@ -339,8 +339,8 @@ class HostActivationCache:
         torch.cuda.current_stream().wait_event(s.h2d_done)
         out = s.dev
         s.dev = None
+        self.host_in_use -= PinnedPool.nbytes_of(s.host)
         self.pool.put(s.host)
-        self.host_in_use -= s.host.numel() * s.host.element_size()
         s.host = None
         return out
 

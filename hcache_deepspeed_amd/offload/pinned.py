@@ -119,8 +119,19 @@ class PinnedPool:
 
     @staticmethod
     def _bucket(nbytes):
-        b = 1 << max(12, (int(nbytes) - 1).bit_length())
-        return b
+        """Power-of-two buckets up to 64 MiB; above, 32 MiB granularity -- a 2.68 GB activation (Llama-3-8B block
+        input at 320k tokens) would otherwise take a 4 GiB buffer, and 60 of them overran the host's memory budget."""
+        n = int(nbytes)
+        if n > (64 << 20):
+            g = 32 << 20
+            return (n + g - 1) // g * g
+        return 1 << max(12, (n - 1).bit_length())
+
+    @staticmethod
+    def nbytes_of(t):
+        """Pinned bytes behind a tensor from ``get`` (its bucket), or its own size."""
+        buf = getattr(t, "_hds_pinned_owner", None)
+        return buf.nbytes if buf is not None else t.numel() * t.element_size()
 
     def get(self, numel, dtype):
         es = torch.tensor([], dtype=dtype).element_size()

@@ -320,3 +320,15 @@ def test_ckpt_offload_policy_checkpoints_every_block_with_hook_visible_inputs():
         torch.testing.assert_close(p.grad, g)
     # one saved input per block + square()'s input: no internal activation of any block was saved
     assert packed.count((8, 16)) == 5 and len(packed) == 5, packed
+
+
+def test_pinned_pool_buckets_bound_the_waste():
+    """Pinned pool buckets: powers of two up to 64 MiB, 32 MiB granularity above (a 2.68 GB activation must not take
+    a 4 GiB buffer: 60 of them overran the host budget at 320k tokens)."""
+    from hcache_deepspeed_amd.offload.pinned import PinnedPool
+    assert PinnedPool._bucket(1) == 4096
+    assert PinnedPool._bucket(5000) == 8192
+    assert PinnedPool._bucket(64 << 20) == 64 << 20
+    n = 327680 * 4096 * 2
+    b = PinnedPool._bucket(n)
+    assert b >= n and b - n < (32 << 20) and b % (32 << 20) == 0
