@@ -49,10 +49,12 @@ def main():
     ap.add_argument("--layers", type=int, default=0, help="debug only: override layer count (result is marked invalid)")
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
-    ap.add_argument("--act-cache-policy", default="budget", choices=["budget", "recompute", "all", "ckpt_offload"],
+    ap.add_argument("--act-cache-policy", default="budget", choices=["budget", "recompute", "all", "ckpt_offload", "auto"],
                     help="host activation cache: spill the over-budget layers (budget), recompute them (recompute), "
                          "spill every eligible layer (all), or checkpoint every block and spill its inputs "
-                         "(ckpt_offload, long context)")
+                         "(ckpt_offload, long context), or recompute then spill what PCIe can hide (auto)")
+    ap.add_argument("--act-cache-spill-overlap", type=float, default=0.5,
+                    help="host activation cache policy auto: fraction of the forward the spilled blocks' D2H may take")
     ap.add_argument("--act-cache-budget-gib", type=float, default=0.0,
                     help="host activation cache: HBM budget the planner keeps activations under (0: 92%% of HBM)")
     ap.add_argument("--host-act-cache", action="store_true",
@@ -132,6 +134,7 @@ def main():
         "gradient_clipping": 1.0,
         "zero_optimization": {"stage": args.zero},
         "mi355x": {"zero3_prefetch_depth": args.prefetch, "comm_stats": world > 1, "host_act_cache": {"enabled": bool(args.host_act_cache), "policy": args.act_cache_policy,
+                                                                        "spill_overlap": args.act_cache_spill_overlap,
                                                                         "gpu_budget_gib": args.act_cache_budget_gib}},
         "steps_per_print": 1000000,
     }

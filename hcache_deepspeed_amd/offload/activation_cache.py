@@ -32,6 +32,11 @@ through ``save_for_backward``, so the pack hook below sees them) and spills thos
 [tokens, hidden] tensors per block -- with no budget: the long-context mode, where even the checkpoints exceed HBM
 (Llama-3-8B at 256k tokens: 4.3 GB per block, 137 GB for 32 blocks, against ~95 s of compute per step).
 
+``policy="auto"`` (spill + recompute): starts as ``recompute``; after the first planned step it moves the EARLIEST
+planned blocks to spilling, as many as the copy stream can drain inside a fraction ``spill_overlap`` of the forward:
+k = spill_overlap * t_forward / (block bytes / PCIe rate), with the PCIe rate measured on the calibration step's
+copies and t_forward on the first planned step. Those blocks then cost no recompute, the rest are recomputed.
+
 ``policy="recompute"`` plans the same over-budget layers but recomputes them in backward (non-reentrant activation
 checkpointing of just those blocks) instead of spilling them: when PCIe cannot hide the spill (at 32k tokens a
 Llama-3-8B layer moves ~3.5 GB each way, ~61 ms per direction against ~27 ms to recompute its forward), selective
@@ -77,10 +82,16 @@ class HostActivationCache:
 
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
                  gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None, recompute=False,
-                 ckpt_offload=False):
+                 ckpt_offload=False, hybrid=False, spill_overlap=0.5):
         self.device = device
-        self.policy_recompute = bool(recompute)
+        self.hybrid = bool(hybrid)  # policy "auto": recompute plan, then the earliest blocks switch to spilling
+        self.policy_recompute = bool(recompute) or self.hybrid
         self.ckpt_offload = bool(ckpt_offload)
+        self.spill_overlap = float(spill_overlap)
+        self._hybrid_state = 0  # 0: not planned, 1: first planned step running (timed), 2: split done
+        self._fwd_ev = None  # (start, end) timing events of the last forward
+        self._cal_copy = [None, None, 0]  # calibration copies: first-start event, last-end event, bytes
+        self.pcie_gbps = None
         self.recompute = set()  # blocks whose forward is checkpointed (policy "recompute")
         # D2H copy window: spilled bytes the host may have queued on the copy stream and not yet seen copied.
         # Autograd runs far ahead of the GPU on the host, and a spilled tensor's HBM is recycled only once its D2H
@@ -130,7 +141,7 @@ class HostActivationCache:
     @classmethod
     def from_config(cls, cfg, device):
         budget = None
-        if getattr(cfg, "policy", "budget") in ("budget", "recompute") and device.type == "cuda":
+        if getattr(cfg, "policy", "budget") in ("budget", "recompute", "auto") and device.type == "cuda":
             gib = float(getattr(cfg, "gpu_budget_gib", 0.0) or 0.0)
             total = torch.cuda.get_device_properties(device).total_memory
             budget = int(gib * 2**30) if gib > 0 else int(0.92 * total)
@@ -143,7 +154,9 @@ class HostActivationCache:
                    prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget,
                    host_budget_bytes=int(hgib * 2**30), copy_window_bytes=int(wgib * 2**30) if wgib > 0 else None,
                    recompute=getattr(cfg, "policy", "budget") == "recompute",
-                   ckpt_offload=getattr(cfg, "policy", "budget") == "ckpt_offload")
+                   ckpt_offload=getattr(cfg, "policy", "budget") == "ckpt_offload",
+                   hybrid=getattr(cfg, "policy", "budget") == "auto",
+                   spill_overlap=float(getattr(cfg, "spill_overlap", 0.5)))
 
     # ---------------------------------------------------------------------------------------
     def attach(self, model):
@@ -199,11 +212,16 @@ class HostActivationCache:
                 self._cal_bytes = dict(self.layer_bytes)
                 if self.policy_recompute:  # the same over-budget layers, recomputed instead of spilled
                     self.recompute, self.plan = set(self.plan), set()
+                    if self.hybrid:
+                        self._hybrid_state = 1
+                        self._measure_pcie()
                 log_dist(f"host activation cache: spilling {len(self.plan)} of {self.n_layers} layers (peak when spilling all {peak / 2**30:.1f} GiB, budget "
                          f"{self.budget / 2**30:.1f} GiB, {self._capped_this_step / 2**30:.1f} GiB kept by the host cap)",
                          ranks=[0])
             elif self.plan is None:
                 self._calibrating = True
+            elif self.hybrid and self._hybrid_state == 1 and self._fwd_ev is not None:
+                self._hybrid_split()
             elif self._turn_peak is not None:
                 cur = self.recompute if self.policy_recompute else self.plan
                 new = refine_plan(cur, self._cal_bytes, self._turn_peak, self.budget)
@@ -228,11 +246,46 @@ class HostActivationCache:
         self.by_layer = {}
         self.layer_bytes = {}
         self._capped_this_step = 0
+        timed = self.hybrid and self._hybrid_state == 1 and self.device.type == "cuda"
+        if timed:
+            self._fwd_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self._fwd_ev[0].record()
         with torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack):
             yield
+        if timed:
+            self._fwd_ev[1].record()
         if self.device.type == "cuda" and self._turn_peak is None:
             # end of the forward: every saved activation is alive -- the turn-around peak the plan refinement uses
             self._turn_peak = torch.cuda.max_memory_allocated(self.device)
+
+    def _measure_pcie(self):
+        t0, t1, nbytes = self._cal_copy
+        if t0 is not None and t1 is not None and nbytes > 0:
+            t1.synchronize()
+            ms = t0.elapsed_time(t1)
+            if ms > 0:
+                self.pcie_gbps = nbytes / ms / 1e6
+        self._cal_copy = [None, None, 0]
+
+    def _hybrid_split(self):
+        """Policy "auto": move the earliest recomputed blocks to spilling -- as many as the copy stream drains within
+        ``spill_overlap`` of the measured forward time (see module docstring)."""
+        self._hybrid_state = 2
+        s, e = self._fwd_ev
+        e.synchronize()
+        t_fwd_s = s.elapsed_time(e) / 1e3
+        self._fwd_ev = None
+        rec = sorted(self.recompute)
+        if not rec or not self.pcie_gbps:
+            return
+        per = sum(self._cal_bytes.get(i, 0) for i in rec) / len(rec)
+        t_copy = per / (self.pcie_gbps * 1e9)
+        k = min(len(rec), int(self.spill_overlap * t_fwd_s / max(t_copy, 1e-9)))
+        self.plan = set(rec[:k])
+        self.recompute = set(rec[k:])
+        log_dist(f"host activation cache (auto): forward {t_fwd_s * 1e3:.0f} ms, PCIe {self.pcie_gbps:.1f} GB/s, "
+                 f"{per / 2**30:.2f} GiB per block -> spilling {k} and recomputing {len(rec) - k} of {len(rec)} "
+                 f"over-budget blocks", ranks=[0])
 
     # ---------------------------------------------------------------------------------------
     def _window(self, q, nbytes):
@@ -266,12 +319,20 @@ class HostActivationCache:
         s.host = self.pool.get(src.numel(), src.dtype)
         ev = torch.cuda.Event()
         ev.record()
+        cal = self.hybrid and self._calibrating
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ev)
+            if cal and self._cal_copy[0] is None:  # PCIe rate of the calibration step's (saturating) copies
+                self._cal_copy[0] = torch.cuda.Event(enable_timing=True)
+                self._cal_copy[0].record(self.stream)
             s.host.copy_(src.view(-1), non_blocking=True)
             src.record_stream(self.stream)
             s.d2h_done = torch.cuda.Event()
             s.d2h_done.record(self.stream)
+            if cal:
+                self._cal_copy[1] = torch.cuda.Event(enable_timing=True)
+                self._cal_copy[1].record(self.stream)
+                self._cal_copy[2] += nbytes
         self._d2h_q.append((s.d2h_done, nbytes))
         self.bytes_offloaded += src.numel() * src.element_size()
         self.host_in_use += PinnedPool.nbytes_of(s.host)  # the pinned bucket, not just the tensor
@@ -348,6 +409,7 @@ class HostActivationCache:
         return {"bytes_offloaded": self.bytes_offloaded, "pinned_pool_bytes": self.pool.bytes_allocated,
                 "spilled_layers": None if self.plan is None else len(self.plan),
                 "recomputed_layers": self.n_layers if self.ckpt_offload else len(self.recompute),
+                "pcie_gbps": None if self.pcie_gbps is None else round(self.pcie_gbps, 1),
                 "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits}

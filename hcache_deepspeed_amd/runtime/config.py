@@ -169,8 +169,10 @@ class HostActCacheConfig:
     min_layers_resident: int = 2
     # "budget": spill only what exceeds gpu_budget_gib; "recompute": checkpoint those layers instead of spilling;
     # "all": spill every eligible layer; "ckpt_offload": checkpoint EVERY block and spill its inputs (the only
-    # tensors a checkpointed block keeps) -- long context, where even the checkpoints do not fit in HBM
+    # tensors a checkpointed block keeps) -- long context, where even the checkpoints do not fit in HBM; "auto":
+    # "recompute", then the earliest planned blocks switch to spilling as far as PCIe can hide them
     policy: str = "budget"
+    spill_overlap: float = 0.5  # policy "auto": fraction of the forward the spilled blocks' D2H may take
     gpu_budget_gib: float = 0.0  # 0: 92% of device memory
     prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block
     host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: min(40% of host RAM, 160 GiB))

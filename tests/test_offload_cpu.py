@@ -332,3 +332,30 @@ def test_pinned_pool_buckets_bound_the_waste():
     n = 327680 * 4096 * 2
     b = PinnedPool._bucket(n)
     assert b >= n and b - n < (32 << 20) and b % (32 << 20) == 0
+
+
+def test_auto_policy_splits_recompute_plan_by_pcie_budget():
+    """policy "auto": after the first planned (all-recompute) step, the earliest blocks whose D2H fits in
+    spill_overlap of the forward move to spilling, the rest stay recomputed."""
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+
+    class Ev:
+        def __init__(self, ms=0.0):
+            self.ms = ms
+
+        def synchronize(self):
+            pass
+
+        def elapsed_time(self, other):
+            return other.ms - self.ms
+
+    c = HostActivationCache(torch.device("cpu"), hybrid=True, spill_overlap=0.5)
+    assert c.policy_recompute and c.hybrid
+    G = 1 << 30
+    c._cal_bytes = {i: 3 * G for i in range(32)}
+    c.recompute = set(range(10))
+    c.pcie_gbps = 50.0                    # a 3 GiB block takes ~64 ms
+    c._fwd_ev = (Ev(0.0), Ev(900.0))      # 900 ms forward -> 450 ms of copies -> 6 blocks
+    c._hybrid_state = 1
+    c._hybrid_split()
+    assert c.plan == set(range(6)) and c.recompute == set(range(6, 10)) and c._hybrid_state == 2
