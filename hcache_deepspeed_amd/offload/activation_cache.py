@@ -418,13 +418,17 @@ class HostActivationCache:
 def refine_plan(plan, layer_bytes, turn_peak, budget, margin=1 << 30):
     """Closed-loop correction of a spill plan (a prefix {0..k-1}) from the turn-around peak of a step that ran it:
     the latest spilled layers whose bytes fit in ``budget - margin - turn_peak`` stay resident from now on; a peak
-    over the budget spills the next layer as well."""
+    over the budget spills the following layers whose bytes cover the excess."""
     spilled = sorted(plan)
     slack = budget - margin - turn_peak
-    if slack < 0:
+    if slack < 0:  # over budget: add the following layers until their bytes cover the excess (one step, not one
+        # layer per step -- a plan refined from a low all-offloaded peak would otherwise creep back over many steps)
         nxt = (spilled[-1] + 1) if spilled else min(layer_bytes, default=None)
-        if nxt is not None and nxt in layer_bytes:
-            return set(spilled) | {nxt}
+        need = -slack
+        while need > 0 and nxt is not None and nxt in layer_bytes:
+            spilled.append(nxt)
+            need -= layer_bytes[nxt]
+            nxt += 1
         return set(spilled)
     while spilled and layer_bytes.get(spilled[-1], 0) <= slack:
         slack -= layer_bytes.get(spilled[-1], 0)

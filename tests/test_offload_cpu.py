@@ -224,6 +224,8 @@ def test_refine_plan_closed_loop():
     assert refine_plan({0, 1, 2}, lb, turn_peak=100, budget=95 + G) == {0, 1, 2, 3}      # over budget
     assert refine_plan(set(), lb, turn_peak=100, budget=95 + G) == {0}
     assert refine_plan({0, 1}, lb, turn_peak=0, budget=1000 + G) == set()
+    assert refine_plan({0}, lb, turn_peak=100, budget=75 + G) == {0, 1, 2, 3}            # 25 B over: 3 more layers
+    assert refine_plan({5, 6}, lb, turn_peak=100, budget=85 + G) == {5, 6, 7}            # runs out of layers
 
 
 def test_recompute_policy_wraps_planned_blocks():
