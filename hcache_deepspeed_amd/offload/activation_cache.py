@@ -51,6 +51,7 @@ Two corrections keep the budgeted cache off the critical path:
   backward of the resident layers instead of bunching up at the end of the step.
 """
 import contextlib
+import functools
 import os
 import sys
 import time
@@ -179,9 +180,13 @@ class HostActivationCache:
         from ..runtime.activation_checkpointing import checkpointing as ck
 
         def run(*args, **kwargs):
-            if torch.is_grad_enabled() and not kwargs:
-                return ck.checkpoint_saved_inputs(fwd, *args)
-            return fwd(*args, **kwargs)
+            if not torch.is_grad_enabled():
+                return fwd(*args, **kwargs)
+            if any(torch.is_tensor(v) and v.requires_grad for v in kwargs.values()):
+                return ck.checkpoint(fwd, *args, **kwargs)  # still recomputed; such inputs stay on the device
+            if kwargs:
+                return ck.checkpoint_saved_inputs(functools.partial(fwd, **kwargs), *args)
+            return ck.checkpoint_saved_inputs(fwd, *args)
 
         return run
 
