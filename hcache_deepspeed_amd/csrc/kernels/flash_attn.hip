@@ -523,7 +523,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
-template <int D, bool FASTDMA = true>
+// SKIPW (variant 7): a wave whose queries all lie below a causal key tile skips that tile's math -- and every later
+// one, which is masked too -- keeping only the workgroup's DMA staging and barrier (waves 0-5 of the last 1-3 tiles).
+template <int D, bool FASTDMA = true, bool SKIPW = false>
 __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   constexpr int NW = 8, BM = 32 * NW;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
@@ -641,6 +643,7 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
     }
   }
 
+  const int skip_from = (SKIPW && p.causal && p.window <= 0) ? wq_hi / BN + 1 : 0x7fffffff;
   auto tile = [&](auto BUFC, int kt) {
     constexpr int buf = decltype(BUFC)::value;
     constexpr int KN = (buf ^ 1) * TL;          // K_{kt+1}
@@ -649,6 +652,7 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
     __syncthreads();                                   // ... of every wave; V_{kt-1} and K_kt are free
     if (kt + 1 < kt_end) stage(smem + 2 * TL + (buf ^ 1) * TL, p.v, p.sv, dv, kt + 1);
     if (kt + 2 < kt_end) stage(smem + buf * TL, p.k, p.sk, dk, kt + 2);
+    if (SKIPW && kt >= skip_from) return;  // wave-uniform
 
     const int k0 = kt * BN;
     const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
@@ -1524,9 +1528,10 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_bwd_pipe = 0;
 
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
-// 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel)
+// 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel);
+// 6 = 5 without the full-tile DMA fast path; 7 = 5 + per-wave skip of the causal tiles above its queries
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 6) return hipErrorInvalidValue;
+  if (var < 0 || var > 7) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1563,6 +1568,7 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
           case 4: hipLaunchKernelGGL((attn_fwd_stg_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 5: hipLaunchKernelGGL((attn_fwd_sp_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 6: hipLaunchKernelGGL((attn_fwd_sp_kernel<D, false>), grid, dim3(512), 0, st, p); break;
+          case 7: hipLaunchKernelGGL((attn_fwd_sp_kernel<D, true, true>), grid, dim3(512), 0, st, p); break;
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;
