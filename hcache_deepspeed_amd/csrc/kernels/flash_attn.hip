@@ -525,9 +525,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // SKIPW (variant 7): a wave whose queries all lie below a causal key tile skips that tile's math -- and every later
 // one, which is masked too -- keeping only the workgroup's DMA staging and barrier (waves 0-5 of the last 1-3 tiles).
-template <int D, bool FASTDMA = true, bool SKIPW = false>
-__global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
-  constexpr int NW = 8, BM = 32 * NW;
+// NW4 (variant 8): 4 waves / 128 queries per workgroup, two workgroups per CU (64 KiB of LDS each, one wave per SIMD
+// each) -- their barriers are independent, so one workgroup's MFMA phase can run beside the other's wait.
+template <int D, bool FASTDMA = true, bool SKIPW = false, int NW = 8>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_sp_kernel(AttnParams p) {
+  constexpr int BM = 32 * NW, PW = 16 / NW;  // PW: 1-KiB tile pieces each wave stages
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
   static_assert(D == 128, "software-pipelined forward: head_dim 128");
   __shared__ __attribute__((aligned(16))) char smem[4 * TL];  // K[2], V[2]
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   const float c = p.scale * kLog2e;
   int klo, khi;
   key_span(p, myq, len, klo, khi);
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half (guide T5)
+  if (NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half (T5)
 
   bf16x8 qf[KS];
   {
@@ -573,10 +575,10 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
     };
   };
   // LDS-DMA of a full tile: uniform tile base + per-lane byte offset (row 4n + lane/16, swizzled 16-B chunk)
-  int32_t dk[2], dv[2];
+  int32_t dk[PW], dv[PW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 4 * (w * 2 + i) + (lane >> 4);
+  for (int i = 0; i < PW; ++i) {
+    const int row = 4 * (w * PW + i) + (lane >> 4);
     const int ch = (lane & 15) ^ swz(row);
     dk[i] = (int32_t)(((int64_t)row * p.sk + 8 * ch) * 2);
     dv[i] = (int32_t)(((int64_t)row * p.sv + 8 * ch) * 2);
@@ -585,8 +587,8 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
     if (FASTDMA && kt * BN + BN <= len) {
       const char* tb = (const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_global_load_lds((gbl_void*)(tb + off[i]), (lds_void*)(dst + (w * 2 + i) * 1024), 16, 0, 0);
+      for (int i = 0; i < PW; ++i)
+        __builtin_amdgcn_global_load_lds((gbl_void*)(tb + off[i]), (lds_void*)(dst + (w * PW + i) * 1024), 16, 0, 0);
     } else {
       stage_tile_d<NW, D>(dst, rowp(base, stride, kt));
     }
@@ -617,9 +619,12 @@ __global__ __launch_bounds__(512) void attn_fwd_sp_kernel(AttnParams p) {
   stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
   if (kt_begin + 1 < kt_end) {
     stage(smem + TL, p.k, p.sk, dk, kt_begin + 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this wave's 2 K_0 DMAs (issued first) have landed
+    // this wave's PW K_0 DMAs (issued first) have landed; V_0 and K_1 (2 PW) may still be in flight
+    if constexpr (NW == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   } else {
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if constexpr (NW == 8) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
   __syncthreads();
   f32x16 sc[2];
@@ -1529,9 +1534,10 @@ int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_b
 
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
 // 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel);
-// 6 = 5 without the full-tile DMA fast path; 7 = 5 + per-wave skip of the causal tiles above its queries
+// 6 = 5 without the full-tile DMA fast path; 7 = 5 + per-wave skip of the causal tiles above its queries;
+// 8 = 5 with 4-wave workgroups (two per CU)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 7) return hipErrorInvalidValue;
+  if (var < 0 || var > 8) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1569,6 +1575,10 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
           case 5: hipLaunchKernelGGL((attn_fwd_sp_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 6: hipLaunchKernelGGL((attn_fwd_sp_kernel<D, false>), grid, dim3(512), 0, st, p); break;
           case 7: hipLaunchKernelGGL((attn_fwd_sp_kernel<D, true, true>), grid, dim3(512), 0, st, p); break;
+          case 8:
+            hipLaunchKernelGGL((attn_fwd_sp_kernel<D, true, false, 4>), dim3((max_len + 127) / 128, hq, batch),
+                               dim3(256), 0, st, p);
+            break;
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;
