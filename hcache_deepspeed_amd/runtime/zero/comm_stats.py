@@ -18,7 +18,26 @@ import time
 import torch
 
 
+def _completed(work):
+    """Non-blocking completion check of a c10d / event-backed work object (unknown kinds count as complete)."""
+    f = getattr(work, "is_completed", None)
+    if f is not None:
+        try:
+            return bool(f())
+        except Exception:
+            return True
+    ev = getattr(work, "ev", None)
+    if ev is not None and hasattr(ev, "query"):
+        return bool(ev.query())
+    return True
+
+
 class ZeroCommStats:
+    """Work objects are accounted and DROPPED as soon as they complete: a c10d NCCL Work keeps its output tensors
+    alive (``outputs_``), so holding every step's works until ``summary()`` would pin each freshly gathered unit
+    buffer -- 14 GB per step for Llama-3-8B -- for the whole timed region."""
+
+    MAX_PENDING = 64  # hard bound on retained works; older ones are accounted without timing
 
     def __init__(self, device):
         self.device = device
@@ -27,12 +46,40 @@ class ZeroCommStats:
 
     def reset(self):
         self._waits = []  # (ev_before, ev_after) or host seconds
-        self._works = []  # (kind, total_bytes, world, work)
+        self._works = []  # (kind, total_bytes, world, work) not yet complete
+        self._kinds = {}
         self.host_wait_s = 0.0
+
+    def _account(self, kind, nbytes, world, work, timed=True):
+        d = self._kinds.setdefault(kind, {"count": 0, "bytes": 0, "timed_ms": 0.0, "timed_bytes_bus": 0.0,
+                                          "world": world})
+        d["count"] += 1
+        d["bytes"] += nbytes
+        ms = None
+        if timed:
+            try:
+                ms = float(work._get_duration())
+            except Exception:  # timing not enabled (TORCH_NCCL_ENABLE_TIMING) or not supported by the backend
+                ms = None
+        if ms is not None and ms > 0:
+            d["timed_ms"] += ms
+            d["timed_bytes_bus"] += nbytes * (world - 1) / world
+
+    def _drain(self, all_done=False):
+        keep = []
+        for item in self._works:
+            if all_done or _completed(item[3]):
+                self._account(*item)
+            else:
+                keep.append(item)
+        while len(keep) > self.MAX_PENDING:
+            self._account(*keep.pop(0), timed=False)
+        self._works = keep
 
     def issued(self, kind, total_bytes, world, work):
         if world > 1 and work is not None:
             self._works.append((kind, int(total_bytes), int(world), work))
+            self._drain()
 
     def wait(self, work):
         if not self.cuda:
@@ -46,30 +93,24 @@ class ZeroCommStats:
         e1.record()
         self._waits.append((e0, e1))
 
+    def pending(self):
+        return len(self._works)
+
     def summary(self):
         """Call after the step's work has completed (e.g. after ``torch.cuda.synchronize()``)."""
+        self._drain(all_done=True)
         if self.cuda:
             exposed_ms = sum(a.elapsed_time(b) for a, b in self._waits)
         else:
             exposed_ms = self.host_wait_s * 1e3
         out = {"exposed_ms": round(exposed_ms, 3), "waits": len(self._waits) if self.cuda else None}
         kinds = {}
-        for kind, nbytes, world, work in self._works:
-            d = kinds.setdefault(kind, {"count": 0, "bytes": 0, "timed_ms": 0.0, "timed_bytes_bus": 0.0,
-                                        "world": world})
-            d["count"] += 1
-            d["bytes"] += nbytes
-            try:
-                ms = float(work._get_duration())
-            except Exception:  # timing not enabled (TORCH_NCCL_ENABLE_TIMING) or not supported by the backend
-                ms = None
-            if ms is not None and ms > 0:
-                d["timed_ms"] += ms
-                d["timed_bytes_bus"] += nbytes * (world - 1) / world
-        for kind, d in kinds.items():
+        for kind, d0 in self._kinds.items():
+            d = dict(d0)
             ms, bus = d.pop("timed_ms"), d.pop("timed_bytes_bus")
             d["collective_ms"] = round(ms, 3) if bus else None
             d["busbw_GBps"] = round(bus / (d["collective_ms"] * 1e-3) / 1e9, 1) if d["collective_ms"] else None
             d["mean_msg_MiB"] = round(d["bytes"] / max(1, d["count"]) / 2**20, 2)
+            kinds[kind] = d
         out["collectives"] = kinds
         return out

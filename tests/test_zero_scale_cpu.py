@@ -196,3 +196,32 @@ def test_memory_plan_bench_configs():
     inf = estimate_llama_training(llama.llama3_70b(), 2, 4096, 8, ckpt=True, offload_optimizer=True,
                                   offload_param=True)
     assert inf["fits"] and inf["host_gib"] > 100
+
+
+def test_comm_stats_drops_completed_works():
+    """ZeroCommStats must not retain c10d Work objects (an NCCL Work pins its output tensors, i.e. every gathered
+    unit buffer of the timed steps): completed works are accounted and dropped on the next issue, and the number
+    retained is bounded even if some never report completion."""
+    from hcache_deepspeed_amd.runtime.zero.comm_stats import ZeroCommStats
+
+    class W:
+
+        def __init__(self, done):
+            self.done = done
+
+        def is_completed(self):
+            return self.done
+
+        def _get_duration(self):
+            return 2.0
+
+    cs = ZeroCommStats(torch.device("cpu"))
+    for i in range(10):
+        cs.issued("all_gather", 1 << 20, 8, W(True))
+        assert cs.pending() == 0
+    for i in range(300):
+        cs.issued("reduce_scatter", 1 << 20, 8, W(False))
+    assert cs.pending() <= ZeroCommStats.MAX_PENDING
+    s = cs.summary()
+    assert s["collectives"]["all_gather"]["count"] == 10 and s["collectives"]["reduce_scatter"]["count"] == 300
+    assert s["collectives"]["all_gather"]["busbw_GBps"] > 0 and cs.pending() == 0
