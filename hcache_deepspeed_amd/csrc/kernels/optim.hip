@@ -15,6 +15,8 @@
 //   * the multi-tensor form (FusedAdam over arbitrary parameter lists) walks a device-resident
 //     chunk table instead of the reference's fixed-depth kernel-argument struct, so one launch
 //     covers any number of tensors.
+#include <cstdlib>
+
 #include "hds_common.h"
 
 using namespace hds;
@@ -42,8 +44,21 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p -= h.lr * upd;
 }
 
+// NT (variant 1): the fp32 state and the bf16 copy are written with non-temporal (streaming) stores -- every byte the
+// step writes is read again only in the next step, so allocating it in L2 only evicts the stream's read lines
+__device__ __forceinline__ void st8_nt(float* p, const float (&v)[8]) {
+  __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(p));
+  __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f32x4*>(p + 4));
+}
+__device__ __forceinline__ void st8_nt(bf16* p, const float (&v)[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = (bf16)v[i];
+  __builtin_nontemporal_store(*reinterpret_cast<u32x4*>(&r), reinterpret_cast<u32x4*>(p));
+}
+
 // p: master (PT = float or bf16), g: grad, m/v: fp32 state, lp: optional low-precision copy of p
-template <typename PT, typename GT>
+template <typename PT, typename GT, bool NT = false>
 __global__ __launch_bounds__(256) void adam_flat(PT* __restrict__ p, const GT* __restrict__ g, float* __restrict__ m,
                                                  float* __restrict__ v, bf16* __restrict__ lp, int64_t n, AdamHP h,
                                                  float gscale, const float* __restrict__ dev_scale,
@@ -59,10 +74,17 @@ __global__ __launch_bounds__(256) void adam_flat(PT* __restrict__ p, const GT* _
     Vec8<float>::load(v + i * 8, vv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) adam_elem<PT, GT>(pv[j], gv[j] * sc, mv[j], vv[j], h);
-    Vec8<PT>::store(p + i * 8, pv);
-    Vec8<float>::store(m + i * 8, mv);
-    Vec8<float>::store(v + i * 8, vv);
-    if (lp) Vec8<bf16>::store(lp + i * 8, pv);
+    if constexpr (NT) {
+      st8_nt(p + i * 8, pv);
+      st8_nt(m + i * 8, mv);
+      st8_nt(v + i * 8, vv);
+      if (lp) st8_nt(lp + i * 8, pv);
+    } else {
+      Vec8<PT>::store(p + i * 8, pv);
+      Vec8<float>::store(m + i * 8, mv);
+      Vec8<float>::store(v + i * 8, vv);
+      if (lp) Vec8<bf16>::store(lp + i * 8, pv);
+    }
   }
   // tail
   for (int64_t i = nvec * 8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -307,9 +329,19 @@ HDS_EXPORT int hds_adam_flat(int pdtype, int gdtype, void* p, const void* g, flo
                              float gscale, const float* dev_scale, const int* found_inf, hipStream_t st) {
   AdamHP h{lr, b1, b2, eps, wd, bc1, bc2, adamw};
   dim3 grid(stream_grid(n / 8 + 1, 256, 4096)), block(256);
-  PG_SWITCH(pdtype, gdtype,
-            hipLaunchKernelGGL((adam_flat<PT, GT>), grid, block, 0, st, (PT*)p, (const GT*)g, m, v, (bf16*)lp, n, h,
-                               gscale, dev_scale, found_inf));
+  static const int nt = [] {
+    const char* e = getenv("HDS_ADAM_NT");
+    return e ? atoi(e) : 0;
+  }();
+  if (nt && pdtype == kF32) {  // fp32 master: the training configuration
+    PG_SWITCH(pdtype, gdtype,
+              hipLaunchKernelGGL((adam_flat<PT, GT, true>), grid, block, 0, st, (PT*)p, (const GT*)g, m, v,
+                                 (bf16*)lp, n, h, gscale, dev_scale, found_inf));
+  } else {
+    PG_SWITCH(pdtype, gdtype,
+              hipLaunchKernelGGL((adam_flat<PT, GT>), grid, block, 0, st, (PT*)p, (const GT*)g, m, v, (bf16*)lp, n,
+                                 h, gscale, dev_scale, found_inf));
+  }
   return hipGetLastError();
 }
 
