@@ -124,6 +124,9 @@ class HostActivationCache:
         # high priority: HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues round-robin, and a copy that
         # lands in the compute stream's queue cannot start before every kernel queued ahead of it has finished
         self.stream = torch.cuda.Stream(device, priority=-1) if device.type == "cuda" else None
+        # backward prefetches get their own stream: on the D2H stream they queued behind the forward's spill backlog
+        # (up to the copy window) and the first recomputed block of a 128k ckpt_offload step waited 191 ms for them
+        self.h2d_stream = torch.cuda.Stream(device, priority=-1) if device.type == "cuda" else None
         self.cur_layer = -1
         self.n_layers = 0
         self.by_layer = {}
@@ -245,6 +248,11 @@ class HostActivationCache:
         for lst in self.by_layer.values():  # a forward whose backward never ran: return its host buffers
             for o in lst:
                 if o.host is not None:
+                    if o.h2d_done is not None and self.stream is not None:
+                        # a prefetch nobody consumed may still read the buffer on the H2D stream: the next D2H into
+                        # it (D2H stream) must come after it (consumed prefetches are ordered through the compute
+                        # stream, which waited for them)
+                        self.stream.wait_event(o.h2d_done)
                     self.host_in_use -= PinnedPool.nbytes_of(o.host)
                     self.pool.put(o.host)
                     o.host = None
@@ -354,15 +362,15 @@ class HostActivationCache:
         s.dev = torch.empty(s.shape, dtype=s.dtype, device=s.device)
         ready = torch.cuda.Event()
         ready.record(cur)
-        with torch.cuda.stream(self.stream):
-            self.stream.wait_event(s.d2h_done)
-            self.stream.wait_event(ready)
+        with torch.cuda.stream(self.h2d_stream):
+            self.h2d_stream.wait_event(s.d2h_done)  # the host copy must be complete
+            self.h2d_stream.wait_event(ready)
             s.dev.view(-1).copy_(s.host, non_blocking=True)
             # no record_stream: the buffer was allocated on the compute stream after everything that used its block
             # (`ready`), and every later user of the block is a compute-stream kernel ordered after the consumer,
             # which waits for h2d_done -- so the block may recycle as soon as the consumer is enqueued
             s.h2d_done = torch.cuda.Event()
-            s.h2d_done.record(self.stream)
+            s.h2d_done.record(self.h2d_stream)
 
     _DEBUG = os.environ.get("HDS_ACT_CACHE_DEBUG") == "1"
 
