@@ -312,9 +312,12 @@ class HostActivationCache:
 
     def _pack(self, t):
         if (not isinstance(t, torch.Tensor) or not t.is_cuda or t.is_leaf or self.cur_layer < 0
-                or self.cur_layer >= self.n_layers - self.keep
                 or t.numel() * t.element_size() < self.min_bytes):
             return t
+        if self.cur_layer >= self.n_layers - self.keep:
+            # kept resident, but tagged once something was spilled: backward touching these last blocks is what
+            # starts the prefetch of the latest spilled ones
+            return _Tagged(t, self.cur_layer) if self.by_layer else t
         nbytes = t.numel() * t.element_size()
         self.layer_bytes[self.cur_layer] = self.layer_bytes.get(self.cur_layer, 0) + nbytes
         if self.plan is not None and self.cur_layer not in self.plan:
@@ -377,7 +380,9 @@ class HostActivationCache:
     def _prefetch_before(self, layer):
         if self._turn_peak is None and self.device.type == "cuda":
             self._turn_peak = torch.cuda.max_memory_allocated(self.device)  # first unpack of the step
-        for j in range(1, self.prefetch_layers + 1):
+        # j = 0 first: the rest of THIS block's spilled tensors (a block unpacks several; if the first was late, the
+        # others must not queue behind the earlier blocks' prefetches -- a 189 ms stall at 128k ckpt_offload)
+        for j in range(0, self.prefetch_layers + 1):
             lst = self.by_layer.get(layer - j, ())
             if self._DEBUG and lst and lst[0].dev is None:
                 print(f"[act-cache] t={time.perf_counter():.3f} backward at layer {layer}: prefetch layer {layer - j} "
