@@ -356,7 +356,7 @@ class HostActivationCache:
         return s
 
     def _prefetch(self, s):
-        if s.dev is not None:
+        if s.dev is not None or s.host is None:  # already fetched, or already consumed (host buffer returned)
             return
         # Allocate on the COMPUTE stream: its caching-allocator pool holds the blocks backward just freed, while
         # an allocation on the copy stream finds an empty per-stream pool and, with HBM nearly full, makes the
