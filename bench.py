@@ -49,10 +49,13 @@ def main():
     ap.add_argument("--layers", type=int, default=0, help="debug only: override layer count (result is marked invalid)")
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
-    ap.add_argument("--act-cache-policy", default="budget", choices=["budget", "recompute", "all", "ckpt_offload", "auto"],
+    ap.add_argument("--act-cache-policy", default="budget", choices=["budget", "recompute", "all", "ckpt_offload", "auto", "plan"],
                     help="host activation cache: spill the over-budget layers (budget), recompute them (recompute), "
                          "spill every eligible layer (all), or checkpoint every block and spill its inputs "
-                         "(ckpt_offload, long context), or recompute then spill what PCIe can hide (auto)")
+                         "(ckpt_offload, long context), or recompute then spill what PCIe can hide (auto), or "
+                         "keep / spill / recompute per tensor class (plan)")
+    ap.add_argument("--act-cache-spill-cost", type=float, default=0.6,
+                    help="host activation cache policy plan: modelled cost of a hidden spill, ms per GB")
     ap.add_argument("--act-cache-spill-overlap", type=float, default=0.5,
                     help="host activation cache policy auto: fraction of the forward the spilled blocks' D2H may take")
     ap.add_argument("--act-cache-budget-gib", type=float, default=0.0,
@@ -66,6 +69,8 @@ def main():
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
     ap.add_argument("--offload-opt-states", action="store_true",
                     help="DeepCompile offload_adam_states: Adam moments + fp32 master on pinned host between steps")
+    ap.add_argument("--offload-states-ratio", type=float, default=1.0,
+                    help="with --offload-opt-states: fraction of the optimizer-state bytes to offload (largest first)")
     ap.add_argument("--offload-params-compile", type=float, default=None, metavar="BUDGET_GIB",
                     help="DeepCompile offload_parameters on the GPU-optimizer engine; the pass keeps shards on the "
                          "device within BUDGET_GIB of HBM (0: every shard on the host)")
@@ -73,6 +78,9 @@ def main():
                     help="ZeRO-3 stage3_max_reuse_distance in elements; 'auto' = every parameter at N > 1 (units stay "
                          "gathered from their forward to their backward: one all-gather per unit per step instead of "
                          "two; HBM allows it at every dp for Llama-3-8B), 0 = release after the forward")
+    ap.add_argument("--comm-timing", action="store_true",
+                    help="N>1: TORCH_NCCL_ENABLE_TIMING=1 for the whole run (in-step RCCL busbw in extra.comm; adds two "
+                         "events per collective to the timed steps too)")
     ap.add_argument("--deepcompile", action="store_true",
                     help="engine.compile() with DeepCompile: profiled ZeRO-3 gather schedule (selective gather + prefetch)")
     args = ap.parse_args()
@@ -89,8 +97,9 @@ def main():
     from hcache_deepspeed_amd.models import gpt2, llama, mixtral
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        # RCCL records start/end events per collective so the bench can report in-step AG/RS busbw (no sync)
+    if world > 1 and args.comm_timing:
+        # opt-in: RCCL records start/end events per collective (every step, timed ones included) so the instrumented
+        # step after the timed region can report in-step AG/RS busbw
         os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
     if world > 1 or "RANK" in os.environ:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -133,9 +142,10 @@ def main():
                                                    "weight_decay": 0.1}},
         "gradient_clipping": 1.0,
         "zero_optimization": {"stage": args.zero},
-        "mi355x": {"zero3_prefetch_depth": args.prefetch, "comm_stats": world > 1, "host_act_cache": {"enabled": bool(args.host_act_cache), "policy": args.act_cache_policy,
+        "mi355x": {"zero3_prefetch_depth": args.prefetch, "comm_stats": False, "host_act_cache": {"enabled": bool(args.host_act_cache), "policy": args.act_cache_policy,
                                                                         "spill_overlap": args.act_cache_spill_overlap,
-                                                                        "gpu_budget_gib": args.act_cache_budget_gib}},
+                                                                        "gpu_budget_gib": args.act_cache_budget_gib,
+                                                                        "spill_cost_ms_per_gb": args.act_cache_spill_cost}},
         "steps_per_print": 1000000,
     }
     if args.zero == 3:
@@ -168,6 +178,8 @@ def main():
     engine, _, _, _ = hds.initialize(model=model, config=ds_config)
     if dc_on:
         kw = {} if args.offload_params_compile is None else {"mem_budget_bytes": args.offload_params_compile * 2**30}
+        if args.offload_opt_states:
+            kw["offload_states_ratio"] = args.offload_states_ratio
         engine.compile(compile_kwargs=kw)  # schedule compiled after the profiled warmup step (compile/backend.py)
     t_init = time.time() - t_init
     dev = engine.device
@@ -203,9 +215,8 @@ def main():
     tdist.barrier()
     sync()
     retries0 = torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) if on_gpu else 0
-    cs = getattr(engine.optimizer, "comm_stats", None)
-    if cs is not None:
-        cs.reset()
+    zopt = engine.optimizer
+    timed_events = getattr(zopt, "comm_stats", None)  # None: the timed steps record no comm accounting events
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = train_step(args.warmup + i)
@@ -228,15 +239,42 @@ def main():
     retries = (torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) - retries0) if on_gpu else 0
     comm = None
     if world > 1:
-        # per-rank communication evidence of the timed steps (exposed wait, in-step busbw) and peak HBM
-        mine = {"rank": rank, "peak_mem_gib": round(mem, 1)}
+        # communication evidence, measured OUTSIDE the timed region: one extra instrumented step (exposed compute-
+        # stream wait on every AG / RS, per-collective traffic; RCCL busbw with --comm-timing), then the unit
+        # all-gather / reduce-scatter alone at the largest unit size over the data-parallel group
+        from hcache_deepspeed_amd.runtime.zero.comm_stats import ZeroCommStats
+        cs = None
+        if hasattr(zopt, "comm_stats"):
+            cs = zopt.comm_stats = ZeroCommStats(dev)
+            sync()
+            train_step(args.warmup + args.steps)
+            sync()
+            zopt.comm_stats = None
+        mine = {"rank": rank, "peak_mem_gib": round(mem, 1), "timed_steps_instrumented": timed_events is not None}
         if cs is not None:
             summ = cs.summary()
-            mine["exposed_comm_ms_per_step"] = round(summ["exposed_ms"] / args.steps, 2)
+            mine["exposed_comm_ms_per_step"] = round(summ["exposed_ms"] / args.gas, 2)
             mine["collectives"] = summ["collectives"]
+        unit_bytes = max((u.shard * u.world * 2 for u in getattr(zopt, "units", []) if u.world > 1), default=0)
+        if unit_bytes:
+            from hcache_deepspeed_amd.compile.profiler import profile_allgather, profile_reduce_scatter
+            dpg = getattr(zopt, "dp_group", None)
+            ag = profile_allgather(dpg, dev, sizes_bytes=[unit_bytes // 8, unit_bytes], iters=3)
+            rs = profile_reduce_scatter(dpg, dev, sizes_bytes=[unit_bytes // 8, unit_bytes], iters=3)
+            mine["unit_collectives_isolated"] = {
+                "unit_mib": round(unit_bytes / 2**20, 1),
+                "all_gather": ag.to_dict(), "all_gather_busbw_GBps": round(ag.busbw(unit_bytes, world) / 1e9, 1),
+                "reduce_scatter": rs.to_dict(),
+                "reduce_scatter_busbw_GBps": round(rs.busbw(unit_bytes, world) / 1e9, 1)}
+        fit = getattr(zopt, "auto_bucket_fit", None)
+        if fit is not None:
+            mine["auto_bucket_fit"] = fit
+            mine["xgmi_bucket_mb"] = getattr(zopt.mi, "xgmi_bucket_mb", None)
+            mine["zero3_unit_bucket_mb"] = getattr(zopt.mi, "zero3_unit_bucket_mb", None)
         per_rank = [None] * world
         tdist.all_gather_object(per_rank, mine)
-        comm = {"backend": tdist.get_backend(), "ranks": world,
+        comm = {"backend": tdist.get_backend(), "ranks": world, "measured": "instrumented step after the timed region",
+                "timed_steps_instrumented": any(r["timed_steps_instrumented"] for r in per_rank),
                 "exposed_comm_ms_per_step_max": max(r.get("exposed_comm_ms_per_step", 0.0) for r in per_rank),
                 "peak_mem_gib_per_rank": [r["peak_mem_gib"] for r in per_rank],
                 "rank0": per_rank[0]}
@@ -286,6 +324,8 @@ def main():
         ac = getattr(engine, "_activation_cache", None)
         if ac is not None:
             out["extra"]["act_cache"] = ac.stats()
+            if ac.peak_seen:  # the cache resets the peak counter every forward: report the max over all steps
+                out["extra"]["peak_mem_gib"] = round(max(mem, ac.peak_seen / 2**30), 1)
         zo = engine.optimizer
         sw = getattr(zo, "opt_swapper", None)
         if sw is not None:  # ZeRO-Infinity NVMe tier: how much of the optimizer's swap I/O hid behind CPU Adam

@@ -180,7 +180,7 @@ def _one_mp_rank(optim_files, model_file, model_files_all, key="fp32"):
         for r in range(W):
             n_sub = len(by_rank[r]["fp32_flat_groups"])
             parts.append(torch.cat([_partition(by_rank[r], i, key).view(-1) for i in range(n_sub)]))
-        state.update(_reconstruct(stage, merged, parts, exact=False))
+        state.update(_reconstruct(stage, merged, parts))  # exact, as the reference's sanity check (:481-485)
         shapes, metas = [], []
     for g, (shp, meta) in enumerate(zip(shapes, metas)):
         W = int(pcs[g])

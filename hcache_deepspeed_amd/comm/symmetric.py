@@ -14,8 +14,14 @@ flags and reads their chunks straight over xGMI -- no ring steps, no host involv
   collectives when ``compile.symmetric_memory`` is on (runtime/zero/optimizer.py ``enable_symmetric_comm``).
 
 The protocol needs every rank to issue the same collectives of one ``SymmetricMemory`` in the same order on ONE
-stream (like any collective); use separate objects for concurrently running streams. Waits inside the kernel are
-bounded: a missing peer sets an error word (``error()``) instead of hanging the GPU.
+stream (like any collective); use separate objects for concurrently running streams.
+
+Failure is loud, never silent: waits inside the kernel are bounded, and a timed-out wait (a peer that fell behind by
+more than the bound, or never issued the collective) marks the buffer failed for good. The kernel writes the error to
+a host-mapped pinned status word that every later call checks for free (``SymmetricMemoryError`` is raised, and the
+group is marked broken so ``small_all_reduce`` falls back to RCCL), and to an optional device flag (``dev_status``)
+that the ZeRO optimizer folds into its step-skip flag, so the step that consumed stale peer data does not update the
+weights (runtime/zero/optimizer.py).
 """
 import ctypes
 import os
@@ -27,8 +33,15 @@ from ..ops import native
 
 MAX_RANKS = 8
 _cache = {}
-# one-shot all-reduce threshold of the tensor-parallel paths (0: always torch.distributed / RCCL)
-SMALL_ALLREDUCE_KB = int(os.environ.get("HDS_SYMM_ALLREDUCE_KB", "0"))
+_broken = set()  # (id(group), tag) of buffers that timed out: RCCL from then on
+# one-shot all-reduce threshold of the tensor-parallel paths (0: always torch.distributed / RCCL). Decode-sized
+# all-reduces (<= 256 KiB: [batch, hidden] activations) are latency-bound, where one kernel reading all peers over
+# every xGMI link beats a ring's 2(W-1) steps
+SMALL_ALLREDUCE_KB = int(os.environ.get("HDS_SYMM_ALLREDUCE_KB", "256"))
+
+
+class SymmetricMemoryError(RuntimeError):
+    """A symmetric-memory collective timed out waiting for a peer: results since then are not trustworthy."""
 
 
 def supported(group=None):
@@ -61,6 +74,10 @@ class SymmetricMemory:
             bases.append(p.value)
             self._opened.append(p.value)
         self._bases = (ctypes.c_int64 * MAX_RANKS)(*(bases + [0] * (MAX_RANKS - len(bases))))
+        st = ctypes.c_void_p()
+        native.check(self.lib.hds_symm_status_alloc(ctypes.byref(st)), "symm_status_alloc")
+        self._status = st.value
+        self._status_word = ctypes.c_uint32.from_address(self._status)
         self.epoch = 0
         self.calls = {"all_reduce": 0, "all_gather": 0, "reduce_scatter": 0}
 
@@ -71,37 +88,64 @@ class SymmetricMemory:
     def fits(self, nbytes, align=16):
         return 0 < nbytes <= self.cap and nbytes % align == 0
 
-    def all_reduce(self, t, out=None):
-        """Sum of ``t`` over the group into ``out`` (default in place); returns ``out``."""
+    def error_nowait(self):
+        """0, or the error code a completed collective of this buffer reported (a host-memory read: no sync)."""
+        return int(self._status_word.value)
+
+    def check(self):
+        """Raise ``SymmetricMemoryError`` if any completed collective of this buffer timed out."""
+        e = self.error_nowait()
+        if e:
+            raise SymmetricMemoryError(f"symmetric-memory collective on rank {self.rank} timed out waiting for peer "
+                                       f"{e - 1} (world {self.world}); results of this buffer since then are invalid")
+
+    @staticmethod
+    def _dev(dev_status):
+        if dev_status is None:
+            return None
+        assert dev_status.is_cuda and dev_status.dtype == torch.int32
+        return dev_status.data_ptr()
+
+    def all_reduce(self, t, out=None, dev_status=None, check=True):
+        """Sum of ``t`` over the group into ``out`` (default in place); returns ``out``. ``check``: raise first if an
+        earlier collective of this buffer timed out (callers that fold ``dev_status`` into a step flag pass False)."""
+        if check:
+            self.check()
         out = t if out is None else out
         n = t.numel()
         if not (t.is_contiguous() and out.is_contiguous() and n % 8 == 0 and self.fits(n * t.element_size())):
             raise ValueError("symmetric all_reduce: contiguous, numel % 8 == 0 and within the buffer capacity")
         native.check(self.lib.hds_symm_allreduce(ctypes.addressof(self._bases), self.rank, self.world, self.cap,
                                                  self._next(), t.data_ptr(), out.data_ptr(), n, native.dt(t),
-                                                 native.stream()), "symm_allreduce")
+                                                 self._status, self._dev(dev_status), native.stream()),
+                     "symm_allreduce")
         self.calls["all_reduce"] += 1
         return out
 
-    def all_gather_into_tensor(self, out, inp):
+    def all_gather_into_tensor(self, out, inp, dev_status=None, check=True):
+        if check:
+            self.check()
         nb = inp.numel() * inp.element_size()
         if not (inp.is_contiguous() and out.is_contiguous() and out.numel() == inp.numel() * self.world
                 and self.fits(nb)):
             raise ValueError("symmetric all_gather: contiguous, out = world x inp, shard bytes % 16 within capacity")
         native.check(self.lib.hds_symm_allgather(ctypes.addressof(self._bases), self.rank, self.world, self.cap,
-                                                 self._next(), inp.data_ptr(), out.data_ptr(), nb, native.stream()),
-                     "symm_allgather")
+                                                 self._next(), inp.data_ptr(), out.data_ptr(), nb, self._status,
+                                                 self._dev(dev_status), native.stream()), "symm_allgather")
         self.calls["all_gather"] += 1
         return out
 
-    def reduce_scatter_tensor(self, out, inp):
+    def reduce_scatter_tensor(self, out, inp, dev_status=None, check=True):
+        if check:
+            self.check()
         n = out.numel()
         if not (inp.is_contiguous() and out.is_contiguous() and inp.numel() == n * self.world and n % 8 == 0
                 and self.fits(inp.numel() * inp.element_size()) and inp.dtype == out.dtype):
             raise ValueError("symmetric reduce_scatter: contiguous, inp = world x out, numel % 8, within capacity")
         native.check(self.lib.hds_symm_reduce_scatter(ctypes.addressof(self._bases), self.rank, self.world, self.cap,
                                                       self._next(), inp.data_ptr(), out.data_ptr(), n,
-                                                      native.dt(inp), native.stream()), "symm_reduce_scatter")
+                                                      native.dt(inp), self._status, self._dev(dev_status),
+                                                      native.stream()), "symm_reduce_scatter")
         self.calls["reduce_scatter"] += 1
         return out
 
@@ -119,6 +163,14 @@ class SymmetricMemory:
         self._opened = []
         native.check(self.lib.hds_symm_free(ctypes.c_void_p(self._own)), "symm_free")
         self._own = None
+        self.lib.hds_symm_status_free(ctypes.c_void_p(self._status))
+        self._status, self._status_word = None, ctypes.c_uint32(0)
+
+    def abandon(self):
+        """Drop a failed buffer WITHOUT the collective barrier of ``close`` (a peer may be gone); the IPC mappings
+        and the allocation are released at process exit."""
+        self._own = None
+        self._opened = []
 
 
 def get_symmetric(group=None, cap_bytes=16 << 20, tag="default"):
@@ -145,8 +197,17 @@ def small_all_reduce(x, group=None, max_kb=None):
     kb = SMALL_ALLREDUCE_KB if max_kb is None else max_kb
     nb = x.numel() * x.element_size()
     if (kb > 0 and x.is_cuda and x.is_contiguous() and x.numel() % 8 == 0 and 0 < nb <= kb * 1024
-            and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and supported(group)):
-        get_symmetric(group, cap_bytes=kb * 1024, tag="small_allreduce").all_reduce(x)
+            and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and supported(group)
+            and (id(group), "small_allreduce") not in _broken):
+        sm = get_symmetric(group, cap_bytes=kb * 1024, tag="small_allreduce")
+        try:
+            sm.all_reduce(x)
+        except SymmetricMemoryError:
+            # loud: the caller's earlier results may be stale; later calls of this group take RCCL
+            _broken.add((id(group), "small_allreduce"))
+            _cache.pop((id(group), "small_allreduce"), None)
+            sm.abandon()
+            raise
         return x
     dist.all_reduce(x, group=group)
     return x

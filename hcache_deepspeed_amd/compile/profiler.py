@@ -102,6 +102,12 @@ class CommPredictor:
     def to_dict(self):
         return {"alpha_s": self.alpha, "beta_Bps": self.beta, "samples": self.samples}
 
+    def busbw(self, nbytes, world):
+        """nccl-tests bus bandwidth (bytes/s) of an all-gather / reduce-scatter of ``nbytes`` (full buffer):
+        (world - 1) / world of the buffer over the predicted time (utils/comms_logging.py factors)."""
+        t = self(nbytes)
+        return nbytes * (world - 1) / world / t if t > 0 else 0.0
+
     @staticmethod
     def fit(samples):
         """Least-squares fit of (bytes, seconds) samples; beta is clamped positive."""
@@ -148,6 +154,36 @@ def profile_allgather(group, device, dtype=torch.bfloat16, sizes_bytes=None, ite
             torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / iters
         # every rank must agree on the model (the schedule is computed identically everywhere): take the max
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=group)
+        samples.append((shard * world * esize, float(t.item())))
+        del inp, out
+    return CommPredictor.fit(samples)
+
+
+def profile_reduce_scatter(group, device, dtype=torch.bfloat16, sizes_bytes=None, iters=3):
+    """Like ``profile_allgather`` for reduce_scatter_tensor (sizes: total input bytes)."""
+    world = tdist.get_world_size(group)
+    if world <= 1:
+        return CommPredictor()
+    if sizes_bytes is None:
+        sizes_bytes = ([4 << 20, 32 << 20, 128 << 20, 512 << 20] if device.type == "cuda" else
+                       [64 << 10, 512 << 10, 2 << 20])
+    esize = torch.empty((), dtype=dtype).element_size()
+    samples = []
+    for total in sizes_bytes:
+        shard = max(1, total // (world * esize))
+        inp = torch.zeros(shard * world, dtype=dtype, device=device)
+        out = torch.empty(shard, dtype=dtype, device=device)
+        tdist.reduce_scatter_tensor(out, inp, group=group)
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            tdist.reduce_scatter_tensor(out, inp, group=group)
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=group)
         samples.append((shard * world * esize, float(t.item())))

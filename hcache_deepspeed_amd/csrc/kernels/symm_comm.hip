@@ -15,8 +15,11 @@
 //   reads chunk b of each peer's data[parity]. Per-block flags need no grid-wide barrier (every rank splits the
 //   message into the same blocks). Two parities make reuse safe: a rank rewrites data[parity] only at epoch e+2,
 //   after every peer signalled e+1, which a peer does only after its epoch-e kernel (all reads of e) has finished.
-// Every wait is bounded (kSpinMax polls): a missing peer sets the error word and the grid still drains; the host
-// reads the error word (hds_symm_error) -- no wave can spin forever.
+// Every wait is bounded (kSpinMax polls): a missing peer sets the error word and the grid still drains -- no wave can
+// spin forever. A timeout is FATAL for the buffer: the error word is sticky (every later collective on it re-reports
+// it), and it is also written to two status words the caller passes: a host-mapped pinned word the host polls at no
+// cost before every call (comm/symmetric.py raises), and an optional device flag the ZeRO optimizer folds into its
+// step's skip flag, so a step whose collective read stale peer data never updates the weights.
 #include <cstring>
 
 #include "hds_common.h"
@@ -40,7 +43,16 @@ struct SymmArgs {
   const void* in;
   void* out;
   int64_t n;              // all-reduce: elements; all-gather: bytes per rank; reduce-scatter: elements per rank
+  uint32_t* host_status;  // host-mapped pinned word (may be null): error code on timeout
+  int32_t* dev_status;    // device flag (may be null): error code on timeout
 };
+
+__device__ __forceinline__ void report(const SymmArgs& a, uint32_t code) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(a.base[a.rank] + kErrOff), code, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  if (a.host_status) __hip_atomic_store(a.host_status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (a.dev_status) __hip_atomic_store(a.dev_status, (int32_t)code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ uint32_t* flag_ptr(char* base, int src, int blk) {
   return reinterpret_cast<uint32_t*>(base) + src * kMaxBlocks + blk;
@@ -71,9 +83,12 @@ __device__ __forceinline__ void exchange(const SymmArgs& a) {
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (!ok)
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(a.base[a.rank] + kErrOff), 1u + (uint32_t)t, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!ok) report(a, 1u + (uint32_t)t);
+  }
+  if (t == 0) {  // a buffer that timed out before stays failed: re-report, so no later step trusts it
+    const uint32_t prev = __hip_atomic_load(reinterpret_cast<uint32_t*>(a.base[a.rank] + kErrOff), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
+    if (prev != 0) report(a, prev);
   }
   __syncthreads();
   __threadfence_system();
@@ -169,7 +184,9 @@ int blocks_for(int64_t nvec) {
 }
 
 bool make_args(SymmArgs& a, const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch, const void* in,
-               void* out, int64_t n) {
+               void* out, int64_t n, void* host_status, void* dev_status) {
+  a.host_status = static_cast<uint32_t*>(host_status);
+  a.dev_status = static_cast<int32_t*>(dev_status);
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || !in || !out || epoch == 0) return false;
   for (int r = 0; r < kMaxRanks; ++r) a.base[r] = r < world ? reinterpret_cast<char*>(bases[r]) : nullptr;
   for (int r = 0; r < world; ++r)
@@ -211,6 +228,21 @@ HDS_EXPORT int hds_symm_close(void* ptr) { return hipIpcCloseMemHandle(ptr); }
 
 HDS_EXPORT int hds_symm_free(void* ptr) { return hipFree(ptr); }
 
+// host-mapped, coherent pinned status word (device stores reach the host without a synchronize)
+HDS_EXPORT int hds_symm_status_alloc(void** ptr) {
+  hipError_t e = hipHostMalloc(ptr, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return e;
+  std::memset(*ptr, 0, 64);
+  return hipSuccess;
+}
+
+HDS_EXPORT int hds_symm_status_free(void* ptr) { return hipHostFree(ptr); }
+
+// clear the sticky error word of this rank's buffer (after every rank abandoned the buffer's epochs)
+HDS_EXPORT int hds_symm_clear_error(void* base) {
+  return hipMemset(static_cast<char*>(base) + kErrOff, 0, 4);
+}
+
 // error word of this rank's buffer: 0, or 1 + the peer whose flag never arrived
 HDS_EXPORT int hds_symm_error(void* base) {
   uint32_t v = 0;
@@ -220,10 +252,11 @@ HDS_EXPORT int hds_symm_error(void* base) {
 
 // dtype: 0 fp32, 1 bf16, 2 fp16 (ops/native.py dt())
 HDS_EXPORT int hds_symm_allreduce(const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch,
-                                  const void* in, void* out, int64_t n, int dtype, hipStream_t st) {
+                                  const void* in, void* out, int64_t n, int dtype, void* host_status, void* dev_status,
+                                  hipStream_t st) {
   SymmArgs a;
   const int64_t es = dtype == 0 ? 4 : 2;
-  if (!make_args(a, bases, rank, world, cap, epoch, in, out, n) || n % 8 || n * es > cap) return hipErrorInvalidValue;
+  if (!make_args(a, bases, rank, world, cap, epoch, in, out, n, host_status, dev_status) || n % 8 || n * es > cap) return hipErrorInvalidValue;
   const dim3 grid(blocks_for(n / 8));
   switch (dtype) {
     case 0: hipLaunchKernelGGL(symm_allreduce_kernel<float>, grid, dim3(kThreads), 0, st, a); break;
@@ -235,19 +268,21 @@ HDS_EXPORT int hds_symm_allreduce(const int64_t* bases, int rank, int world, int
 }
 
 HDS_EXPORT int hds_symm_allgather(const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch,
-                                  const void* in, void* out, int64_t nbytes, hipStream_t st) {
+                                  const void* in, void* out, int64_t nbytes, void* host_status, void* dev_status,
+                                  hipStream_t st) {
   SymmArgs a;
-  if (!make_args(a, bases, rank, world, cap, epoch, in, out, nbytes) || nbytes % 16 || nbytes > cap)
+  if (!make_args(a, bases, rank, world, cap, epoch, in, out, nbytes, host_status, dev_status) || nbytes % 16 || nbytes > cap)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(symm_allgather_kernel, dim3(blocks_for(nbytes / 16)), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 
 HDS_EXPORT int hds_symm_reduce_scatter(const int64_t* bases, int rank, int world, int64_t cap, uint32_t epoch,
-                                       const void* in, void* out, int64_t n, int dtype, hipStream_t st) {
+                                       const void* in, void* out, int64_t n, int dtype, void* host_status,
+                                       void* dev_status, hipStream_t st) {
   SymmArgs a;
   const int64_t es = dtype == 0 ? 4 : 2;
-  if (!make_args(a, bases, rank, world, cap, epoch, in, out, n) || n % 8 || world * n * es > cap)
+  if (!make_args(a, bases, rank, world, cap, epoch, in, out, n, host_status, dev_status) || n % 8 || world * n * es > cap)
     return hipErrorInvalidValue;
   const dim3 grid(blocks_for(n / 8));
   switch (dtype) {

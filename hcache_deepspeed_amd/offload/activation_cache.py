@@ -141,6 +141,7 @@ class HostActivationCache:
         self._cal_bytes = {}  # per-layer eligible bytes measured by the calibration step
         self._turn_peak = None  # max allocation at the forward/backward turn-around of the last step
         self.plan_adjustments = 0
+        self.peak_seen = 0  # max allocation over every step (the planner resets the peak counter per forward)
 
     @classmethod
     def from_config(cls, cfg, device):
@@ -243,10 +244,16 @@ class HostActivationCache:
                              f"{self.budget / 2**30:.1f} GiB -> {'recomputing' if self.policy_recompute else 'spilling'} "
                              f"{len(new)} layers", ranks=[0])
             self._turn_peak = None
+            self.peak_seen = max(self.peak_seen, torch.cuda.max_memory_allocated(self.device))
             torch.cuda.reset_peak_memory_stats(self.device)
         self.cur_layer = -1
         for lst in self.by_layer.values():  # a forward whose backward never ran: return its host buffers
             for o in lst:
+                if o.dev is not None and o.h2d_done is not None:
+                    # a prefetch nobody consumed: its device buffer belongs to the compute stream's pool, and the
+                    # H2D copy may still be writing it -- the compute stream must not reuse the block before then
+                    torch.cuda.current_stream().wait_event(o.h2d_done)
+                    o.dev = None
                 if o.host is not None:
                     if o.h2d_done is not None and self.stream is not None:
                         # a prefetch nobody consumed may still read the buffer on the H2D stream: the next D2H into
@@ -430,7 +437,8 @@ class HostActivationCache:
                 "pcie_gbps": None if self.pcie_gbps is None else round(self.pcie_gbps, 1),
                 "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
-                "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits}
+                "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits,
+                "peak_gib_all_steps": round(self.peak_seen / 2**30, 1)}
 
 
 def refine_plan(plan, layer_bytes, turn_peak, budget, margin=1 << 30):
@@ -477,3 +485,12 @@ def plan_offload(layer_bytes, peak_all, budget):
         resident += layer_bytes[layers[i]]
         k = i
     return set(layers[:k])
+
+
+def build_activation_cache(cfg, device):
+    """The cache for ``mi355x.host_act_cache`` (``cfg``): policy "plan" is the per-tensor planner
+    (offload/act_plan.py), every other policy the block-level cache above."""
+    if getattr(cfg, "policy", "budget") == "plan":
+        from .act_plan import PlannedActivationCache
+        return PlannedActivationCache.from_config(cfg, device)
+    return HostActivationCache.from_config(cfg, device)

@@ -7,6 +7,7 @@ import torch
 import torch.nn.functional as F
 
 from . import native
+from ..offload import act_plan as _ap
 
 SILU, GELU_TANH, RELU, GELU, IDENTITY = 0, 1, 2, 3, 4
 _NAMES = {"silu": SILU, "swish": SILU, "gelu_tanh": GELU_TANH, "gelu_new": GELU_TANH, "gelu_pytorch_tanh": GELU_TANH,
@@ -37,6 +38,29 @@ def _t_ok(gu):
             and I % 8 == 0 and rows > 0 and gu.data_ptr() % 16 == 0)
 
 
+def _glu_out(gu, act):
+    I = gu.shape[-1] // 2
+    if native.use_native(gu):
+        gu2 = gu.reshape(-1, 2 * I).contiguous()
+        y = torch.empty(gu2.shape[0], I, device=gu.device, dtype=gu.dtype)
+        native.check(native.kernels().hds_glu_fwd(native.dt(gu), act, gu2.data_ptr(), y.data_ptr(), gu2.shape[0], I,
+                                                  native.stream()), "glu_fwd")
+        return y.view(*gu.shape[:-1], I)
+    g, u = gu.float().split(I, dim=-1)
+    return (_ref_act(g, act) * u).to(gu.dtype)
+
+
+def _glu_t_recompute(gu, act):
+    """The transposed SwiGLU output [I, rows] the down projection saved (per-tensor activation plan recipe)."""
+    I = gu.shape[-1] // 2
+    rows = gu.numel() // (2 * I)
+    y = torch.empty(rows, I, device=gu.device, dtype=gu.dtype)
+    yt = torch.empty(I, rows, device=gu.device, dtype=gu.dtype)
+    native.check(native.kernels().hds_glu_fwd_t(act, gu.data_ptr(), y.data_ptr(), yt.data_ptr(), rows, I,
+                                                native.stream()), "glu_fwd_t")
+    return yt
+
+
 class _GLUFn(torch.autograd.Function):
 
     @staticmethod
@@ -53,15 +77,13 @@ class _GLUFn(torch.autograd.Function):
                                                         native.stream()), "glu_fwd_t")
             out = y.view(*gu.shape[:-1], I)
             out._hds_t = yt  # the consumer may save this [I, rows] copy instead of out (runtime/zero/linear.py)
+            if _ap.tracking():
+                _ap.tag(yt, "glu_t", fn=_glu_t_recompute, srcs=(gu, act))
             return out
-        if native.use_native(gu):
-            gu2 = gu.reshape(-1, 2 * I).contiguous()
-            y = torch.empty(gu2.shape[0], I, device=gu.device, dtype=gu.dtype)
-            native.check(native.kernels().hds_glu_fwd(native.dt(gu), act, gu2.data_ptr(), y.data_ptr(), gu2.shape[0],
-                                                      I, native.stream()), "glu_fwd")
-            return y.view(*gu.shape[:-1], I)
-        g, u = gu.float().split(I, dim=-1)
-        return (_ref_act(g, act) * u).to(gu.dtype)
+        y = _glu_out(gu, act)
+        if _ap.tracking():
+            _ap.tag(y, "glu_out", fn=_glu_out, srcs=(gu, act))
+        return y
 
     @staticmethod
     def backward(ctx, dy):

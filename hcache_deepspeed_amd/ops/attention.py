@@ -23,6 +23,7 @@ import torch
 
 from . import native
 from .rope import rope_
+from ..offload import act_plan as _ap
 
 _HEAD_DIMS_NATIVE = (32, 48, 64, 80, 96, 112, 128, 160, 192, 256)  # mirrors HDS_ATTN_DIMS in flash_attn.hip
 
@@ -255,12 +256,25 @@ def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window
     return (o, lse) if return_lse else o
 
 
+def _qkv_recipe(proj, NH, D, n_rot, cos, sin, seq_len, pos_ids):
+    """The packed qkv tensor attention saved: the projection's recipe, then RoPE in place (as in forward)."""
+
+    def run(*args):
+        y = proj(*args)
+        if cos is not None:
+            rope_(y.view(-1, NH, D), cos, sin, n_rot, seq_len=seq_len, pos_ids=pos_ids)
+        return y
+
+    return run
+
+
 class _QKVAttnFn(torch.autograd.Function):
     """RoPE(q,k) + attention on the packed QKV GEMM output; see module docstring."""
 
     @staticmethod
     def forward(ctx, qkv, n_q, n_kv, cos, sin, seq_len, causal, scale, cu_seqlens, pos_ids, window):
         T, NH, D = qkv.shape
+        tagged = _ap.lookup(qkv) if _ap.tracking() else None
         if cos is not None:
             rope_(qkv, cos, sin, n_q + n_kv, seq_len=seq_len, pos_ids=pos_ids)  # in place on the GEMM output
         q = qkv[:, :n_q]
@@ -273,6 +287,14 @@ class _QKVAttnFn(torch.autograd.Function):
             _native_fwd(q, k, v, o, lse, causal, scale, cu, B, sl, max_len, window)
         else:
             o, lse = _ref_attention(q, k, v, causal, scale, cu_seqlens, seq_len, window)
+        if _ap.tracking():  # per-tensor activation plan: qkv = RoPE(projection), recomputable; o / LSE are not
+            if tagged is not None and tagged.fn is not None:
+                _ap.tag(qkv, "qkv", fn=_qkv_recipe(tagged.fn, NH, D, n_q + n_kv, cos, sin, seq_len, pos_ids),
+                        srcs=tagged.srcs)
+            else:
+                _ap.tag(qkv, "qkv")
+            _ap.tag(o, "attn_out")
+            _ap.tag(lse, "attn_lse")
         ctx.save_for_backward(qkv, o, lse, cos, sin, cu_seqlens, pos_ids)
         ctx.args = (n_q, n_kv, seq_len, causal, scale, window)
         return o.view(T, n_q * D)

@@ -100,9 +100,12 @@ _KERNEL_SIGS = {
     "hds_symm_close": "p",
     "hds_symm_free": "p",
     "hds_symm_error": "p",
-    "hds_symm_allreduce": "p" + "ii" + "l" + "u" + "pp" + "l" + "i" + "s",
-    "hds_symm_allgather": "p" + "ii" + "l" + "u" + "pp" + "l" + "s",
-    "hds_symm_reduce_scatter": "p" + "ii" + "l" + "u" + "pp" + "l" + "i" + "s",
+    "hds_symm_status_alloc": "p",
+    "hds_symm_status_free": "p",
+    "hds_symm_clear_error": "p",
+    "hds_symm_allreduce": "p" + "ii" + "l" + "u" + "pp" + "l" + "i" + "pp" + "s",
+    "hds_symm_allgather": "p" + "ii" + "l" + "u" + "pp" + "l" + "pp" + "s",
+    "hds_symm_reduce_scatter": "p" + "ii" + "l" + "u" + "pp" + "l" + "i" + "pp" + "s",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "u": ctypes.c_uint32, "l": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p}

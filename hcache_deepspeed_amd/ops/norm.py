@@ -9,6 +9,7 @@ import torch
 import torch.nn as nn
 
 from . import native
+from ..offload import act_plan as _ap
 
 
 def _ref_norm(x, residual, weight, bias, eps, is_ln):
@@ -65,6 +66,14 @@ def _native_bwd(dy2, h2, dres2, weight, bias, mean, rstd, is_ln, need_wgrad):
     return dx, dw, db
 
 
+def _norm_out(h, weight, bias, eps, is_ln):
+    """Recompute the norm output from the saved pre-norm sum (bit-identical: the fused kernel rounds the sum to the
+    activation dtype before its statistics, like this unfused call)."""
+    if native.use_native(h):
+        return _native_fwd(h.contiguous(), None, weight, bias, eps, is_ln)[0]
+    return _ref_norm(h, None, weight, bias, eps, is_ln)[0]
+
+
 class _NormFn(torch.autograd.Function):
     """y = norm(x [+ residual]); returns (y, h) where h is the pre-norm sum (the new residual)."""
 
@@ -84,6 +93,10 @@ class _NormFn(torch.autograd.Function):
             mean = hf.mean(-1) if is_ln else None
             var = ((hf - (mean[:, None] if is_ln else 0.0)) ** 2).mean(-1)
             rstd = torch.rsqrt(var + eps)
+        if _ap.tracking():  # per-tensor activation plan: the output (and the new residual) can be recomputed
+            if r2 is not None:
+                _ap.tag(h, "resid", fn=torch.add, srcs=(x2, r2))
+            _ap.tag(y, "norm_out", fn=_norm_out, srcs=(h, weight, bias, float(eps), bool(is_ln)))
         ctx.save_for_backward(h, weight, bias, mean, rstd)
         ctx.is_ln = is_ln
         ctx.has_res = residual is not None

@@ -83,15 +83,17 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
         assert engine.optimizer is not None, "DeepCompile needs an optimizer"
     t0 = time.perf_counter()
     if cfg.offload_activation and engine._activation_cache is None:
-        from ..offload.activation_cache import HostActivationCache
+        from ..offload.activation_cache import build_activation_cache
         hc = engine._config.mi355x.host_act_cache
-        engine._activation_cache = HostActivationCache.from_config(hc, engine.device).attach(engine.module)
+        engine._activation_cache = build_activation_cache(hc, engine.device).attach(engine.module)
     times["offload_activation"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     if cfg.offload_opt_states:
         assert engine.optimizer is not None and hasattr(engine.optimizer, "enable_state_offload"), \
             "offload_opt_states needs the ZeRO optimizer"
-        engine.optimizer.enable_state_offload(include_master=bool((compile_kwargs or {}).get("offload_master", True)))
+        kw = compile_kwargs or {}
+        engine.optimizer.enable_state_offload(include_master=bool(kw.get("offload_master", True)),
+                                              ratio=float(kw.get("offload_states_ratio", 1.0)))
     times["offload_adam_states"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     if cfg.offload_parameters and not engine._config.zero_config.offload_param.enabled:

@@ -177,6 +177,10 @@ class HostActCacheConfig:
     prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block
     host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: min(40% of host RAM, 160 GiB))
     copy_window_gib: float = 0.0  # queued-but-unfinished copy bytes per direction (0: from the HBM headroom)
+    # policy "plan" (offload/act_plan.py): per-tensor keep / spill / recompute. The modelled cost of a hidden spill
+    # (concurrent kernels slow down while a copy runs), and optional fixed {tensor class: action} overrides
+    spill_cost_ms_per_gb: float = 0.6
+    forced_actions: Optional[dict] = None
 
 
 AUTO = -1
@@ -315,10 +319,11 @@ class DeepSpeedConfig:
         hac = m.get("host_act_cache") or {}
         self.mi355x = MI355XConfig(
             # "auto": sized from an alpha-beta fit of the data-parallel all-gather measured at startup (AUTO = -1)
-            xgmi_bucket_mb=_auto_or(m.get("xgmi_bucket_mb", 256), int),
+            # default "auto": at dp > 1 the buckets follow the measured xGMI all-gather (at dp = 1: 256 / 128 MiB)
+            xgmi_bucket_mb=_auto_or(m.get("xgmi_bucket_mb", "auto"), int),
             zero3_prefetch_depth=int(m.get("zero3_prefetch_depth", 2)),
             zero3_max_reduce_inflight=int(m.get("zero3_max_reduce_inflight", 2)),
-            zero3_unit_bucket_mb=_auto_or(m.get("zero3_unit_bucket_mb", 128), float),
+            zero3_unit_bucket_mb=_auto_or(m.get("zero3_unit_bucket_mb", "auto"), float),
             comm_stats=bool(m.get("comm_stats", False)),
             direct_wgrad=bool(m.get("direct_wgrad", True)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),

@@ -181,9 +181,8 @@ class DeepSpeedEngine(nn.Module):
                                           q_rounding=0 if wq["rounding"] == "nearest" else 1)
         self._activation_cache = None
         if cfg.mi355x.host_act_cache.enabled:
-            from ..offload.activation_cache import HostActivationCache
-            self._activation_cache = HostActivationCache.from_config(cfg.mi355x.host_act_cache,
-                                                                     self.device).attach(self.module)
+            from ..offload.activation_cache import build_activation_cache
+            self._activation_cache = build_activation_cache(cfg.mi355x.host_act_cache, self.device).attach(self.module)
         log_dist(f"DeepSpeedEngine ready: dtype={self.compute_dtype} zero_stage={self.zero_optimization_stage()} "
                  f"dp={self.dp_world_size} micro_bs={self.train_micro_batch_size_per_gpu()} "
                  f"gas={self.gradient_accumulation_steps()}", ranks=[0])

@@ -114,3 +114,53 @@ class ZeroCommStats:
             kinds[kind] = d
         out["collectives"] = kinds
         return out
+
+
+class UnitEventProfiler:
+    """Host-side counts and durations of ZeRO-3 unit events (fetch, prefetch, wait, release) with the elements each
+    moved; the API of the reference's partitioned-parameter profiler (runtime/zero/partitioned_param_profiler.py:10),
+    kept next to the collective accounting above. ``timers`` (utils/timer.SynchronizedWallClockTimer) optionally
+    receives the same start/stop calls so the events appear in the engine's timer log."""
+
+    class _Event:
+        __slots__ = ("name", "count", "num_elem", "seconds", "_t0")
+
+        def __init__(self, name):
+            self.name, self.count, self.num_elem, self.seconds, self._t0 = name, 0, 0, 0.0, None
+
+    def __init__(self, timers=None):
+        self.timers = timers
+        self.event_counters = {}
+
+    def reset_events(self):
+        self.event_counters = {k: self._Event(k) for k in self.event_counters}
+
+    def start_event(self, name):
+        ev = self.event_counters.get(name)
+        if ev is None:
+            ev = self.event_counters[name] = self._Event(name)
+        ev._t0 = time.perf_counter()
+        if self.timers is not None:
+            self.timers(name).start()
+
+    def stop_event(self, name, num_elem):
+        ev = self.event_counters.get(name)
+        if ev is None or ev._t0 is None:
+            raise KeyError(f"stop_event({name!r}) without a matching start_event")
+        ev.seconds += time.perf_counter() - ev._t0
+        ev._t0 = None
+        ev.count += 1
+        ev.num_elem += int(num_elem)
+        if self.timers is not None:
+            self.timers(name).stop()
+
+    def summary(self):
+        return {k: {"count": e.count, "numel": e.num_elem, "ms": round(e.seconds * 1e3, 3)}
+                for k, e in self.event_counters.items()}
+
+    def log_events(self):
+        from ...utils.logging import log_dist
+        parts = [f"{k}: {d['count']}x {d['numel']} elem {d['ms']} ms" for k, d in self.summary().items()]
+        log_dist("zero-3 unit events | " + " | ".join(parts), ranks=[0])
+        if self.timers is not None and self.event_counters:
+            self.timers.log(names=list(self.event_counters))

@@ -230,6 +230,13 @@ def build_state_dict(z, flats, scalars):
 
 
 def _split_like(flat, groups):
+    """Cut one rank's concatenated stage-3 sub-group flats into this model's per-group partitions. A shortfall is
+    accepted only up to the alignment padding a writer may leave off the tail (2 * world elements per group); a
+    larger one means a mismatched or truncated checkpoint and raises instead of loading zeros."""
+    total = sum(g.part for g in groups)
+    slack = sum(2 * g.world for g in groups)
+    if flat.numel() + slack < total:
+        raise ValueError(f"stage-3 sub-group flats hold {flat.numel()} elements per rank, this model needs {total}")
     out, off = [], 0
     for g in groups:
         n = min(g.part, max(0, flat.numel() - off))

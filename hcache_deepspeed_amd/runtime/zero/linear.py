@@ -117,7 +117,11 @@ class LinearFunctionForZeroStage3(torch.autograd.Function):
         ctx.save_for_backward(xt if ctx.x_t else x)
         ctx.weight = weight
         ctx.has_bias = bias is not None
-        return _linear_fwd(x, weight, bias)
+        out = _linear_fwd(x, weight, bias)
+        from ...offload import act_plan
+        if act_plan.tracking() and not ctx.x_t:  # recomputable from its (saved) input: offload/act_plan.py
+            act_plan.tag(out, "linear_out", fn=_linear_fwd, srcs=(x, weight, bias))
+        return out
 
     @staticmethod
     def backward(ctx, dy):

@@ -1018,6 +1018,12 @@ class ZeroOptimizer:
             return False
         self._symm = {key: symmetric.SymmetricMemory(g, nb) for key, (g, nb) in need.items()}
         self._symm_streams = {k: torch.cuda.Stream(device=self.device, priority=-1) for k in ("ag", "rs")}
+        # a timed-out exchange raises this device flag (symm_comm.hip): step() folds it, reduced over the data-parallel
+        # group, into the skip flag -- the step that consumed stale peer data never updates the weights -- and raises
+        # at the next step on every rank (read from pinned memory once the copy has landed: no extra host sync)
+        self._symm_err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._symm_flag_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._symm_flag_ev = None
         log_dist(f"symmetric_memory: {len(self._symm)} buffers, "
                  f"{sum(sm.cap for sm in self._symm.values()) * 2 / 2**20:.0f} MiB per rank", ranks=[0])
         return True
@@ -1037,7 +1043,7 @@ class ZeroOptimizer:
 
     def _all_gather(self, out, inp, group):
         w = self._symm_issue("ag", group, inp.numel() * inp.element_size(),
-                             lambda sm: sm.all_gather_into_tensor(out, inp))
+                             lambda sm: sm.all_gather_into_tensor(out, inp, dev_status=self._symm_err, check=False))
         if w is not None:
             return w
         c = self._ncomm(group)
@@ -1048,7 +1054,7 @@ class ZeroOptimizer:
     def _reduce_scatter(self, out, inp, group):
         if out.numel() % 8 == 0 and inp.dtype == out.dtype:
             w = self._symm_issue("rs", group, inp.numel() * inp.element_size(),
-                                 lambda sm: sm.reduce_scatter_tensor(out, inp))
+                                 lambda sm: sm.reduce_scatter_tensor(out, inp, dev_status=self._symm_err, check=False))
             if w is not None:
                 return w
         c = self._ncomm(group)
@@ -1535,29 +1541,58 @@ class ZeroOptimizer:
     def _seg_group(self, seg):
         return self.param_groups[seg.group]
 
-    @torch.no_grad()
-    def enable_state_offload(self, include_master=True):
+    def enable_state_offload(self, include_master=True, ratio=1.0):
         """Optimizer states (and the fp32 master) live in pinned host memory between ``step()`` and the late
         backward of the next step (compile ``offload_opt_states``)."""
         if self.kind == "generic":
             raise NotImplementedError("offload_opt_states needs a fused optimizer (Adam/Lion/Adagrad) over the flat store")
         from .state_offload import OptimizerStateOffload
         if self.state_offload is None:
-            self.state_offload = OptimizerStateOffload(self, include_master)
+            self.state_offload = OptimizerStateOffload(self, include_master, ratio)
         return self.state_offload
 
     def _states_resident(self):
         if self.state_offload is not None:
             self.state_offload.wait()
 
+    def _symm_check_failed(self):
+        """Raise (on every rank, consistently) if an earlier step's symmetric-memory collective timed out on any
+        rank; that step was skipped on the device. The unit collectives fall back to RCCL before raising."""
+        ev = getattr(self, "_symm_flag_ev", None)
+        if ev is None or not ev.query() or int(self._symm_flag_host[0]) == 0:
+            return
+        from ...comm.symmetric import SymmetricMemoryError
+        code = int(self._symm_flag_host[0])
+        for sm in self._symm.values():
+            sm.abandon()
+        self._symm, self._symm_flag_ev = {}, None
+        raise SymmetricMemoryError(f"a ZeRO symmetric-memory unit collective timed out (code {code}); that step was "
+                                   f"skipped on every rank and the unit collectives now use RCCL")
+
+    def _symm_fold(self):
+        """Fold the symmetric-memory error flag (max over the data-parallel group, over RCCL) into the skip flag."""
+        flag = self._symm_err.clone()
+        if self.dp_world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.dp_group)
+        torch.maximum(self._inf_buf, flag, out=self._inf_buf)
+        self._symm_flag_host.copy_(flag, non_blocking=True)
+        self._symm_flag_ev = torch.cuda.Event()
+        self._symm_flag_ev.record()
+
+    @torch.no_grad()
     def step(self, closure=None):
         s = self.store
+        symm = bool(getattr(self, "_symm", None))
+        if symm:
+            self._symm_check_failed()
         self._states_resident()
         inv = 1.0 / (self.layout_world_for_avg() * self.loss_scaler.loss_scale)
         self._norm_buf.zero_()
         self._inf_buf.zero_()
         fused.grad_sumsq([s.grad], out=self._norm_buf, found_inf=self._inf_buf)
         self._reduce_norm()
+        if symm:
+            self._symm_fold()
         coef = fused.clip_coef(self._norm_buf, self.clip_grad, inv, coef=self._coef_buf)
         self.global_norm = self._norm_buf  # sqrt applied lazily in get_global_norm
         self._norm_scale = inv
@@ -1568,7 +1603,7 @@ class ZeroOptimizer:
                 log_dist(f"overflow: skipping step, loss scale -> {self.loss_scaler.loss_scale}", ranks=[0])
                 self.zero_grad()
                 return False
-        found_inf = self._inf_buf if self.loss_scaler.dynamic else None
+        found_inf = self._inf_buf if (self.loss_scaler.dynamic or symm) else None
         for gi, group in enumerate(self.param_groups):
             group["step"] = group.get("step", 0) + 1
         if self.kind == "generic":

@@ -13,18 +13,25 @@ of reading stale data). The reload is issued at a backward trace position chosen
 measured H2D time) or, without a plan, when backward starts; the device buffer is allocated on the compute stream
 (whose allocator pool holds what backward freed) and ``step()`` waits on the per-state H2D events. Between those
 two points the HBM the states occupied (12 B/param with the fp32 master) is free for activations.
+
+Offload and reload run on SEPARATE copy streams (like the reference's dedicated streams in z3.cpp): a reload issued
+while the post-step offload of other states is still draining does not queue behind it -- it waits only for its own
+state's offload. ``ratio`` < 1 offloads only that fraction of the state bytes (whole states, the largest first): the
+partial offload for a model whose states almost fit, planned from the bytes the step is over budget.
 """
 import torch
 
 
 class OptimizerStateOffload:
 
-    def __init__(self, zopt, include_master=True):
+    def __init__(self, zopt, include_master=True, ratio=1.0):
         self.z = zopt
         self.include_master = bool(include_master)
+        self.ratio = float(ratio)
         dev = zopt.device
         self.cuda = dev.type == "cuda"
-        self.stream = torch.cuda.Stream(dev, priority=-1) if self.cuda else None
+        self.stream = torch.cuda.Stream(dev, priority=-1) if self.cuda else None  # offload (D2H)
+        self.reload_stream = torch.cuda.Stream(dev, priority=-1) if self.cuda else None  # reload (H2D)
         self.host = {}
         self.events = {}
         self.offloaded = False
@@ -36,13 +43,26 @@ class OptimizerStateOffload:
 
     def _tensors(self):
         """Device-resident states this executor moves (host-resident ones -- ZeRO-Offload -- are left alone; an
-        fp32 master that IS the compute-dtype shard, as in fp32 training, stays too)."""
+        fp32 master that IS the compute-dtype shard, as in fp32 training, stays too); with ``ratio`` < 1 the largest
+        states first, until that fraction of their bytes is covered."""
         s = self.z.store
         out = [(k, v) for k, v in s.states.items() if v is not None and v.device.type == self.z.device.type]
         m = s.master
         if (self.include_master and m is not None and m.device.type == self.z.device.type
                 and not (m.numel() and s.lp.numel() and m.data_ptr() == s.lp.data_ptr())):
             out.append(("master", m))
+        if self.ratio < 1.0:
+            if not hasattr(self, "_keys"):  # fixed at the first call (sizes never change; offloaded ones read 0)
+                size = lambda kv: kv[1].numel() * kv[1].element_size()  # noqa: E731
+                total = sum(size(kv) for kv in out)
+                keys, acc = [], 0
+                for kv in sorted(out, key=size, reverse=True):
+                    if acc >= self.ratio * total - 1:
+                        break
+                    keys.append(kv[0])
+                    acc += size(kv)
+                self._keys = set(keys)
+            out = [kv for kv in out if kv[0] in self._keys]
         return out
 
     def state_bytes(self):
@@ -92,14 +112,15 @@ class OptimizerStateOffload:
             if self.cuda:
                 ready = torch.cuda.Event()
                 ready.record(cur)
-                with torch.cuda.stream(self.stream):
-                    self.stream.wait_event(ready)
+                rs = self.reload_stream
+                with torch.cuda.stream(rs):
+                    rs.wait_event(ready)
                     if k in self.events:
-                        self.stream.wait_event(self.events[k])  # the offload of this state has drained
+                        rs.wait_event(self.events[k])  # this state's offload has drained (and only this one)
                     buf.copy_(h, non_blocking=True)
-                    buf.record_stream(self.stream)
+                    buf.record_stream(rs)
                     ev = torch.cuda.Event()
-                    ev.record(self.stream)
+                    ev.record(rs)
                 self.events[k] = ev
             else:
                 buf.copy_(h)
@@ -127,4 +148,5 @@ class OptimizerStateOffload:
 
     def stats(self):
         return {"state_bytes": self.bytes, "offloads": self.n_offloads, "reloads": self.n_reloads,
-                "reload_pos": self.reload_pos}
+                "reload_pos": self.reload_pos, "ratio": self.ratio,
+                "states": sorted(k for k, _ in self._tensors()) if self.ratio < 1.0 else "all"}

@@ -462,3 +462,17 @@ def test_universal_moments_load_into_unstepped_generic_optimizer(tmp_path):
     d = str(tmp_path)
     run_distributed(_generic_save, 1, d)
     run_distributed(_generic_load, 1, d)
+
+
+def test_stage3_split_rejects_truncated_flat():
+    """A stage-3 sub-group flat shorter than this model's partitions by more than the alignment padding raises
+    (it used to load zero-padded weights and moments)."""
+    import types
+    import pytest
+    import torch
+    from hcache_deepspeed_amd.runtime.zero.ds_state import _split_like
+    groups = [types.SimpleNamespace(part=100, world=2), types.SimpleNamespace(part=50, world=2)]
+    out = _split_like(torch.ones(148), groups)  # 2 short: alignment padding, accepted
+    assert [t.numel() for t in out] == [100, 50] and float(out[1][-1]) == 0.0
+    with pytest.raises(ValueError):
+        _split_like(torch.ones(120), groups)

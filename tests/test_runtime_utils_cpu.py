@@ -105,9 +105,11 @@ def test_nvtx_decorator_and_profiler_and_comet_gate():
     assert not m.enabled
 
 
-def test_engine_compile_offload_opt_states_roundtrip():
+@pytest.mark.parametrize("ratio", [1.0, 0.5])
+def test_engine_compile_offload_opt_states_roundtrip(ratio):
     """engine.compile() with offload_opt_states: Adam states leave the device after each step and come back
-    for the next; training matches an uncompiled engine exactly."""
+    for the next; training matches an uncompiled engine exactly. ratio 0.5: only the largest states covering half
+    the bytes move (fp32 training: the master is the parameter shard itself, so one of exp_avg / exp_avg_sq)."""
     import hcache_deepspeed_amd as ds
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
     from tests.test_zero_cpu import TINY
@@ -124,7 +126,7 @@ def test_engine_compile_offload_opt_states_roundtrip():
         calls = []
         if compiled:
             eng.register_compile_pass("probe", lambda e: calls.append(e))
-            eng.compile()
+            eng.compile(compile_kwargs={"offload_states_ratio": ratio})
             assert eng.is_compiled and eng.is_deepcompile_enabled() and calls == [eng]
             assert "offload_adam_states" in eng.get_compile_time()
         g = torch.Generator().manual_seed(3)
@@ -136,6 +138,11 @@ def test_engine_compile_offload_opt_states_roundtrip():
             eng.step()
             out.append(float(loss))
         losses[compiled] = out
+        if compiled:
+            st = eng.optimizer.state_offload.stats()
+            assert st["offloads"] == 3 and st["ratio"] == ratio
+            if ratio < 1:
+                assert len(st["states"]) == 1, st
     assert losses[True] == pytest.approx(losses[False], rel=1e-6, abs=1e-6)
 
 

@@ -59,3 +59,36 @@ def _run(rank, world):
 
 def test_symmetric_collectives_world2_gpu():
     run_distributed(_run, 2, timeout=240)
+
+
+def _run_skip(rank, world):
+    """Rank 1 skips one TP all-reduce: the exchange that waits for it times out, and every rank's symmetric
+    all-reduce then raises SymmetricMemoryError within a few calls (never returns stale sums silently after the
+    timeout is known); afterwards the group falls back to torch.distributed with correct results."""
+    from hcache_deepspeed_amd.comm import symmetric
+    from hcache_deepspeed_amd.comm.symmetric import SymmetricMemoryError
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    x = torch.ones(1024, device=dev)
+    for _ in range(3):
+        y = symmetric.small_all_reduce(x.clone(), None, max_kb=64)
+        torch.cuda.synchronize()
+        assert torch.equal(y, torch.full_like(x, world))
+    raised_at = None
+    for i in range(6):
+        if rank == 1 and i == 0:
+            continue  # the skipped collective
+        try:
+            symmetric.small_all_reduce(x.clone(), None, max_kb=64)
+            torch.cuda.synchronize()
+        except SymmetricMemoryError:
+            raised_at = i
+            break
+    assert raised_at is not None, "no SymmetricMemoryError after a skipped collective"
+    torch.distributed.barrier()
+    y = symmetric.small_all_reduce(x.clone(), None, max_kb=64)  # broken group: torch.distributed now
+    assert torch.equal(y, torch.full_like(x, world))
+
+
+def test_symmetric_skipped_collective_raises_world2_gpu():
+    run_distributed(_run_skip, 2, timeout=240)

@@ -124,3 +124,75 @@ def test_zero3_symmetric_memory_world2_matches_world1(tmp_path):
     for n, w in a["weights"].items():
         rel = float((b["weights"][n] - w).norm() / w.norm().clamp_min(1e-12))
         assert rel < 2e-2, (n, rel)
+
+
+def _run_skip(rank, world, d):
+    """Rank 1 silently skips one symmetric all-gather in step 2: the ranks' epochs desynchronise, rank 0's last
+    exchange of the step times out. That step must be skipped on BOTH ranks (weights unchanged) and the next step
+    must raise SymmetricMemoryError on both ranks -- within bounded time, never silently wrong weights."""
+    import time
+    import hcache_deepspeed_amd as hds
+    import hcache_deepspeed_amd.comm as hcomm
+    from hcache_deepspeed_amd.comm.symmetric import SymmetricMemoryError
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    torch.cuda.set_device(0)
+    for name in ("all_gather_into_tensor", "reduce_scatter_tensor"):
+        setattr(hcomm, name, _staged(name))
+        setattr(hcomm.comm, name, getattr(hcomm, name))
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(**CFG))
+    cfg = {"train_micro_batch_size_per_gpu": 2, "bf16": {"enabled": True}, "gradient_clipping": 1.0,
+           "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "zero_optimization": {"stage": 3},
+           "compile": {"symmetric_memory": True}}
+    eng, _, _, _ = hds.initialize(model=m, config=cfg)
+    eng.compile()
+    z = eng.optimizer
+    assert z._symm
+    g = torch.Generator().manual_seed(7)
+
+    def batch():
+        ids = torch.randint(0, CFG["vocab_size"], (4, 128), generator=g)
+        return ids[rank * 2:(rank + 1) * 2].to(eng.device)
+
+    def train_step():
+        x = batch()
+        loss = eng(x, labels=x)
+        eng.backward(loss)
+        eng.step()
+
+    train_step()
+    torch.cuda.synchronize()
+    before = z.store.master.detach().clone()
+    if rank == 1:
+        orig, n = z._symm_issue, [0]
+
+        def skipping(kind, group, nbytes, fn):
+            if kind == "ag":
+                n[0] += 1
+                if n[0] == 2:
+                    return hcomm.comm._Done()  # "forgot" this collective: no kernel, no epoch
+            return orig(kind, group, nbytes, fn)
+
+        z._symm_issue = skipping
+    train_step()  # the desynchronised step
+    torch.cuda.synchronize()
+    if rank == 1:
+        z._symm_issue = orig
+    assert torch.equal(z.store.master, before), "a step with a timed-out symmetric collective updated the weights"
+    t0 = time.time()
+    raised = False
+    try:
+        train_step()
+    except SymmetricMemoryError:
+        raised = True
+    assert raised, "no SymmetricMemoryError after a timed-out collective"
+    assert time.time() - t0 < 120
+    assert not z._symm  # fell back to RCCL for the unit collectives
+    torch.save({"ok": True}, os.path.join(d, f"skip{rank}.pt"))
+
+
+def test_zero3_symmetric_memory_skipped_collective_fails_loudly(tmp_path):
+    d = str(tmp_path)
+    run_distributed(_run_skip, 2, d, timeout=300)
+    for r in range(2):
+        assert torch.load(os.path.join(d, f"skip{r}.pt"), weights_only=True)["ok"]

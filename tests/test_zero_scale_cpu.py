@@ -182,6 +182,12 @@ def test_bench_torchrun_cpu_dry_run():
     coll = comm["rank0"]["collectives"]
     assert coll["all_gather"]["count"] > 0 and coll["reduce_scatter"]["count"] > 0
     assert coll["all_gather"]["bytes"] > 0 and coll["reduce_scatter"]["world"] == 4
+    # the timed steps run uninstrumented; the evidence comes from one extra step and isolated collectives after them
+    assert comm["timed_steps_instrumented"] is False and comm["rank0"]["timed_steps_instrumented"] is False
+    iso = comm["rank0"]["unit_collectives_isolated"]
+    assert iso["all_gather_busbw_GBps"] >= 0 and iso["reduce_scatter"]["samples"]
+    # bucket sizes default to "auto" at N > 1: the alpha-beta fit of the data-parallel all-gather is reported
+    assert comm["rank0"]["auto_bucket_fit"]["samples"] and comm["rank0"]["xgmi_bucket_mb"] >= 16
 
 
 def test_memory_plan_bench_configs():
