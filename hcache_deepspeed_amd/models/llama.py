@@ -177,14 +177,15 @@ class LlamaAttention(nn.Module):
             return self.o_proj(o)
         qkv = self.qkv_proj(x).view(T, self.n_q + 2 * self.n_kv, self.d)
         if self.sp_group is not None:
-            from ..parallel.ulysses import ulysses_out, ulysses_qkv
+            from ..parallel.ulysses import local_heads, ulysses_out, ulysses_qkv
             from .. import comm as dist
             P = dist.get_world_size(self.sp_group)
             B = T // seq_len
+            lq, lkv = local_heads(self.n_q, self.n_kv, self.sp_group)  # uneven heads / GQA with n_kv < sp
             full = ulysses_qkv(qkv, self.n_q, self.n_kv, self.sp_group, B)
-            o = qkv_attention(full, self.n_q // P, self.n_kv // P, cos, sin, seq_len=seq_len * P, causal=True,
+            o = qkv_attention(full, lq, lkv, cos, sin, seq_len=seq_len * P, causal=True,
                               window=self.cfg.sliding_window)
-            o = ulysses_out(o.view(B * seq_len * P, self.n_q // P, self.d), self.sp_group, B).reshape(T, -1)
+            o = ulysses_out(o.view(B * seq_len * P, lq, self.d), self.sp_group, B, self.n_q, self.n_kv).reshape(T, -1)
             return self.o_proj(o)
         o = qkv_attention(qkv, self.n_q, self.n_kv, cos, sin, seq_len=seq_len, causal=True, cu_seqlens=cu_seqlens,
                           pos_ids=pos_ids, window=self.cfg.sliding_window)

@@ -514,10 +514,12 @@ class PlannedActivationCache(HostActivationCache):
         else:
             v = h.t
             if v is None:
-                args = [self._src_value(s) for s in h.srcs]
+                # a peek (consume=False: calibration timing) must not consume the sources either, nor cache
+                args = [self._src_value(s, consume) for s in h.srcs]
                 with torch.no_grad():
                     v = h.fn(*args)
-                h.t = v
+                if consume:
+                    h.t = v
         if consume:
             h.refs -= 1
             if h.refs <= 0:

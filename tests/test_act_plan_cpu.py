@@ -131,3 +131,20 @@ def test_planner_prefers_cheap_recompute_then_spill_then_gemm_recompute():
     assert sum(items[k] for k in spilled) <= 3 * GB
     freed = sum(items[k] for k, a in acts.items() if a != KEEP)
     assert freed >= 9 * GB
+
+
+def test_calibration_step_times_recipes_without_consuming():
+    """The calibration step (everything spilled) runs each class's recipe once to time it; that peek must not
+    consume any handle (an inlined recipe's sources included) -- gradients stay exact."""
+    model = _model()
+    ids = torch.randint(0, 128, (2, 16))
+    ref_loss, ref = _grads(model, ids)
+    cache = PlannedActivationCache(torch.device("cpu"), min_bytes=0, min_layers_resident=1)
+    cache.attach(model)
+    cache._stage = 1  # what forward_context's planner does on the GPU before the calibration forward
+    loss, g = _grads(model, ids, cache)
+    assert torch.equal(loss, ref_loss)
+    for n in ref:
+        torch.testing.assert_close(g[n], ref[n], rtol=0, atol=0, msg=n)
+    assert {"norm_out#0", "resid#1", "linear_out#0", "glu_out#0", "qkv#0"} <= set(cache.rec_ms), cache.rec_ms
+    assert cache._cal_items and cache.bytes_offloaded > 0

@@ -147,3 +147,101 @@ def _domino(rank, world):
 def test_domino_tp_matches_single():
     """Domino half-batch overlap of the TP all-reduces reproduces single-process training."""
     run_distributed(_domino, 2)
+
+
+def _gqa_local(q_, k_, v_):
+    """[B, S, Hq, D] x [B, S, Hkv, D] causal attention; q head i uses kv head i // (Hq // Hkv)."""
+    G = q_.shape[2] // k_.shape[2]
+    k_ = k_.repeat_interleave(G, dim=2)
+    v_ = v_.repeat_interleave(G, dim=2)
+    return torch.nn.functional.scaled_dot_product_attention(q_.transpose(1, 2), k_.transpose(1, 2),
+                                                            v_.transpose(1, 2), is_causal=True).transpose(1, 2)
+
+
+def _ulysses_uneven(rank, world, n_q, n_kv):
+    import hcache_deepspeed_amd.comm as hcomm
+    from hcache_deepspeed_amd.parallel.ulysses import DistributedAttention
+    from hcache_deepspeed_amd.utils import groups
+    groups.initialize(sp=world)
+    grp = groups._get_sequence_parallel_group()
+    torch.manual_seed(0)
+    B, S, D = 2, 16, 8
+    q = torch.randn(B, S, n_q, D, requires_grad=True)
+    k = torch.randn(B, S, n_kv, D, requires_grad=True)
+    v = torch.randn(B, S, n_kv, D, requires_grad=True)
+    go = torch.randn(B, S, n_q, D)
+    full = _gqa_local(q, k, v)
+    full.backward(go)
+    sl = slice(rank * S // world, (rank + 1) * S // world)
+    ql, kl, vl = (t.detach()[:, sl].clone().requires_grad_(True) for t in (q, k, v))
+    # record the order of all-to-all issues and waits: with even heads all three must be in flight before a wait
+    log, orig = [], hcomm.all_to_all_single
+
+    class W:
+        def __init__(self, w):
+            self.w = w
+
+        def wait(self):
+            log.append("wait")
+            return self.w.wait() if self.w is not None else True
+
+    def spy(*a, async_op=False, **kw):
+        log.append("issue")
+        w = orig(*a, async_op=async_op, **kw)
+        return W(w) if async_op else w
+
+    hcomm.all_to_all_single = spy
+    try:
+        out = DistributedAttention(_gqa_local, grp, sp_stream=object())(ql, kl, vl)
+    finally:
+        hcomm.all_to_all_single = orig
+    assert torch.allclose(out, full[:, sl], atol=1e-5), (out - full[:, sl]).abs().max()
+    out.backward(go[:, sl])
+    for a, b in ((ql, q), (kl, k), (vl, v)):
+        assert torch.allclose(a.grad, b.grad[:, sl], atol=1e-5), (a.grad - b.grad[:, sl]).abs().max()
+    if n_q % world == 0 and n_kv % world == 0:
+        assert log[:4] == ["issue", "issue", "issue", "wait"], log
+
+
+@pytest.mark.parametrize("heads", [(6, 2), (8, 4), (7, 7)])
+def test_ulysses_uneven_heads_and_gqa_world4(heads):
+    """6 q / 2 kv heads on 4 ranks (kv heads replicated, uneven q split), 7 heads on 4 ranks (uneven MHA), and the
+    even case with its three all-to-alls issued before the first wait; forward and backward match unsharded."""
+    run_distributed(_ulysses_uneven, 4, *heads)
+
+
+def _sp_llama_uneven(rank, world):
+    """The Llama attention path (fused qkv all-to-all) with 6 q / 2 kv heads at sp = 4: loss and gradients match
+    one process."""
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.parallel.ulysses import enable_sequence_parallel
+    from hcache_deepspeed_amd.utils import groups
+    groups.initialize(sp=world)
+    grp = groups._get_sequence_parallel_group()
+    cfg = dict(vocab_size=64, hidden_size=48, intermediate_size=64, num_hidden_layers=2, num_attention_heads=6,
+               num_key_value_heads=2, head_dim=8, max_position_embeddings=64)
+    torch.manual_seed(0)
+    ref = LlamaForCausalLM(tiny(**cfg))
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(**cfg))
+    enable_sequence_parallel(m, grp)
+    g = torch.Generator().manual_seed(5)
+    S = 16
+    x = torch.randint(0, 64, (2, S + 1), generator=g)
+    x, t = x[:, :-1].contiguous(), x[:, 1:].contiguous()
+    lr = ref(x, targets=t)
+    lr.backward()
+    sl = slice(rank * S // world, (rank + 1) * S // world)
+    loss = m(x[:, sl].contiguous(), targets=t[:, sl].contiguous())
+    loss.backward()
+    lt = loss.detach().clone()
+    torch.distributed.all_reduce(lt)
+    assert abs(float(lt) / world - float(lr)) < 1e-4
+    for (n, p), (_, pr) in zip(m.named_parameters(), ref.named_parameters()):
+        gsum = p.grad.clone()
+        torch.distributed.all_reduce(gsum)
+        assert torch.allclose(gsum / world, pr.grad, atol=1e-5, rtol=1e-3), (n, (gsum / world - pr.grad).abs().max())
+
+
+def test_ulysses_llama_gqa_fewer_kv_heads_than_ranks():
+    run_distributed(_sp_llama_uneven, 4)
