@@ -1,13 +1,22 @@
 """Activation checkpointing (reference: runtime/activation_checkpointing/checkpointing.py -- ``checkpoint`` :488,
-``non_reentrant_checkpoint`` :704, ``configure``, model-parallel RNG tracker :124-247, cpu_checkpointing :474-486).
+``non_reentrant_checkpoint`` :704, ``configure``, model-parallel RNG tracker :124-247, cpu_checkpointing :474-486,
+partition_activations :266-303 / :377-431, contiguous buffers, ``profile``).
 
-Implementation: torch's non-reentrant checkpoint (saved-tensor hooks), which composes with the ZeRO-3
-forward hooks (a recomputed block re-gathers its unit) and with the host activation cache. ``cpu_checkpointing``
-keeps the block inputs in pinned host memory via ``torch.autograd.graph.save_on_cpu(pin_memory=True)``.
-``partition_activations`` splits checkpointed inputs across the tensor-parallel group and all-gathers them
-on recompute.
+Implementation: torch's non-reentrant checkpoint (saved-tensor hooks), which composes with the ZeRO-3 forward hooks
+(a recomputed block re-gathers its unit) and with the host activation cache. ``cpu_checkpointing`` keeps the block
+inputs in pinned host memory via ``torch.autograd.graph.save_on_cpu(pin_memory=True)``.
+
+``partition_activations`` (tensor parallelism, where every model-parallel rank holds the same block inputs): each
+rank keeps only its 1/mp slice of every floating checkpointed input (``_PartitionedCheckpoint``: the slices go
+through ``save_for_backward``, so the host activation cache or ``cpu_checkpointing`` can move them too) and the
+recompute all-gathers them over the model-parallel group first. ``contiguous_memory_optimization`` stores those
+slices in ONE preallocated buffer per input position with ``number_checkpoints`` slots (no allocator churn between
+layers; ``reset()`` rewinds it every forward), and requires ``number_checkpoints``. ``profile`` times every
+checkpointed forward and recompute (synchronised) and logs the totals at ``reset()``.
 """
 import contextlib
+import functools
+import time
 
 import torch
 import torch.utils.checkpoint as _tc
@@ -39,6 +48,10 @@ def configure(mpu_, deepspeed_config=None, partition_activations=None, contiguou
                  ("profile", profile)):
         if v is not None:
             _CONFIG[k] = v
+    if _CONFIG["contiguous_memory_optimization"] and not _CONFIG["number_checkpoints"]:
+        raise ValueError("activation_checkpointing.contiguous_memory_optimization needs number_checkpoints (the slots "
+                         "of its preallocated buffers)")
+    _CONTIG.bufs.clear()
     _CONFIGURED = True
 
 
@@ -46,30 +59,176 @@ def is_configured():
     return _CONFIGURED
 
 
+class _Contiguous:
+    """One preallocated flat buffer per checkpointed-input position, ``number_checkpoints`` slots each."""
+
+    def __init__(self):
+        self.bufs = {}  # position -> (buffer [slots, n], next slot)
+
+    def take(self, pos, part):
+        slots = _CONFIG["number_checkpoints"]
+        b = self.bufs.get(pos)
+        if b is None or b[0].shape[1] != part.numel() or b[0].dtype != part.dtype or b[0].device != part.device:
+            b = [torch.empty(slots, part.numel(), dtype=part.dtype, device=part.device), 0]
+            self.bufs[pos] = b
+        if b[1] >= slots:
+            raise RuntimeError(f"contiguous_memory_optimization: more than number_checkpoints={slots} checkpointed "
+                               f"calls since the last reset()")
+        buf, i = b[0], b[1]
+        b[1] += 1
+        # a slot tensor over the buffer's storage WITHOUT the view relationship: views share one version counter,
+        # so filling a later slot would invalidate the earlier slots saved for backward
+        n = part.numel()
+        out = torch.empty(0, dtype=part.dtype, device=part.device).set_(buf.untyped_storage(),
+                                                                        buf.storage_offset() + i * n, (n, ))
+        out.copy_(part)
+        return out
+
+    def rewind(self):
+        for b in self.bufs.values():
+            b[1] = 0
+
+
+_CONTIG = _Contiguous()
+_STATS = {"calls": 0, "saved_bytes": 0, "full_bytes": 0, "fwd_s": 0.0, "recompute_s": 0.0}
+
+
+def stats():
+    """Counters since the last ``reset()``: checkpointed calls, bytes of inputs kept (after partitioning) against
+    their full size, and with ``profile`` the synchronised forward / recompute seconds."""
+    return dict(_STATS)
+
+
 def reset():
-    pass
+    """Start of a new forward (reference ``reset``): rewind the contiguous buffers, log and clear the profile."""
+    if _CONFIG["profile"] and _STATS["calls"]:
+        from ...utils.logging import log_dist
+        log_dist(f"activation checkpointing: {_STATS['calls']} calls, forward {_STATS['fwd_s'] * 1e3:.1f} ms, "
+                 f"recompute {_STATS['recompute_s'] * 1e3:.1f} ms, kept {_STATS['saved_bytes'] / 2**20:.1f} of "
+                 f"{_STATS['full_bytes'] / 2**20:.1f} MiB", ranks=[0])
+    _CONTIG.rewind()
+    for k in _STATS:
+        _STATS[k] = 0.0 if k.endswith("_s") else 0
 
 
-class _PartitionedInput(torch.autograd.Function):
-    """Keep only this TP rank's slice of a checkpointed activation; all-gather it on recompute."""
+def _mp_group():
+    if _MPU is not None:
+        g = _MPU.get_model_parallel_group() if hasattr(_MPU, "get_model_parallel_group") else None
+    else:
+        from ...utils import groups
+        g = groups._get_model_parallel_group() if dist.is_initialized() else None
+    if g is None or dist.get_world_size(g) <= 1:
+        return None
+    return g
+
+
+def _partitionable(t, mp):
+    return torch.is_tensor(t) and t.is_floating_point() and t.numel() >= mp
+
+
+class _Timer:
+
+    def __init__(self, key):
+        self.key = key
+
+    def __enter__(self):
+        if _CONFIG["profile"]:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        if _CONFIG["profile"]:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            _STATS[self.key] += time.perf_counter() - self.t0
+
+
+class _PartitionedCheckpoint(torch.autograd.Function):
+    """Reentrant checkpoint that keeps 1/mp of each floating input (see module docstring)."""
 
     @staticmethod
-    def forward(ctx, x):
-        return x
+    def forward(ctx, run, group, *args):
+        mp, r = dist.get_world_size(group), dist.get_rank(group)
+        ctx.run, ctx.group = run, group
+        ctx.meta = []  # per arg: None (kept whole / non-tensor) or (shape, numel, requires_grad)
+        keep, saved = [], []
+        for i, a in enumerate(args):
+            if _partitionable(a, mp):
+                flat = a.detach().reshape(-1)
+                part_n = -(-flat.numel() // mp)
+                lo, hi = min(r * part_n, flat.numel()), min((r + 1) * part_n, flat.numel())
+                part = flat.new_zeros(part_n)
+                part[:hi - lo] = flat[lo:hi]
+                if _CONFIG["contiguous_memory_optimization"]:
+                    part = _CONTIG.take(len(saved), part)
+                ctx.meta.append((a.shape, flat.numel(), a.requires_grad))
+                saved.append(part)
+                keep.append(None)
+                _STATS["saved_bytes"] += part.numel() * part.element_size()
+                _STATS["full_bytes"] += flat.numel() * flat.element_size()
+            else:
+                ctx.meta.append(None)
+                keep.append(a)
+        ctx.keep = keep
+        ctx.save_for_backward(*saved)
+        ctx.cpu_rng = torch.get_rng_state()
+        ctx.dev_rng = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
+        _STATS["calls"] += 1
+        with torch.no_grad(), _Timer("fwd_s"):
+            out = run(*args)
+        ctx.tuple_out = isinstance(out, tuple)
+        return out
 
     @staticmethod
-    def backward(ctx, g):
-        return g
+    def backward(ctx, *gouts):
+        parts = list(ctx.saved_tensors)
+        mp = dist.get_world_size(ctx.group)
+        args = []
+        for m, k in zip(ctx.meta, ctx.keep):
+            if m is None:
+                args.append(k)
+                continue
+            shape, n, rg = m
+            part = parts.pop(0)
+            full = part.new_empty(part.numel() * mp)
+            dist.all_gather_into_tensor(full, part.contiguous(), group=ctx.group)
+            args.append(full[:n].view(shape).requires_grad_(rg))
+        devs = [torch.cuda.current_device()] if ctx.dev_rng is not None else []
+        with torch.random.fork_rng(devices=devs), _Timer("recompute_s"):
+            torch.set_rng_state(ctx.cpu_rng)
+            if ctx.dev_rng is not None:
+                torch.cuda.set_rng_state(ctx.dev_rng)
+            with torch.enable_grad():
+                out = ctx.run(*args)
+        outs = out if ctx.tuple_out else (out, )
+        pairs = [(o, g) for o, g in zip(outs, gouts) if torch.is_tensor(o) and o.requires_grad and g is not None]
+        if pairs:
+            torch.autograd.backward([o for o, _ in pairs], [g for _, g in pairs])
+        return (None, None) + tuple(a.grad if torch.is_tensor(a) and a.requires_grad else None for a in args)
 
 
 def checkpoint(function, *args, **kwargs):
-    """Recompute ``function(*args)`` in backward instead of storing its activations."""
+    """Recompute ``function(*args)`` in backward instead of storing its activations (with ``partition_activations``
+    under tensor parallelism: keeping 1/mp of the inputs, all-gathered on recompute)."""
     ctx = contextlib.nullcontext()
     if _CONFIG["cpu_checkpointing"]:
         ctx = torch.autograd.graph.save_on_cpu(pin_memory=torch.cuda.is_available())
     if _CONFIG["synchronize_checkpoint_boundary"] and torch.cuda.is_available():
         torch.cuda.synchronize()
-    with ctx:
+    group = _mp_group() if _CONFIG["partition_activations"] else None
+    if group is not None and torch.is_grad_enabled():
+        fn = functools.partial(function, **kwargs) if kwargs else function
+        with ctx:
+            return _PartitionedCheckpoint.apply(fn, group, *args)
+    if _CONFIG["profile"] or _CONFIG["contiguous_memory_optimization"]:
+        _STATS["calls"] += 1
+        for a in args:
+            if torch.is_tensor(a) and a.is_floating_point():
+                nb = a.numel() * a.element_size()
+                _STATS["saved_bytes"] += nb
+                _STATS["full_bytes"] += nb
+    with ctx, _Timer("fwd_s"):
         return _tc.checkpoint(function, *args, use_reentrant=False, **kwargs)
 
 

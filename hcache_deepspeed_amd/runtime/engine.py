@@ -144,6 +144,14 @@ class DeepSpeedEngine(nn.Module):
         self.training_dataloader = self.deepspeed_io(training_data, collate_fn=collate_fn) \
             if training_data is not None else None
 
+        # activation checkpointing (reference: the user calls deepspeed.checkpointing.configure; a config section is
+        # applied here so partition_activations / contiguous buffers / profile take effect without that call)
+        from .activation_checkpointing import checkpointing as _ac
+        if cfg.raw.get("activation_checkpointing") and not _ac.is_configured():
+            _ac.configure(mpu, deepspeed_config=cfg)
+        acc = cfg.activation_checkpointing_config
+        self._ac_reset = bool(acc.partition_activations or acc.contiguous_memory_optimization or acc.profile)
+
         # flops profiler
         self.flops_profiler = None
         if cfg.flops_profiler_config.get("enabled", False):
@@ -381,6 +389,9 @@ class DeepSpeedEngine(nn.Module):
             kwargs.update(self.progressive_layer_drop.get_state())
         if self.optimizer is not None:
             self.optimizer.pre_forward()
+        if self._ac_reset and self.module.training:
+            from .activation_checkpointing import checkpointing as _ac
+            _ac.reset()  # rewind the contiguous checkpoint buffers, log the profile
         ctx = self._activation_cache.forward_context() if (self._activation_cache is not None and
                                                              self.module.training) else contextlib.nullcontext()
         with ctx:

@@ -49,6 +49,15 @@ class PipelineEngine(DeepSpeedEngine):
         self.agg_eval_loss = None
         self._eval_outputs = None
         self._compute_loss = True
+        # tensor parallelism inside a stage: every model-parallel rank holds the same activation, so each sends only
+        # its 1/mp slice to the next stage (and its slice of the input gradient back) and the receiver all-gathers
+        # over the model-parallel group -- the p2p bytes per link drop by mp (reference engine.py:144-145,720-842)
+        pcfg = self._config.pipeline or {}
+        mp = self.grid.get_model_parallel_world_size()
+        self.is_pipe_partitioned = mp > 1 and bool(pcfg.get("pipe_partitioned", True))
+        self.is_grad_partitioned = self.is_pipe_partitioned and bool(pcfg.get("grad_partitioned", True))
+        self._mp_group = self.grid.get_model_parallel_group() if mp > 1 else None
+        self.p2p_bytes_sent = 0
         if self.num_stages > 1:
             self.module.sync_tied_weights()
             if self.optimizer is not None:
@@ -90,6 +99,9 @@ class PipelineEngine(DeepSpeedEngine):
         self.module.train()
         self.total_loss = None
         self._compute_loss = True
+        if getattr(self, "_ac_reset", False):
+            from ..activation_checkpointing import checkpointing as _ac
+            _ac.reset()  # every micro-batch of the previous batch has finished its backward
         sched = S.TrainSchedule(self.micro_batches, self.num_stages, self.stage_id)
         self._exec_schedule(sched)
         self.agg_train_loss = self._aggregate_loss(self.total_loss)
@@ -214,9 +226,7 @@ class PipelineEngine(DeepSpeedEngine):
             zopt.backward(loss)
         else:
             outs = [t for t in _as_tuple(out) if isinstance(t, torch.Tensor) and t.requires_grad]
-            grads = self.pipe_buffers["grads_in"].pop(mb)
-            if zopt.loss_scale != 1.0:
-                pass  # gradients arriving from the next stage already carry the loss scale
+            grads = self.pipe_buffers["grads_in"].pop(mb)  # already carry the loss scale of the next stage
             torch.autograd.backward(outs, grad_tensors=list(grads[:len(outs)]))
         zopt.finish_backward()
         x = self.pipe_buffers["inputs"].pop(mb, None)
@@ -246,6 +256,36 @@ class PipelineEngine(DeepSpeedEngine):
         self.micro_steps += self.micro_batches
 
     # ---- communication ------------------------------------------------------------------
+    def _slice(self, t):
+        """This model-parallel rank's 1/mp of ``t`` (flat, zero-padded to a multiple of mp)."""
+        mp, r = dist.get_world_size(self._mp_group), dist.get_rank(self._mp_group)
+        flat = t.detach().reshape(-1)
+        n = -(-flat.numel() // mp)
+        part = flat.new_zeros(n)
+        lo, hi = min(r * n, flat.numel()), min((r + 1) * n, flat.numel())
+        part[:hi - lo] = flat[lo:hi]
+        return part
+
+    def _part_buf(self, shape, dtype):
+        mp = dist.get_world_size(self._mp_group)
+        numel = 1
+        for d in shape:
+            numel *= d
+        return torch.empty(-(-numel // mp), dtype=dtype, device=self.device)
+
+    def _gather_full(self, part, shape):
+        mp = dist.get_world_size(self._mp_group)
+        full = part.new_empty(part.numel() * mp)
+        dist.all_gather_into_tensor(full, part, group=self._mp_group)
+        numel = 1
+        for d in shape:
+            numel *= d
+        return full[:numel].view(shape)
+
+    @staticmethod
+    def _first_float(ts):
+        return next((i for i, t in enumerate(ts) if t.is_floating_point()), None)
+
     def _exec_comm(self, cmds):
         ops, posts = [], []
         for cmd in cmds:
@@ -256,16 +296,25 @@ class PipelineEngine(DeepSpeedEngine):
                 if not self._send_meta_done:
                     p2p.send_meta(ts, self.next_rank, self.device)
                     self._send_meta_done = True
-                ops += [("send", t.detach(), self.next_rank) for t in ts]
+                send = [t.detach() for t in ts]
+                i0 = self._first_float(send) if self.is_pipe_partitioned else None
+                if i0 is not None:
+                    send[i0] = self._slice(send[i0])
+                ops += [("send", t, self.next_rank) for t in send]
             elif isinstance(cmd, S.RecvActivation):
                 if self._recv_meta is None:
                     self._recv_meta = p2p.recv_meta(self.prev_rank, self.device)
                 bufs = p2p.alloc_from_meta(self._recv_meta, self.device)
+                i0 = self._first_float(bufs) if self.is_pipe_partitioned else None
+                if i0 is not None:
+                    bufs[i0] = self._part_buf(self._recv_meta[i0][2], self._recv_meta[i0][0])
                 ops += [("recv", t, self.prev_rank) for t in bufs]
 
-                def post(mb=mb, bufs=bufs):
+                def post(mb=mb, bufs=bufs, i0=i0):
                     xs = []
-                    for t, (_, grad, _) in zip(bufs, self._recv_meta):
+                    for i, (t, (_, grad, shape)) in enumerate(zip(bufs, self._recv_meta)):
+                        if i == i0:
+                            t = self._gather_full(t, shape)
                         if t.is_floating_point() and self._train:
                             t.requires_grad_(True)
                         xs.append(t)
@@ -273,14 +322,24 @@ class PipelineEngine(DeepSpeedEngine):
 
                 posts.append(post)
             elif isinstance(cmd, S.SendGrad):
-                gs = self.pipe_buffers["grads_out"].pop(mb)
+                gs = list(self.pipe_buffers["grads_out"].pop(mb))
+                if self.is_grad_partitioned and gs:
+                    gs[0] = self._slice(gs[0])
                 ops += [("send", g, self.prev_rank) for g in gs]
             elif isinstance(cmd, S.RecvGrad):
                 out = self.pipe_buffers["outputs"][mb]
                 ts = [t for t in _as_tuple(out) if isinstance(t, torch.Tensor) and t.is_floating_point()]
                 bufs = [torch.empty_like(t) for t in ts]
+                if self.is_grad_partitioned and bufs:
+                    bufs[0] = self._part_buf(ts[0].shape, ts[0].dtype)
+
+                    def post(mb=mb, bufs=bufs, shape=ts[0].shape):
+                        bufs[0] = self._gather_full(bufs[0], shape)
+
+                    posts.append(post)
                 ops += [("recv", g, self.next_rank) for g in bufs]
                 self.pipe_buffers["grads_in"][mb] = bufs
+        self.p2p_bytes_sent += sum(t.numel() * t.element_size() for kind, t, _ in ops if kind == "send")
         p2p.batch_p2p(ops)
         for post in posts:
             post()

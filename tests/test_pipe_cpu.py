@@ -137,3 +137,69 @@ def test_partition_methods():
     assert partition_balanced([1, 1, 1, 1, 10, 1], 3) == [0, 4, 5, 6]
     b = partition_balanced([5] * 8, 4)
     assert b == [0, 2, 4, 6, 8]
+
+
+class CkBlock(Block):
+    """Block whose forward is activation-checkpointed through the runtime's ``checkpoint``."""
+
+    def forward(self, x):
+        from hcache_deepspeed_amd.runtime.activation_checkpointing import checkpointing
+        return checkpointing.checkpoint(super().forward, x)
+
+
+def _ck_specs():
+    from hcache_deepspeed_amd.runtime.pipe.module import LayerSpec, TiedLayerSpec
+    return ([TiedLayerSpec("embed", Embed)] + [LayerSpec(CkBlock) for _ in range(NBLK)] +
+            [TiedLayerSpec("embed", Embed, forward_fn=unembed)])
+
+
+def _pipe_tp_partitioned(rank, world, partitioned, out_dir):
+    """TP2 x PP2 (world 4): both model-parallel ranks of a stage hold the same activations. With
+    partition_activations + pipe/grad partitioning each keeps half of every checkpointed input and sends half of
+    every activation / gradient; training matches the unpartitioned run and the single-process reference."""
+    import os
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.runtime.activation_checkpointing import checkpointing
+    from hcache_deepspeed_amd.runtime.pipe.module import PipelineModule
+    from hcache_deepspeed_amd.runtime.pipe.topology import PipeModelDataParallelTopology
+    M, mb, steps = 3, 2, 3
+    g = torch.Generator().manual_seed(3)
+    glob = [torch.randint(0, V, (M * mb, 6), generator=g) for _ in range(steps)]
+    glob = [(x, torch.roll(x, -1, dims=1)) for x in glob]
+    ref = _reference(glob, steps, 1e-2)
+    model = PipelineModule(_ck_specs(), topology=PipeModelDataParallelTopology(num_pp=2, num_mp=2, num_dp=1),
+                           loss_fn=loss_fn, seed_layers=True, base_seed=1234, partition_method="parameters")
+    cfg = {"train_micro_batch_size_per_gpu": mb, "gradient_accumulation_steps": M,
+           "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}, "zero_optimization": {"stage": 0},
+           "activation_checkpointing": {"partition_activations": partitioned,
+                                        "contiguous_memory_optimization": partitioned,
+                                        "number_checkpoints": 2 * M, "profile": True},
+           "pipeline": {"pipe_partitioned": partitioned, "grad_partitioned": partitioned}}
+    checkpointing._CONFIGURED = False
+    eng, _, _, _ = ds.initialize(model=model, config=cfg)
+    assert eng.is_pipe_partitioned == partitioned and eng.is_grad_partitioned == partitioned
+    losses, saved, full = [], 0, 0
+    for x, y in glob:
+        loss = eng.train_batch(iter(list(zip(x.split(mb), y.split(mb)))))
+        st = checkpointing.stats()
+        saved, full = saved + st["saved_bytes"], full + st["full_bytes"]
+        losses.append(float(loss))
+    assert losses == pytest.approx(ref, rel=1e-4, abs=1e-4), (losses, ref)
+    assert full > 0
+    torch.save({"losses": losses, "saved": saved, "full": full, "p2p": eng.p2p_bytes_sent},
+               os.path.join(out_dir, f"{int(partitioned)}_{rank}.pt"))
+
+
+def test_partition_activations_and_pipe_partitioned_tp2_pp2(tmp_path):
+    import os
+    run_distributed(_pipe_tp_partitioned, 4, False, str(tmp_path))
+    run_distributed(_pipe_tp_partitioned, 4, True, str(tmp_path))
+    for r in range(4):
+        a = torch.load(os.path.join(tmp_path, f"0_{r}.pt"), weights_only=True)
+        b = torch.load(os.path.join(tmp_path, f"1_{r}.pt"), weights_only=True)
+        assert a["losses"] == pytest.approx(b["losses"], rel=1e-5, abs=1e-6)
+        # checkpointed inputs kept: half at TP2 (the last stage's first call of a batch is counted like the rest)
+        assert a["saved"] == a["full"] and b["saved"] * 2 == pytest.approx(b["full"], rel=0.01), (a, b)
+        assert b["saved"] == pytest.approx(a["saved"] / 2, rel=0.01)
+        # activations / gradients between the stages: half the bytes
+        assert b["p2p"] == pytest.approx(a["p2p"] / 2, rel=0.01), (a["p2p"], b["p2p"])
