@@ -43,8 +43,51 @@ def _moment_keys(osd):
     return keys
 
 
-def ds_to_universal(input_dir, output_dir, tag=None):
-    """Convert ``<input_dir>/<tag>`` (a ZeRO checkpoint in the reference schema) into a universal checkpoint."""
+def _extract_job(job):
+    """Worker: one (state key, TP rank) -> every parameter's merged-over-DP tensor, one temp file each."""
+    key, mp, optim_files, model_file, model_files_all, tmp = job
+    per_param = _one_mp_rank(optim_files, model_file, model_files_all, key=key)[0]
+    for name, t in per_param.items():
+        d = os.path.join(tmp, key, name)
+        os.makedirs(d, exist_ok=True)
+        torch.save(t.clone(), os.path.join(d, f"mp_{mp:02d}.pt"))
+    return key, mp, len(per_param)
+
+
+def _merge_job(job):
+    """Worker: one (state key, parameter) -> its TP slices merged into the universal file."""
+    key, name, mps, tmp, zdir, info, bare = job
+    slices = [torch.load(os.path.join(tmp, key, name, f"mp_{mp:02d}.pt"), map_location="cpu", weights_only=True)
+              for mp in mps]
+    full, extra = merge_tp_slices(name, slices, info)
+    d = os.path.join(zdir, name)
+    os.makedirs(d, exist_ok=True)
+    torch.save(full.clone() if bare else dict(extra, param=full), os.path.join(d, f"{key}.pt"))
+    return name, key, tuple(full.shape), sum(t.numel() for t in slices)
+
+
+def _run_pool(fn, jobs, workers):
+    if workers <= 1 or len(jobs) <= 1:
+        return [fn(j) for j in jobs]
+    from concurrent.futures import ThreadPoolExecutor
+    # threads: the jobs are torch.load / torch.save and tensor copies, which release the GIL; worker processes
+    # would re-import torch per worker and (forked) can deadlock in an OpenMP pool the parent already used
+    with ThreadPoolExecutor(max_workers=min(workers, len(jobs))) as ex:
+        return list(ex.map(fn, jobs))
+
+
+def ds_to_universal(input_dir, output_dir, tag=None, num_extract_workers=1, num_merge_workers=1,
+                    keep_temp_folder=False, strict=True, inject_missing_state=False):
+    """Convert ``<input_dir>/<tag>`` (a ZeRO checkpoint in the reference schema) into a universal checkpoint.
+
+    Like the reference tool (checkpoint/ds_to_universal.py:469-540): (1) extraction -- one job per (state, TP
+    rank) rebuilds every parameter from the DP shards into ``<out>/tmp`` -- runs on ``num_extract_workers``
+    processes; (2) merging of the TP slices, one job per (state, parameter), on ``num_merge_workers`` processes
+    (fewer: it holds whole parameters); (3) the non-sharded optimizer state. ``keep_temp_folder`` keeps ``tmp``;
+    ``strict`` (default) fails on a parameter of the source's ``param_shapes`` that did not convert, whose element
+    count changed in the merge, or that disagrees with the weights of the model states; ``inject_missing_state`` supplies a default ``universal_checkpoint_info`` to a
+    ZeRO-1/2 source that lacks it (otherwise that is an error, as in the reference). Writes ``latest_universal``
+    next to ``output_dir``."""
     ckpt_dir = _resolve(input_dir, tag)
     optim = _files_by_mp(ckpt_dir, "_optim_states.pt")
     models = _files_by_mp(ckpt_dir, "_model_states.pt")
@@ -61,23 +104,55 @@ def ds_to_universal(input_dir, output_dir, tag=None):
         return [f for f in mf if _dp_rank(f) == 0][0]
 
     msd0 = _load(model_file(min(optim)))
-    info = msd0.get("universal_checkpoint_info") or {}
+    injected = None
+    if "universal_checkpoint_info" not in msd0 and stage <= 2:
+        if not inject_missing_state:
+            raise ValueError(f"{model_file(min(optim))}: required 'universal_checkpoint_info' state is missing "
+                             f"(the training client must record it, or pass inject_missing_state=True)")
+        injected = {"universal_checkpoint_version": 0.2}
+    info = msd0.get("universal_checkpoint_info") or injected or {}
     buffers = set(msd0.get("buffer_names") or [])
     zdir = os.path.join(output_dir, "zero")
+    tmp = os.path.join(output_dir, "tmp")
     os.makedirs(zdir, exist_ok=True)
-    for key in keys:
-        per_mp = [_one_mp_rank(optim[mp], model_file(mp), models[mp], key=key)[0] for mp in sorted(optim)]
-        for name in per_mp[0]:
-            if name in buffers:
-                continue
-            full, extra = merge_tp_slices(name, [s[name] for s in per_mp], info)
-            d = os.path.join(zdir, name)
-            os.makedirs(d, exist_ok=True)
-            if stage == 3 and len(per_mp) == 1:
-                torch.save(full.clone(), os.path.join(d, f"{key}.pt"))  # bare tensor: the reference stage-3 flavour
-            else:
-                torch.save(dict(extra, param=full), os.path.join(d, f"{key}.pt"))
-        del per_mp
+    # 1. extraction
+    jobs = [(key, mp, optim[mp], model_file(mp), models[mp], tmp) for key in keys for mp in sorted(optim)]
+    _run_pool(_extract_job, jobs, num_extract_workers)
+    # 2. TP merge
+    mps = sorted(optim)
+    bare = stage == 3 and len(mps) == 1  # the reference stage-3 flavour: the bare tensor
+    names = sorted(n for n in os.listdir(os.path.join(tmp, "fp32")) if n not in buffers)
+    merged = _run_pool(_merge_job, [(key, n, mps, tmp, zdir, info, bare) for key in keys
+                                    for n in names if os.path.isdir(os.path.join(tmp, key, n))], num_merge_workers)
+    # 3. validity (strict) against the source's parameter list
+    declared = set()
+    for mp in mps:
+        for d in (_load(model_file(mp)).get("param_shapes") or []):
+            declared.update(d.keys())
+    problems = []
+    done = {(n, k) for n, k, _, _ in merged}
+    for n in sorted(declared - buffers):
+        for k in keys:
+            if (n, k) not in done:
+                problems.append(f"{n}: no {k} state converted")
+    module = msd0.get("module") or {}
+    for n, k, shape, n_slices in merged:
+        numel = 1
+        for x in shape:
+            numel *= x
+        if numel not in (n_slices, n_slices // max(1, len(mps))):
+            problems.append(f"{n}/{k}: merged {numel} elements from {n_slices} in {len(mps)} TP slices")
+        w = module.get(n)
+        if k == "fp32" and torch.is_tensor(w) and numel not in (w.numel(), w.numel() * len(mps)):
+            problems.append(f"{n}: {numel} elements converted, the model states hold {tuple(w.shape)}")
+    if problems:
+        msg = "universal conversion: " + "; ".join(problems[:10]) + (" ..." if len(problems) > 10 else "")
+        if strict:
+            raise ValueError(msg)
+        from ..utils.logging import logger
+        logger.warning(msg)
+    if not keep_temp_folder:
+        shutil.rmtree(tmp, ignore_errors=True)
     # global (non-sharded) optimizer state
     if stage == 3:
         gsd = dict(osd0)
@@ -98,11 +173,20 @@ def ds_to_universal(input_dir, output_dir, tag=None):
                     torch.save(step, os.path.join(zdir, name, "step.pt"))
     torch.save(gsd, os.path.join(zdir, "optimizer_state.pt"))
     # model files: one per TP rank under the world-size independent name
-    for mp in sorted(optim):
+    for mp in mps:
         src = model_file(mp)
-        shutil.copyfile(src, os.path.join(output_dir, f"mp_rank_{mp:02d}_model_states.pt"))
+        dst = os.path.join(output_dir, f"mp_rank_{mp:02d}_model_states.pt")
+        if injected is not None:
+            sd = _load(src)
+            sd["universal_checkpoint_info"] = injected
+            torch.save(sd, dst)
+        else:
+            shutil.copyfile(src, dst)
     for f in glob.glob(os.path.join(ckpt_dir, "expp_rank_*")):
         shutil.copy2(f, output_dir)
+    root, step_folder = os.path.split(os.path.normpath(output_dir))
+    with open(os.path.join(root, "latest_universal"), "w") as f:
+        f.write(step_folder)
     return output_dir
 
 

@@ -5,7 +5,7 @@ Reference parity: deepspeed/module_inject/containers/megatron_gpt.py (``Megatron
 ``query_key_value`` / ``dense`` / ``mlp.dense_h_to_4h`` / ``mlp.dense_4h_to_h`` / the two LayerNorms, converted
 into the fused ``DeepSpeedGPTInference`` block), megatron_gpt_moe.py (same block with the Megatron-DeepSpeed MoE
 MLP -- ``mlp.deepspeed_moe.experts`` -- kept as the expert path) and internlm.py (``InternLMLayerPolicy``: a
-LLaMA-style block with biased q/k/v/o projections).
+LLaMA-style block with biased q/k/v/o projections; InternLM2's fused ``wqkv`` / ``wo`` layout with GQA).
 
 MI355X design: the converted block runs this framework's HIP kernels end to end -- fused LayerNorm (with the
 residual add folded into the second norm), one qkv GEMM whose output is split with Megatron's per-head
@@ -67,10 +67,40 @@ class DSMegatronGPTBlock(nn.Module):
             self.h4_w, self.h4_b = wd(layer.mlp.dense_h_to_4h.weight), wd(getattr(layer.mlp.dense_h_to_4h, "bias", None))
             self.o4_w, self.o4_b = wd(layer.mlp.dense_4h_to_h.weight), wd(getattr(layer.mlp.dense_4h_to_h, "bias", None))
         self.apply_residual_post_ln = bool(getattr(layer, "apply_residual_connection_post_layernorm", False))
-        self.kv = None  # (k, v) [b, heads, t, d] of the incremental-decoding cache
+        # incremental-decoding KV cache: preallocated [b, heads, capacity, d] buffers, grown by doubling; a decode
+        # token is written in place by the HIP kv_append kernel (one launch for k and v), not by concatenation
+        self.kc = self.vc = None
+        self.kv_len = 0
 
     def reset_cache(self):
-        self.kv = None
+        self.kc = self.vc = None
+        self.kv_len = 0
+
+    @property
+    def kv(self):
+        """(k, v) views [b, heads, t, d] of the cached tokens, or None."""
+        if self.kc is None:
+            return None
+        return self.kc[:, :, :self.kv_len], self.vc[:, :, :self.kv_len]
+
+    def _cache_append(self, k, v):
+        b, nh, s, d = k.shape
+        t0, need = self.kv_len, self.kv_len + s
+        if self.kc is None or need > self.kc.shape[2] or self.kc.shape[0] != b:
+            cap = max(need, 2 * (self.kc.shape[2] if self.kc is not None else 0), 256)
+            kc, vc = k.new_empty(b, nh, cap, d), v.new_empty(b, nh, cap, d)
+            if t0:
+                kc[:, :, :t0].copy_(self.kc[:, :, :t0])
+                vc[:, :, :t0].copy_(self.vc[:, :, :t0])
+            self.kc, self.vc = kc, vc
+        if s == 1 and k.is_cuda:
+            from ..ops.decode_attention import kv_append
+            kv_append(k[:, :, 0], v[:, :, 0], self.kc, self.vc, torch.tensor([t0], device=k.device, dtype=torch.int64))
+        else:
+            self.kc[:, :, t0:need].copy_(k)
+            self.vc[:, :, t0:need].copy_(v)
+        self.kv_len = need
+        return self.kc[:, :, :need], self.vc[:, :, :need]
 
     def _ln(self, x, w, b, residual=None):
         from ..ops.norm import layer_norm
@@ -84,11 +114,10 @@ class DSMegatronGPTBlock(nn.Module):
         qkv = qkv.view(s, b, nh, 3, d)
         q, k, v = (qkv[:, :, :, i].permute(1, 2, 0, 3) for i in range(3))  # [b, nh, s, d]
         if use_cache:
-            if self.kv is not None:
-                k = torch.cat([self.kv[0], k], 2)
-                v = torch.cat([self.kv[1], v], 2)
-            self.kv = (k, v)
-        o = fused_core_attention(q.contiguous(), k.contiguous(), v.contiguous(), None, scale=1.0 / math.sqrt(d))
+            k, v = self._cache_append(k, v)
+        else:
+            k, v = k.contiguous(), v.contiguous()
+        o = fused_core_attention(q.contiguous(), k, v, None, scale=1.0 / math.sqrt(d))
         return o.permute(2, 0, 1, 3).reshape(s * b, nh * d)  # [s*b, h]
 
     @torch.no_grad()
@@ -155,16 +184,57 @@ def _internlm_attn_forward(self, hidden_states, attention_mask=None, position_id
     return o, None, past
 
 
+def _internlm2_attn_forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_value=None,
+                            output_attentions=False, use_cache=False, **kwargs):
+    """InternLM2 attention: ONE fused ``wqkv`` projection laid out per kv head as [q_per_kv query heads, k, v]
+    (x head_dim), GQA, ``wo`` output; same kernels as InternLM (reference containers/internlm.py)."""
+    from .containers import fused_core_attention
+    B, S, _ = hidden_states.shape
+    nh, d = self.num_heads, self.head_dim
+    nkv = int(getattr(self, "num_key_value_heads", nh))
+    g = nh // nkv
+    qkv = self.wqkv(hidden_states).view(B, S, nkv, g + 2, d)
+    q = qkv[:, :, :, :g].reshape(B, S, nh, d).transpose(1, 2)
+    k = qkv[:, :, :, g].transpose(1, 2)
+    v = qkv[:, :, :, g + 1].transpose(1, 2)
+    kv_len = S + (past_key_value[0].shape[-2] if past_key_value is not None else 0)
+    cos, sin = self.rotary_emb(v, seq_len=kv_len)
+    if position_ids is None:
+        position_ids = torch.arange(kv_len - S, kv_len, device=q.device)[None].expand(B, S)
+    cos = cos.squeeze(1).squeeze(0)[position_ids].unsqueeze(1).to(q.dtype)
+    sin = sin.squeeze(1).squeeze(0)[position_ids].unsqueeze(1).to(q.dtype)
+    q = q * cos + _rotate_half(q) * sin
+    k = k * cos + _rotate_half(k) * sin
+    if past_key_value is not None:
+        k = torch.cat([past_key_value[0], k], 2)  # the remote code's cache contract: a (k, v) tuple returned
+        v = torch.cat([past_key_value[1], v], 2)
+    past = (k, v) if use_cache else None
+    o = fused_core_attention(q, k.contiguous(), v.contiguous(), attention_mask, scale=1.0 / math.sqrt(d))
+    o = self.wo(o.transpose(1, 2).reshape(B, S, nh * d))
+    return o, None, past
+
+
 def _is_internlm_attention(m):
     return type(m).__name__ in ("InternLMAttention", "InternLM2Attention") and \
         all(hasattr(m, a) for a in ("q_proj", "k_proj", "v_proj", "o_proj", "rotary_emb", "num_heads", "head_dim"))
 
 
+def _is_internlm2_attention(m):
+    return type(m).__name__ == "InternLM2Attention" and \
+        all(hasattr(m, a) for a in ("wqkv", "wo", "rotary_emb", "num_heads", "head_dim"))
+
+
 def inject_internlm(model):
     n = 0
     for m in model.modules():
-        if _is_internlm_attention(m) and not getattr(m, "_hds_container", False):
+        if getattr(m, "_hds_container", False):
+            continue
+        if _is_internlm2_attention(m):
+            m.forward = types.MethodType(_internlm2_attn_forward, m)
+        elif _is_internlm_attention(m):
             m.forward = types.MethodType(_internlm_attn_forward, m)
-            m._hds_container = True
-            n += 1
+        else:
+            continue
+        m._hds_container = True
+        n += 1
     return n

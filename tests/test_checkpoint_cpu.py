@@ -93,3 +93,64 @@ def _load_w1_universal(rank, world, d):
 def test_universal_reshard_2_to_1(tmp_path):
     run_distributed(_save_w2, 2, str(tmp_path))
     run_distributed(_load_w1_universal, 1, str(tmp_path))
+
+
+def _save_w2_stage(rank, world, d, stage):
+    eng = _engine(stage)
+    _train(eng, 2, 5 + rank)
+    eng.save_checkpoint(d, tag="t")
+
+
+@pytest.mark.parametrize("stage", [1, 3])
+def test_ds_to_universal_workers_strict_inject(stage, tmp_path):
+    """Parallel extraction / merge give byte-identical files to the serial conversion; keep_temp_folder keeps the
+    slices; a ZeRO-1/2 source without universal_checkpoint_info needs inject_missing_state; strict fails on a
+    parameter that did not convert."""
+    from hcache_deepspeed_amd.checkpoint.ds_to_universal import main, parse_arguments
+    from hcache_deepspeed_amd.checkpoint.universal import ds_to_universal
+    d = str(tmp_path)
+    run_distributed(_save_w2_stage, 2, d, stage)
+    a, b = os.path.join(d, "ua"), os.path.join(d, "ub")
+    ds_to_universal(d, a, tag="t")
+    main(parse_arguments(["--input_folder", d, "--output_folder", b, "--tag", "t", "--num_extract_workers", "3",
+                          "--num_merge_workers", "2", "--keep_temp_folder"]))
+    assert os.path.isdir(os.path.join(b, "tmp")) and not os.path.isdir(os.path.join(a, "tmp"))
+    with open(os.path.join(d, "latest_universal")) as f:
+        assert f.read().strip() == "ub"
+    names = sorted(os.listdir(os.path.join(a, "zero")))
+    assert names == sorted(os.listdir(os.path.join(b, "zero"))) and len(names) > 3
+    for n in names:
+        pa = os.path.join(a, "zero", n)
+        if not os.path.isdir(pa):
+            continue
+        for f in os.listdir(pa):
+            x = torch.load(os.path.join(pa, f), weights_only=True)
+            y = torch.load(os.path.join(b, "zero", n, f), weights_only=True)
+            x, y = (v["param"] if isinstance(v, dict) else v for v in (x, y))
+            assert torch.equal(x, y) if torch.is_tensor(x) else x == y, (n, f)  # step.pt holds an int
+    # a source missing universal_checkpoint_info
+    mf = [f for f in os.listdir(os.path.join(d, "t")) if f.endswith("model_states.pt")]
+    for f in mf:
+        p = os.path.join(d, "t", f)
+        sd = torch.load(p, weights_only=False)
+        sd.pop("universal_checkpoint_info", None)
+        torch.save(sd, p)
+    if stage <= 2:
+        with pytest.raises(ValueError, match="universal_checkpoint_info"):
+            ds_to_universal(d, os.path.join(d, "uc"), tag="t")
+    out = ds_to_universal(d, os.path.join(d, "uc"), tag="t", inject_missing_state=True)
+    sd = torch.load(os.path.join(out, "mp_rank_00_model_states.pt"), weights_only=False)
+    assert stage == 3 or sd["universal_checkpoint_info"]["universal_checkpoint_version"] == 0.2
+    # strict: a converted parameter that disagrees with the model states' weights fails the conversion
+    bad = None
+    for f in mf:
+        p = os.path.join(d, "t", f)
+        sd = torch.load(p, weights_only=False)
+        bad = bad or next((k for k, v in sd["module"].items() if torch.is_tensor(v) and v.numel() > 4), None)
+        if bad is None:
+            return  # stage 3: the model states hold no full weights to check against
+        sd["module"][bad] = torch.zeros(3)
+        torch.save(sd, p)
+    with pytest.raises(ValueError, match="model states"):
+        ds_to_universal(d, os.path.join(d, "ud"), tag="t", inject_missing_state=True)
+    ds_to_universal(d, os.path.join(d, "ud"), tag="t", inject_missing_state=True, strict=False)

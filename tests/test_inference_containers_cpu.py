@@ -85,6 +85,9 @@ def test_megatron_gpt_block_matches_layer(post_ln_residual):
             h = blk(h, use_cache=True)
         outs.append(h)
     torch.testing.assert_close(torch.cat(outs, 0), ref, atol=2e-4, rtol=2e-4)
+    # the cache is one preallocated buffer per layer (tokens written in place), not a concatenation per token
+    blk = model[0]
+    assert blk.kv_len == 10 and blk.kc.shape[2] >= 256 and blk.kv[0].shape[2] == 10
 
 
 class _MoEMLP(nn.Module):
@@ -170,6 +173,50 @@ def test_internlm_attention_container():
         got, _, past = m[0](x, use_cache=True)
     torch.testing.assert_close(got, ref, atol=2e-4, rtol=2e-4)
     assert past[0].shape == (2, 4, 9, 16)
+
+
+class InternLM2Attention(nn.Module):
+    """InternLM2 remote-code layout: fused ``wqkv`` per kv head [q_per_kv query heads, k, v] x head_dim, GQA."""
+
+    def __init__(self, h=64, nh=4, nkv=2):
+        super().__init__()
+        self.num_heads, self.head_dim, self.num_key_value_heads = nh, h // nh, nkv
+        self.num_key_value_groups = nh // nkv
+        self.wqkv = nn.Linear(h, (nh + 2 * nkv) * (h // nh), bias=False)
+        self.wo = nn.Linear(h, h, bias=False)
+        self.rotary_emb = _Rotary(h // nh)
+
+    def forward(self, x, attention_mask=None, position_ids=None, past_key_value=None, output_attentions=False,
+                use_cache=False):
+        B, S, _ = x.shape
+        nh, d, nkv, g = self.num_heads, self.head_dim, self.num_key_value_heads, self.num_key_value_groups
+        qkv = self.wqkv(x).view(B, S, nkv, g + 2, d)
+        q = qkv[..., :g, :].reshape(B, S, nh, d).transpose(1, 2)
+        k, v = qkv[..., -2, :].transpose(1, 2), qkv[..., -1, :].transpose(1, 2)
+        cos, sin = self.rotary_emb(v, S)
+        cos, sin = cos[0, 0][:S], sin[0, 0][:S]
+        rot = lambda t: torch.cat((-t[..., d // 2:], t[..., :d // 2]), -1)  # noqa: E731
+        q, k = q * cos + rot(q) * sin, k * cos + rot(k) * sin
+        k, v = k.repeat_interleave(g, 1), v.repeat_interleave(g, 1)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        return self.wo(o.transpose(1, 2).reshape(B, S, nh * d)), None, None
+
+
+def test_internlm2_wqkv_attention_container():
+    from hcache_deepspeed_amd.inference.megatron import inject_internlm
+    torch.manual_seed(0)
+    m = nn.ModuleList([InternLM2Attention()])
+    x = torch.randn(2, 9, 64)
+    with torch.no_grad():
+        ref = m[0](x)[0]
+        assert inject_internlm(m) == 1
+        got, _, past = m[0](x, use_cache=True)
+        # incremental: 8 tokens then the 9th against the returned cache
+        o8, _, p8 = m[0](x[:, :8], use_cache=True)
+        o9, _, _ = m[0](x[:, 8:], past_key_value=p8, position_ids=torch.tensor([[8], [8]]), use_cache=True)
+    torch.testing.assert_close(got, ref, atol=2e-4, rtol=2e-4)
+    torch.testing.assert_close(o9, ref[:, 8:], atol=2e-4, rtol=2e-4)
+    assert past[0].shape == (2, 2, 9, 16)  # GQA: the cache holds the 2 kv heads
 
 
 # ---------------------------------------------------------------------------------------------------------------

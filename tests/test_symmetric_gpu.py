@@ -62,9 +62,11 @@ def test_symmetric_collectives_world2_gpu():
 
 
 def _run_skip(rank, world):
-    """Rank 1 skips one TP all-reduce: the exchange that waits for it times out, and every rank's symmetric
-    all-reduce then raises SymmetricMemoryError within a few calls (never returns stale sums silently after the
-    timeout is known); afterwards the group falls back to torch.distributed with correct results."""
+    """Rank 1 skips one TP all-reduce. Collectives pair by order (as with RCCL), so the ranks run shifted by one
+    until rank 0's extra call finds no partner and times out: rank 0's next call raises SymmetricMemoryError, and
+    rank 1 -- whose next exchange has no partner any more -- raises within two more calls. Nothing hangs, and
+    afterwards the group runs on torch.distributed with correct sums."""
+    import time
     from hcache_deepspeed_amd.comm import symmetric
     from hcache_deepspeed_amd.comm.symmetric import SymmetricMemoryError
     torch.cuda.set_device(0)
@@ -74,10 +76,15 @@ def _run_skip(rank, world):
         y = symmetric.small_all_reduce(x.clone(), None, max_kb=64)
         torch.cuda.synchronize()
         assert torch.equal(y, torch.full_like(x, world))
-    raised_at = None
-    for i in range(6):
+    t0 = time.time()
+    for i in range(4):
         if rank == 1 and i == 0:
             continue  # the skipped collective
+        symmetric.small_all_reduce(x.clone(), None, max_kb=64)
+        torch.cuda.synchronize()  # rank 0's last call times out here (bounded wait)
+    torch.distributed.barrier()
+    raised_at = None
+    for i in range(3):
         try:
             symmetric.small_all_reduce(x.clone(), None, max_kb=64)
             torch.cuda.synchronize()
@@ -85,8 +92,11 @@ def _run_skip(rank, world):
             raised_at = i
             break
     assert raised_at is not None, "no SymmetricMemoryError after a skipped collective"
+    assert raised_at == 0 or rank == 1, (rank, raised_at)
+    assert time.time() - t0 < 180
     torch.distributed.barrier()
     y = symmetric.small_all_reduce(x.clone(), None, max_kb=64)  # broken group: torch.distributed now
+    torch.cuda.synchronize()
     assert torch.equal(y, torch.full_like(x, world))
 
 
