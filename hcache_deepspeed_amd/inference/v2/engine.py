@@ -44,7 +44,7 @@ class RaggedInferenceEngineConfig:
     tensor_parallel: dict = field(default_factory=lambda: {"tp_size": 1})
     state_manager: DSStateManagerConfig = field(default_factory=DSStateManagerConfig)
     quantization: dict = field(default_factory=dict)
-    latent_mode: str = "hidden"  # HCache: "hidden" (per-layer normed hidden) or "kv" (pre-RoPE K|V)
+    latent_mode: str = "hidden"  # HCache: "hidden" (per-layer normed hidden), "hidden_fp8" (e4m3 + per-token scale) or "kv" (pre-RoPE K|V)
     dtype: str = "bf16"
 
     @staticmethod

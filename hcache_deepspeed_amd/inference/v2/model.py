@@ -19,6 +19,12 @@ HCache, as implemented here (with the defects fixed):
   Attention, O-projection and MLP are skipped.
 * ``latent_mode="kv"`` stores the PRE-RoPE K|V rows per token-layer instead (2*Hkv*D elements; half of H for
   Llama-3 GQA); restore then only rotates and scatters.
+* ``latent_mode="hidden_fp8"`` stores the hidden state as OCP e4m3 with one fp32 scale per token (``fpq`` /
+  ``quant.hip`` kernels), packed per token as [H bytes | 4 scale bytes]: H + 4 bytes per token-layer, byte parity
+  with KV offload for Llama-3 GQA (2*Hkv*D*2 = H bytes) where bf16 hidden states are 2x KV (SURVEY §7.4(5));
+  restore dequantizes on the device before the K|V GEMM.
+* latent host buffers come from a pinned pool (``offload/pinned.PinnedPool``) and return to it when the caller
+  drops the latents -- no hipHostMalloc / torch pinned allocation per ``put()``.
 * every family above implements the contract (the reference broke ``put`` for all non-Llama models).
 """
 import math
@@ -310,9 +316,7 @@ class RaggedTransformer:
         lat = None
         events = []
         if capture_latents:
-            width = spec.hidden_size if self.latent_mode == "hidden" else 2 * self.n_kv * self.d
-            lat = torch.empty(spec.num_hidden_layers, T, width, dtype=self.dtype,
-                              pin_memory=self.device.type == "cuda")
+            lat = self._latent_buffer(spec.num_hidden_layers, T)
         for i, L in enumerate(self.layers):
             if residual is None:
                 x = self._norm(h, L["ln1.w"], L["ln1.b"])
@@ -321,6 +325,8 @@ class RaggedTransformer:
                 x, residual = self._norm(h, L["ln1.w"], L["ln1.b"], residual)
             if capture_latents and self.latent_mode == "hidden":
                 self._d2h(x, lat[i], events)
+            elif capture_latents and self.latent_mode == "hidden_fp8":
+                self._d2h(self._pack_fp8(x), lat[i], events)
             a = self._attn(i, L, x, batch, T, capture_latents, lat, events)
             if spec.parallel == "shared_ln":
                 h = self._allreduce(a + self._mlp(L, x))
@@ -336,6 +342,43 @@ class RaggedTransformer:
         if events and sync_latents:
             events[-1].synchronize()
         return logits, lat
+
+    _latent_pool = None
+
+    def latent_width(self):
+        """Elements of one token-layer latent (bytes for ``hidden_fp8``)."""
+        H = self.spec.hidden_size
+        return {"hidden": H, "kv": 2 * self.n_kv * self.d, "hidden_fp8": H + 4}[self.latent_mode]
+
+    def _latent_buffer(self, n_layers, T):
+        dtype = torch.uint8 if self.latent_mode == "hidden_fp8" else self.dtype
+        shape = (n_layers, T, self.latent_width())
+        if self.device.type != "cuda":
+            return torch.empty(shape, dtype=dtype)
+        from ...offload.pinned import PinnedPool
+        pool = RaggedTransformer._latent_pool
+        if pool is None:
+            pool = RaggedTransformer._latent_pool = PinnedPool()
+        # back to the pool once the caller has dropped the latents and every per-sequence view of them
+        return pool.get_tracked(shape[0] * shape[1] * shape[2], dtype).view(shape)
+
+    def _pack_fp8(self, x):
+        """[T, H] activations -> [T, H + 4] uint8: e4m3 values, then the token's fp32 scale as 4 bytes."""
+        from ...ops.quantizer import quantize_fp8
+        T, H = x.shape
+        q, sc = quantize_fp8(x, group_size=H)
+        pk = torch.empty(T, H + 4, dtype=torch.uint8, device=x.device)
+        pk[:, :H].copy_(q.view(T, H))
+        pk[:, H:].copy_(sc.view(torch.uint8).view(T, 4))
+        return pk
+
+    def _unpack_fp8(self, pk):
+        from ...ops.quantizer import dequantize_fp8
+        T, W = pk.shape
+        H = W - 4
+        q = pk[:, :H].contiguous().view(-1)
+        sc = pk[:, H:].contiguous().view(torch.float32).view(-1)
+        return dequantize_fp8(q, sc, group_size=H, dtype=self.dtype).view(T, H)
 
     def _d2h(self, src, dst, events):
         if self.copy_stream is None:
@@ -372,7 +415,7 @@ class RaggedTransformer:
             offs.append(offs[-1] + p.shape[1])
         assert offs[-1] == T, "latents must cover exactly the batch's tokens"
         width = pieces[0].shape[-1]
-        bufs = [torch.empty(T, width, dtype=self.dtype, device=self.device) for _ in range(2)]
+        bufs = [torch.empty(T, width, dtype=pieces[0].dtype, device=self.device) for _ in range(2)]
         loaded = [torch.cuda.Event() for _ in range(2)]
         freed = [torch.cuda.Event() for _ in range(2)]
         main = torch.cuda.current_stream()
@@ -401,7 +444,9 @@ class RaggedTransformer:
     def _restore_layer(self, i, L, x, batch, T):
         nq, nkv, D = self.n_q, self.n_kv, self.d
         cache = self.kv_cache.get_cache(i)
-        if self.latent_mode == "hidden":
+        if self.latent_mode == "hidden_fp8":
+            x = self._unpack_fp8(x)
+        if self.latent_mode in ("hidden", "hidden_fp8"):
             # only the K|V rows of the projection are needed: GEMM against the k/v slice of W_qkv
             if isinstance(L["qkv.w"], _PackedWeight):  # packed rows cannot be sliced: full projection
                 kv = self.qkv_lin(x, L["qkv.w"], L["qkv.b"]).view(T, nq + 2 * nkv, D)[:, nq:].contiguous()

@@ -146,9 +146,31 @@ class PinnedPool:
         t._hds_pinned_owner = buf
         return t
 
+    def get_tracked(self, numel, dtype):
+        """Like ``get``, but the buffer goes back to the pool by itself once the returned tensor AND every view of
+        it are gone."""
+        import weakref
+        es = torch.tensor([], dtype=dtype).element_size()
+        b = self._bucket(numel * es)
+        with self._lock:
+            lst = self._free.get(b)
+            buf = lst.pop() if lst else None
+        if buf is None:
+            buf = PinnedBuffer(b)
+            self.bytes_allocated += b
+        # the storage of a tensor made by from_numpy keeps that numpy array alive until the storage itself dies,
+        # i.e. until the last tensor / view over it is gone: the finalizer rides on the array
+        import numpy as np
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * buf.nbytes).from_address(buf.ptr))
+        weakref.finalize(arr, self.put_buffer, buf)
+        return torch.from_numpy(arr)[:numel * es].view(dtype)
+
     def put(self, t):
         buf = getattr(t, "_hds_pinned_owner", None)
         if buf is None:
             return
+        self.put_buffer(buf)
+
+    def put_buffer(self, buf):
         with self._lock:
             self._free.setdefault(buf.nbytes, []).append(buf)

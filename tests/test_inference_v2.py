@@ -80,6 +80,47 @@ def test_hcache_consistency_gpu(latent_mode, sync_latents):
     _run_consistency("cuda", torch.bfloat16, latent_mode, 6e-2, sync_latents)
 
 
+def _run_fp8_latents(device, dtype):
+    """latent_mode="hidden_fp8": H + 4 bytes per token-layer (e4m3 + an fp32 scale per token), restore continues
+    decoding with logits within 2e-2 (relative, norm-wise) of the bf16/fp32 hidden-state restore."""
+    m = _model(device, dtype)
+    g = torch.Generator().manual_seed(1)
+    p1 = torch.randint(0, 211, (70, ), generator=g)
+    cont = torch.randint(0, 211, (6, ), generator=g)
+    outs = {}
+    for mode in ("hidden", "hidden_fp8"):
+        eng = build_engine_from_model(m, {"latent_mode": mode, "dtype": {torch.float32: "fp32",
+                                                                        torch.bfloat16: "bf16"}[dtype],
+                                          "state_manager": {"max_context": 1024, "kv_block_size": 64}},
+                                      device=torch.device(device), num_kv_blocks=64)
+        _, lats = eng.put([1], [p1])
+        if mode == "hidden_fp8":
+            assert lats[0].dtype == torch.uint8 and lats[0].shape == (3, 70, 256 + 4)
+        eng.evict(1)
+        eng.restore_kv([1], [p1], [lats[0]])
+        seq = []
+        for j in range(cont.numel()):
+            lg, _ = eng.put([1], [cont[j:j + 1]], capture_latents=False)
+            seq.append(lg[0].float())
+        outs[mode] = torch.stack(seq)
+        eng.flush(1)
+    a, b = outs["hidden"], outs["hidden_fp8"]
+    rel = ((a - b).norm(dim=-1) / a.norm(dim=-1)).max().item()
+    assert rel < 2e-2, rel
+    assert torch.equal(a.argmax(-1), b.argmax(-1))
+
+
+def test_hcache_fp8_latents_cpu():
+    _run_fp8_latents("cpu", torch.float32)
+
+
+@pytest.mark.gpu
+def test_hcache_fp8_latents_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_fp8_latents("cuda", torch.bfloat16)
+
+
 @pytest.mark.gpu
 def test_decode_graph_matches_eager_gpu():
     """HIP-graph decode (one captured forward per batch size, replayed with new metadata) produces the logits of the

@@ -6,7 +6,12 @@ is prefilled, evicted, and brought back three ways:
 * recompute   — full prefill again (``put`` without latent capture),
 * HCache      — ``restore_kv`` from the per-layer hidden-state latents kept in pinned host memory
                 (H2D of layer i+1 overlapped with layer i's QKV GEMM + fused RoPE/paged-KV scatter),
-* KV offload  — ``restore_kv`` in ``latent_mode="kv"`` (pre-RoPE K|V rows on the host; RoPE + scatter only).
+* KV offload  — ``restore_kv`` in ``latent_mode="kv"`` (pre-RoPE K|V rows on the host; RoPE + scatter only),
+* HCache FP8  — ``latent_mode="hidden_fp8"``: e4m3 hidden states + a per-token fp32 scale (H + 4 bytes per token-layer,
+                byte parity with KV for GQA), dequantized on the device before the K|V GEMM.
+
+After each restore, sequence 1 decodes ``--gen`` greedy tokens; the FP8 run is compared with the bf16 hidden-state
+run (first-step logit relative error, token agreement).
 
 Reports restored tokens/s and host bytes per token for each, plus the cost of capturing latents during prefill.
 
@@ -41,6 +46,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=2048)
     ap.add_argument("--layers", type=int, default=0)
     ap.add_argument("--model", default="llama3-8b", help="llama3-8b (GQA 32/8) or llama2-7b (MHA)")
+    ap.add_argument("--gen", type=int, default=64, help="greedy tokens decoded after each restore")
     args = ap.parse_args()
     from hcache_deepspeed_amd.inference.v2 import build_engine_from_model
     from hcache_deepspeed_amd.models.llama import PRESETS, LlamaForCausalLM
@@ -60,7 +66,8 @@ def main():
     prompts = [torch.randint(0, cfg.vocab_size, (C, ), generator=g) for _ in range(S)]
     uids = list(range(1, S + 1))
     res = {}
-    for mode in ("hidden", "kv"):
+    gen = {}
+    for mode in ("hidden", "kv", "hidden_fp8"):
         eng = build_engine_from_model(model, dict(econf, latent_mode=mode), device=dev, num_kv_blocks=blocks)
 
         def prefill(capture):
@@ -87,6 +94,16 @@ def main():
 
         res[f"restore_kv latent_mode={mode}"] = timed(restore)
         res[f"host bytes/token latent_mode={mode}"] = lat_bytes / n_tok
+        # greedy continuation of sequence 1 after the restore
+        toks, first = [], None
+        nxt = torch.tensor([int(prompts[0][-1])])
+        for _ in range(args.gen):
+            lg, _ = eng.put([uids[0]], [nxt], capture_latents=False)
+            if first is None:
+                first = lg[0].float().cpu()
+            nxt = lg[0].argmax().view(1).cpu()
+            toks.append(int(nxt))
+        gen[mode] = (first, toks)
         del eng, lats
         torch.cuda.empty_cache()
     print(f"{args.model} ({cfg.num_hidden_layers} layers, {cfg.num_attention_heads}/{cfg.num_key_value_heads} heads) bf16, {S} sequences x {C} tokens = {n_tok} tokens")
@@ -97,7 +114,21 @@ def main():
             print(f"  {k:40s} {v * 1e3:8.1f} ms  {n_tok / v:10.0f} tokens/s")
     rc = res["recompute (prefill)"]
     print(f"  HCache restore speedup vs recompute: {rc / res['restore_kv latent_mode=hidden']:.2f}x; "
+          f"FP8 HCache: {rc / res['restore_kv latent_mode=hidden_fp8']:.2f}x; "
           f"KV-offload restore speedup vs recompute: {rc / res['restore_kv latent_mode=kv']:.2f}x")
+    (f0, t0), (f1, t1) = gen["hidden"], gen["hidden_fp8"]
+    rel = float((f0 - f1).norm() / f0.norm())
+    agree = sum(a == b for a, b in zip(t0, t1))
+    first_diff = next((i for i, (a, b) in enumerate(zip(t0, t1)) if a != b), None)
+    print(f"  FP8 vs bf16 hidden restore: first-step logit rel err {rel:.2e}, greedy tokens equal {agree}/{len(t0)}"
+          f" (first difference at {first_diff}); kv vs hidden tokens equal "
+          f"{sum(a == b for a, b in zip(t0, gen['kv'][1]))}/{len(t0)}")
+    import json
+    print(json.dumps({"tokens": n_tok, "model": args.model, "layers": cfg.num_hidden_layers,
+                      "restore_tok_s": {m: round(n_tok / res[f"restore_kv latent_mode={m}"]) for m in gen},
+                      "host_bytes_per_token": {m: res[f"host bytes/token latent_mode={m}"] for m in gen},
+                      "recompute_tok_s": round(n_tok / rc), "fp8_logit_rel_err": rel, "fp8_tokens_equal": agree,
+                      "gen": len(t0), "fp8_first_token_diff": first_diff}))
 
 
 if __name__ == "__main__":
