@@ -80,15 +80,16 @@ def test_hcache_consistency_gpu(latent_mode, sync_latents):
     _run_consistency("cuda", torch.bfloat16, latent_mode, 6e-2, sync_latents)
 
 
-def _run_fp8_latents(device, dtype):
+def _run_fp8_latents(device, dtype, mode="hidden_fp8"):
     """latent_mode="hidden_fp8": H + 4 bytes per token-layer (e4m3 + an fp32 scale per token), restore continues
     decoding with logits within 2e-2 (relative, norm-wise) of the bf16/fp32 hidden-state restore."""
     m = _model(device, dtype)
+    qmode = mode
     g = torch.Generator().manual_seed(1)
     p1 = torch.randint(0, 211, (70, ), generator=g)
     cont = torch.randint(0, 211, (6, ), generator=g)
     outs = {}
-    for mode in ("hidden", "hidden_fp8"):
+    for mode in ("hidden", qmode):
         eng = build_engine_from_model(m, {"latent_mode": mode, "dtype": {torch.float32: "fp32",
                                                                         torch.bfloat16: "bf16"}[dtype],
                                           "state_manager": {"max_context": 1024, "kv_block_size": 64}},
@@ -96,6 +97,8 @@ def _run_fp8_latents(device, dtype):
         _, lats = eng.put([1], [p1])
         if mode == "hidden_fp8":
             assert lats[0].dtype == torch.uint8 and lats[0].shape == (3, 70, 256 + 4)
+        if mode == "hidden_int8":
+            assert lats[0].dtype == torch.uint8 and lats[0].shape == (3, 70, 256 + 8)
         eng.evict(1)
         eng.restore_kv([1], [p1], [lats[0]])
         seq = []
@@ -104,21 +107,36 @@ def _run_fp8_latents(device, dtype):
             seq.append(lg[0].float())
         outs[mode] = torch.stack(seq)
         eng.flush(1)
-    a, b = outs["hidden"], outs["hidden_fp8"]
+    a, b = outs["hidden"], outs[qmode]
     rel = ((a - b).norm(dim=-1) / a.norm(dim=-1)).max().item()
     assert rel < 2e-2, rel
     assert torch.equal(a.argmax(-1), b.argmax(-1))
 
 
-def test_hcache_fp8_latents_cpu():
-    _run_fp8_latents("cpu", torch.float32)
+@pytest.mark.parametrize("mode", ["hidden_fp8", "hidden_int8"])
+def test_hcache_quantized_latents_cpu(mode):
+    _run_fp8_latents("cpu", torch.float32, mode)
 
 
 @pytest.mark.gpu
-def test_hcache_fp8_latents_gpu():
+@pytest.mark.parametrize("mode", ["hidden_fp8", "hidden_int8"])
+def test_hcache_quantized_latents_gpu(mode):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run_fp8_latents("cuda", torch.bfloat16)
+    _run_fp8_latents("cuda", torch.bfloat16, mode)
+
+
+def test_hcache_auto_latent_mode_picks_smaller_lossless():
+    m = _model("cpu", torch.float32)  # H = 256 < 2 x 2 kv heads x 128 = 512: the hidden state is smaller
+    eng = build_engine_from_model(m, {"latent_mode": "auto", "dtype": "fp32",
+                                      "state_manager": {"max_context": 256, "kv_block_size": 64}},
+                                  device=torch.device("cpu"), num_kv_blocks=8)
+    assert eng._model.latent_mode == "hidden"
+    m2 = _model("cpu", torch.float32, hidden_size=1024, num_attention_heads=8, num_key_value_heads=2)
+    eng2 = build_engine_from_model(m2, {"latent_mode": "auto", "dtype": "fp32",
+                                        "state_manager": {"max_context": 256, "kv_block_size": 64}},
+                                   device=torch.device("cpu"), num_kv_blocks=8)
+    assert eng2._model.latent_mode == "kv"  # 2 x 2 x 128 = 512 < 1024
 
 
 @pytest.mark.gpu

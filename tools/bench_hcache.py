@@ -67,7 +67,7 @@ def main():
     uids = list(range(1, S + 1))
     res = {}
     gen = {}
-    for mode in ("hidden", "kv", "hidden_fp8"):
+    for mode in ("hidden", "kv", "hidden_fp8", "hidden_int8"):
         eng = build_engine_from_model(model, dict(econf, latent_mode=mode), device=dev, num_kv_blocks=blocks)
 
         def prefill(capture):
@@ -116,19 +116,24 @@ def main():
     print(f"  HCache restore speedup vs recompute: {rc / res['restore_kv latent_mode=hidden']:.2f}x; "
           f"FP8 HCache: {rc / res['restore_kv latent_mode=hidden_fp8']:.2f}x; "
           f"KV-offload restore speedup vs recompute: {rc / res['restore_kv latent_mode=kv']:.2f}x")
-    (f0, t0), (f1, t1) = gen["hidden"], gen["hidden_fp8"]
-    rel = float((f0 - f1).norm() / f0.norm())
-    agree = sum(a == b for a, b in zip(t0, t1))
-    first_diff = next((i for i, (a, b) in enumerate(zip(t0, t1)) if a != b), None)
-    print(f"  FP8 vs bf16 hidden restore: first-step logit rel err {rel:.2e}, greedy tokens equal {agree}/{len(t0)}"
-          f" (first difference at {first_diff}); kv vs hidden tokens equal "
-          f"{sum(a == b for a, b in zip(t0, gen['kv'][1]))}/{len(t0)}")
+    (f0, t0) = gen["hidden"]
+    quality = {}
+    for qm in ("hidden_fp8", "hidden_int8"):
+        f1, t1 = gen[qm]
+        rel = float((f0 - f1).norm() / f0.norm())
+        agree = sum(a == b for a, b in zip(t0, t1))
+        first_diff = next((i for i, (a, b) in enumerate(zip(t0, t1)) if a != b), None)
+        quality[qm] = {"logit_rel_err": rel, "tokens_equal": agree, "first_diff": first_diff}
+        print(f"  {qm} vs bf16 hidden restore: first-step logit rel err {rel:.2e}, greedy tokens equal "
+              f"{agree}/{len(t0)} (first difference at {first_diff})")
+    print(f"  kv vs hidden tokens equal {sum(a == b for a, b in zip(t0, gen['kv'][1]))}/{len(t0)}")
+    rel, agree, first_diff = (quality["hidden_fp8"][k] for k in ("logit_rel_err", "tokens_equal", "first_diff"))
     import json
     print(json.dumps({"tokens": n_tok, "model": args.model, "layers": cfg.num_hidden_layers,
                       "restore_tok_s": {m: round(n_tok / res[f"restore_kv latent_mode={m}"]) for m in gen},
                       "host_bytes_per_token": {m: res[f"host bytes/token latent_mode={m}"] for m in gen},
                       "recompute_tok_s": round(n_tok / rc), "fp8_logit_rel_err": rel, "fp8_tokens_equal": agree,
-                      "gen": len(t0), "fp8_first_token_diff": first_diff}))
+                      "gen": len(t0), "fp8_first_token_diff": first_diff, "quantized": quality}))
 
 
 if __name__ == "__main__":
