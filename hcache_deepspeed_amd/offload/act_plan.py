@@ -57,6 +57,7 @@ import torch
 
 from ..utils.logging import log_dist
 from .activation_cache import HostActivationCache, _Spilled
+from ..ops.hostcopy import d2h_
 from .pinned import PinnedPool
 
 KEEP, SPILL, RECOMPUTE = "keep", "spill", "recompute"
@@ -478,7 +479,7 @@ class PlannedActivationCache(HostActivationCache):
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record(self.stream)
-            h.host.copy_(b.view(-1), non_blocking=True)
+            d2h_(h.host, b.view(-1))  # few-workgroup copy kernel, not the wide blit (ops/hostcopy.py)
             b.record_stream(self.stream)
             h.d2h_done = torch.cuda.Event(enable_timing=timed)
             h.d2h_done.record(self.stream)

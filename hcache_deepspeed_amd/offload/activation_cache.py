@@ -60,6 +60,7 @@ import torch
 import torch.nn as nn
 
 from ..utils.logging import log_dist
+from ..ops.hostcopy import d2h_
 from .pinned import PinnedPool
 
 
@@ -348,7 +349,7 @@ class HostActivationCache:
             if cal and self._cal_copy[0] is None:  # PCIe rate of the calibration step's (saturating) copies
                 self._cal_copy[0] = torch.cuda.Event(enable_timing=True)
                 self._cal_copy[0].record(self.stream)
-            s.host.copy_(src.view(-1), non_blocking=True)
+            d2h_(s.host, src.view(-1))  # few-workgroup copy kernel, not the wide blit (ops/hostcopy.py)
             src.record_stream(self.stream)
             s.d2h_done = torch.cuda.Event()
             s.d2h_done.record(self.stream)

@@ -1,0 +1,27 @@
+"""Device -> pinned-host copies for the activation spills (csrc/kernels/hostcopy.hip).
+
+``d2h_(dst_host, src_dev)`` copies with a kernel of ``HDS_D2H_WG`` workgroups (default 16) on the CURRENT stream
+instead of hipMemcpyAsync, whose device->host path on this ROCm stack is a blit kernel spread over many workgroups
+that slows the compute kernels it overlaps (see the kernel file). ``HDS_D2H_WG=0`` restores ``copy_``.
+"""
+import os
+
+import torch
+
+from . import native
+
+D2H_WG = int(os.environ.get("HDS_D2H_WG", "16"))
+
+
+def d2h_(dst, src, n_wg=None):
+    """dst (pinned host, contiguous) <- src (device, contiguous), asynchronous on the current stream."""
+    wg = D2H_WG if n_wg is None else int(n_wg)
+    nbytes = src.numel() * src.element_size()
+    if (wg <= 0 or not src.is_cuda or dst.is_cuda or not src.is_contiguous() or not dst.is_contiguous()
+            or dst.numel() * dst.element_size() < nbytes or src.data_ptr() % 16 or dst.data_ptr() % 16):
+        dst.view(-1)[:src.numel()].copy_(src.view(-1), non_blocking=True) if dst.dtype == src.dtype else \
+            dst.copy_(src, non_blocking=True)
+        return dst
+    native.check(native.kernels().hds_copy_d2h(dst.data_ptr(), src.data_ptr(), nbytes, wg, native.stream()),
+                 "copy_d2h")
+    return dst

@@ -1549,6 +1549,9 @@ class ZeroOptimizer:
         from .state_offload import OptimizerStateOffload
         if self.state_offload is None:
             self.state_offload = OptimizerStateOffload(self, include_master, ratio)
+            # off the device from the start: the first forward is the one that needs the HBM when the states and
+            # the activations do not fit together
+            self.state_offload.offload()
         return self.state_offload
 
     def _states_resident(self):

@@ -173,3 +173,22 @@ def test_deepcompile_zero_infinity_schedule_gpu():
     assert sched.meta["comm_model"]["beta_Bps"] > 1e9  # measured PCIe H2D bandwidth, not the zero-cost default
     assert f1[-1] < f0[-1], (f0, f1)
     assert l1 == pytest.approx(l0, rel=1e-5, abs=1e-5)
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096 + 6, (64 << 20) + 10, 300 << 20])
+@pytest.mark.parametrize("wg", [1, 16])
+def test_few_workgroup_d2h_copy(nbytes, wg):
+    """ops/hostcopy.d2h_: the activation-spill copy kernel writes exactly the device bytes into pinned host memory
+    (16-byte vectors plus a byte tail), visible to the host after the stream completes."""
+    from hcache_deepspeed_amd.offload.pinned import PinnedPool
+    from hcache_deepspeed_amd.ops.hostcopy import d2h_
+    src = torch.randint(0, 255, (nbytes, ), dtype=torch.uint8, device="cuda")
+    pool = PinnedPool()
+    dst = pool.get(nbytes, torch.uint8)
+    dst.fill_(7)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        d2h_(dst, src, n_wg=wg)
+    s.synchronize()
+    assert torch.equal(dst, src.cpu())
