@@ -44,7 +44,8 @@ Mechanism:
   less than a spill, then spilling (earliest blocks first, the classes most expensive to recompute first) up to the
   bytes the copy stream drains within ``spill_overlap`` of the forward time measured on the first planned step,
   then recomputing by cost per byte. After every step the measured forward/backward turn-around peak corrects the
-  base estimate and the plan is recomputed (closed loop).
+  base estimate, the forward time against the no-spill forward prices what the spills really cost (concurrent
+  copies slow the kernels they overlap), and the plan is recomputed (closed loop).
 
 Reference anchors: FPDT's host chunk spill (sequence/fpdt_layer.py:462-508), CPU activation checkpointing
 (runtime/activation_checkpointing/checkpointing.py:474-486), the DeepCompile offload_activation pass
@@ -216,6 +217,7 @@ class PlannedActivationCache(HostActivationCache):
         self._copy_busy = [0.0, 0]  # ms, bytes of timed calibration copies
         self._copy_evs = []
         self.t_fwd_ms = None
+        self.spill_cost_measured = None  # ms per spilled GB the forward actually slowed down by
         self.est_cost_ms = 0.0
         self.step_spill_bytes = 0
         self.step_recomputed = 0
@@ -276,7 +278,7 @@ class PlannedActivationCache(HostActivationCache):
         self.layer_bytes = {}
         self._capped_this_step = 0
         self._handles, self._occ, self._tags = {}, {}, {}
-        timed = cuda and self._stage == 2
+        timed = cuda and self._stage >= 2 and self.forced is None
         if timed:
             self._fwd_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self._fwd_ev[0].record()
@@ -332,12 +334,20 @@ class PlannedActivationCache(HostActivationCache):
             self._replan(spill_cap=0)
             self._stage = 2
             return
-        if self._stage == 2 and self._fwd_ev is not None:
+        t_last = None
+        if self._fwd_ev is not None:
             s, e = self._fwd_ev
-            e.synchronize()
-            self.t_fwd_ms = s.elapsed_time(e)
+            e.synchronize()  # the forward ended a whole backward ago
+            t_last = s.elapsed_time(e)
             self._fwd_ev = None
+        if self._stage == 2 and t_last is not None:
+            self.t_fwd_ms = t_last  # forward with no spills: the base of the spill capacity and the spill cost
             self._stage = 3
+        elif t_last is not None and self.step_spill_bytes > (1 << 30) and self.t_fwd_ms:
+            # what spilling actually cost: the copies slow the kernels they overlap (measured, not modelled)
+            meas = max(0.0, t_last - self.t_fwd_ms) / (self.step_spill_bytes / 1e9)
+            self.spill_cost_measured = meas if self.spill_cost_measured is None else \
+                0.5 * (self.spill_cost_measured + meas)
         if self._turn_peak is not None:
             # closed loop: the measured turn-around peak corrects the all-off-device base estimate
             kept = sum(b for k, b in self.items.items() if self.actions.get(k, KEEP) == KEEP)
@@ -354,8 +364,9 @@ class PlannedActivationCache(HostActivationCache):
     def _replan(self, spill_cap=None):
         cap = self.spill_capacity() if spill_cap is None else spill_cap
         no_spill = range(self.n_layers - self.keep, self.n_layers)
-        new, self.est_cost_ms = plan_tensors(self.items, self._peak_all, self.budget, self.rec_ms, cap,
-                                             self.spill_cost, no_spill)
+        cost = max(self.spill_cost, self.spill_cost_measured or 0.0)
+        new, self.est_cost_ms = plan_tensors(self.items, self._peak_all, self.budget, self.rec_ms, cap, cost,
+                                             no_spill)
         if new != self.actions:
             self.replans += 1
             n = {a: sum(1 for v in new.values() if v == a) for a in (KEEP, SPILL, RECOMPUTE)}
@@ -364,7 +375,8 @@ class PlannedActivationCache(HostActivationCache):
             log_dist(f"activation plan: keep {n[KEEP]}, spill {n[SPILL]} ({sb / 2**30:.1f} GiB, cap "
                      f"{cap / 2**30:.1f} GiB), recompute {n[RECOMPUTE]} ({rb / 2**30:.1f} GiB, ~{self.est_cost_ms:.0f} ms)"
                      f" | base peak {self._peak_all / 2**30:.1f} GiB, budget {self.budget / 2**30:.1f} GiB, PCIe "
-                     f"{(self.pcie_gbps or 0):.1f} GB/s busy-rate, forward {self.t_fwd_ms or 0:.0f} ms", ranks=[0])
+                     f"{(self.pcie_gbps or 0):.1f} GB/s busy-rate, forward {self.t_fwd_ms or 0:.0f} ms, spill cost "
+                     f"{cost:.2f} ms/GB", ranks=[0])
         self.actions = new
 
     # ---------------------------------------------------------------------------------------------------------------
@@ -584,6 +596,9 @@ class PlannedActivationCache(HostActivationCache):
                   "recomputed_tensors_step": self.step_recomputed, "est_recompute_ms": round(self.est_cost_ms, 1),
                   "recipe_ms": {k: round(v, 3) for k, v in sorted(self.rec_ms.items())},
                   "t_fwd_ms": None if self.t_fwd_ms is None else round(self.t_fwd_ms, 1),
+                  "spill_cost_ms_per_gb": round(max(self.spill_cost, self.spill_cost_measured or 0.0), 3),
+                  "spill_cost_measured": None if self.spill_cost_measured is None else
+                  round(self.spill_cost_measured, 3),
                   "spill_cap_gib": round(self.spill_capacity() / 2**30, 1), "replans": self.replans,
                   "spilled_layers": None, "recomputed_layers": None})
         return s

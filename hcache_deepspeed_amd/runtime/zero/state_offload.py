@@ -10,7 +10,7 @@ overlapping the next forward; the device storage is released the moment its DMA 
 ``set_`` to an empty storage -- any stray access while offloaded sees a 0-element tensor and fails loudly instead
 of reading stale data). The reload is issued at a backward trace position chosen by the pass
 (``compile/passes.plan_state_reload``: the latest position whose remaining backward compute still covers the
-measured H2D time) or, without a plan, when backward starts; the device buffer is allocated on the compute stream
+measured H2D time) or, without a plan, state by state as soon as the HBM the backward has freed holds it; the device buffer is allocated on the compute stream
 (whose allocator pool holds what backward freed) and ``step()`` waits on the per-state H2D events. Between those
 two points the HBM the states occupied (12 B/param with the fp32 master) is free for activations.
 
@@ -99,14 +99,19 @@ class OptimizerStateOffload:
         self.reloading = False
         self.n_offloads += 1
 
-    def reload(self):
-        """Issue the H2D of every offloaded state (non-blocking); ``wait()`` orders the compute stream after it."""
+    def _pending(self):
+        """(key, tensor, host) of the states still off the device."""
+        return [(k, t, self.host[k]) for k, t in self._tensors() if k in self.host and t.numel() == 0]
+
+    def reload(self, keys=None):
+        """Issue the H2D of the offloaded states (all, or ``keys``; non-blocking); ``wait()`` orders the compute
+        stream after it."""
         if not self.offloaded or self.reloading:
             return
         cur = torch.cuda.current_stream() if self.cuda else None
         for k, t in self._tensors():
             h = self.host.get(k)
-            if h is None or t.numel() != 0:
+            if h is None or t.numel() != 0 or (keys is not None and k not in keys):
                 continue
             buf = torch.empty(h.numel(), dtype=h.dtype, device=t.device)  # compute stream's allocator pool
             if self.cuda:
@@ -125,8 +130,9 @@ class OptimizerStateOffload:
             else:
                 buf.copy_(h)
             t.set_(buf)
-        self.reloading = True
-        self.n_reloads += 1
+        if not self._pending():
+            self.reloading = True
+            self.n_reloads += 1
 
     def wait(self):
         """Make the states usable on the current stream (reloading first if nothing scheduled it)."""
@@ -143,8 +149,24 @@ class OptimizerStateOffload:
     ensure_resident = wait
 
     def on_backward_position(self, pos):
-        if self.offloaded and not self.reloading and (self.reload_pos is None or pos <= self.reload_pos):
+        if not self.offloaded or self.reloading:
+            return
+        if self.reload_pos is not None:  # placed by the compiled schedule (compile/passes.plan_state_reload)
+            if pos <= self.reload_pos:
+                self.reload()
+            return
+        if not self.cuda:
             self.reload()
+            return
+        # no schedule: bring each state back as soon as the HBM the backward has freed holds it -- at the start of
+        # backward when everything fits, late (state by state) when the states and the activations do not fit
+        # together; step() reloads whatever is left
+        limit = int(self.mem_fraction * torch.cuda.get_device_properties(self.z.device).total_memory)
+        for k, t, h in sorted(self._pending(), key=lambda x: -x[2].numel() * x[2].element_size()):
+            if torch.cuda.memory_allocated(self.z.device) + h.numel() * h.element_size() <= limit:
+                self.reload(keys={k})
+
+    mem_fraction = 0.9
 
     def stats(self):
         return {"state_bytes": self.bytes, "offloads": self.n_offloads, "reloads": self.n_reloads,
