@@ -57,7 +57,7 @@ import weakref
 import torch
 
 from ..utils.logging import log_dist
-from .activation_cache import HostActivationCache, _Spilled
+from .activation_cache import HostActivationCache, _Spilled, default_host_budget_gib
 from ..ops.hostcopy import d2h_
 from .pinned import PinnedPool
 
@@ -235,8 +235,7 @@ class PlannedActivationCache(HostActivationCache):
             budget = int(gib * 2**30) if gib > 0 else int(0.92 * total)
         hgib = float(getattr(cfg, "host_budget_gib", 0.0) or 0.0)
         if hgib <= 0:
-            import psutil
-            hgib = min(0.4 * psutil.virtual_memory().total / 2**30, 160.0)
+            hgib = default_host_budget_gib()
         wgib = float(getattr(cfg, "copy_window_gib", 0.0) or 0.0)
         return cls(device, spill_cost_ms_per_gb=float(getattr(cfg, "spill_cost_ms_per_gb", 0.6)),
                    forced=getattr(cfg, "forced_actions", None),

@@ -64,6 +64,14 @@ from ..ops.hostcopy import d2h_
 from .pinned import PinnedPool
 
 
+def default_host_budget_gib():
+    """Pinned host bytes one rank's cache may hold: 40 % of the host's RAM (at most 160 GiB) shared by the ranks
+    running on this node -- eight GPUs spill into one host's DRAM."""
+    import psutil
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return min(0.4 * psutil.virtual_memory().total / 2**30 / local, 160.0)
+
+
 class _Spilled:
     __slots__ = ("host", "shape", "dtype", "device", "layer", "d2h_done", "dev", "h2d_done", "stride_ok")
 
@@ -153,8 +161,7 @@ class HostActivationCache:
             budget = int(gib * 2**30) if gib > 0 else int(0.92 * total)
         hgib = float(getattr(cfg, "host_budget_gib", 0.0) or 0.0)
         if hgib <= 0:
-            import psutil
-            hgib = min(0.4 * psutil.virtual_memory().total / 2**30, 160.0)
+            hgib = default_host_budget_gib()
         wgib = float(getattr(cfg, "copy_window_gib", 0.0) or 0.0)
         return cls(device, min_bytes=1 << 20, min_layers_resident=cfg.min_layers_resident,
                    prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget,
