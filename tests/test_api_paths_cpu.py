@@ -24,6 +24,7 @@ PATHS = [
     ("moe.layer", ["MoE"]),
     ("moe.utils", ["split_params_into_different_moe_groups_for_optimizer", "is_moe_param"]),
     ("sequence.layer", ["DistributedAttention"]),
+    ("sequence.cross_entropy", ["vocab_sequence_parallel_cross_entropy"]),
     ("sequence.fpdt_layer", ["FPDT_Attention", "FPDT_FFN", "FPDT_LogitsLoss", "FPDTInputConstruct"]),
     ("ops.adam", ["FusedAdam", "DeepSpeedCPUAdam"]),
     ("ops.lamb", ["FusedLamb"]),

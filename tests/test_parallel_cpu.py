@@ -245,3 +245,27 @@ def _sp_llama_uneven(rank, world):
 
 def test_ulysses_llama_gqa_fewer_kv_heads_than_ranks():
     run_distributed(_sp_llama_uneven, 4)
+
+
+def _sp_ce(rank, world):
+    from hcache_deepspeed_amd.sequence.cross_entropy import vocab_sequence_parallel_cross_entropy
+    from hcache_deepspeed_amd.utils import groups
+    groups.initialize(sp=world)
+    grp = groups._get_sequence_parallel_group()
+    torch.manual_seed(0)
+    S, B, V = 8, 3, 11
+    logits = torch.randn(S, B, V, requires_grad=True)
+    target = torch.randint(0, V, (S, B))
+    ref = torch.nn.functional.cross_entropy(logits.view(-1, V), target.view(-1), reduction="none").view(S, B)
+    gout = torch.randn(S, B)
+    ref.backward(gout)
+    sl = slice(rank * S // world, (rank + 1) * S // world)
+    mine = logits.detach()[sl].clone().requires_grad_(True)
+    loss = vocab_sequence_parallel_cross_entropy(mine, target[sl], grp)
+    assert loss.shape == (S, B) and torch.allclose(loss, ref.detach(), atol=1e-5)
+    loss.backward(gout)
+    assert torch.allclose(mine.grad, logits.grad[sl], atol=1e-5)
+
+
+def test_vocab_sequence_parallel_cross_entropy():
+    run_distributed(_sp_ce, 2)
