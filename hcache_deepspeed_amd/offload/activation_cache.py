@@ -92,8 +92,9 @@ class HostActivationCache:
 
     def __init__(self, device, min_bytes=1 << 20, min_layers_resident=2, prefetch_layers=1,
                  gpu_budget_bytes=None, host_budget_bytes=None, copy_window_bytes=None, recompute=False,
-                 ckpt_offload=False, hybrid=False, spill_overlap=0.5):
+                 ckpt_offload=False, hybrid=False, spill_overlap=0.5, stash_attention=True):
         self.device = device
+        self.stash_attention = bool(stash_attention)  # ckpt_offload: keep attention outputs, skip FA in recompute
         self.hybrid = bool(hybrid)  # policy "auto": recompute plan, then the earliest blocks switch to spilling
         self.policy_recompute = bool(recompute) or self.hybrid
         self.ckpt_offload = bool(ckpt_offload)
@@ -169,7 +170,8 @@ class HostActivationCache:
                    recompute=getattr(cfg, "policy", "budget") == "recompute",
                    ckpt_offload=getattr(cfg, "policy", "budget") == "ckpt_offload",
                    hybrid=getattr(cfg, "policy", "budget") == "auto",
-                   spill_overlap=float(getattr(cfg, "spill_overlap", 0.5)))
+                   spill_overlap=float(getattr(cfg, "spill_overlap", 0.5)),
+                   stash_attention=bool(getattr(cfg, "stash_attention", True)))
 
     # ---------------------------------------------------------------------------------------
     def attach(self, model):
@@ -187,18 +189,20 @@ class HostActivationCache:
                 b.forward = self._ckpt_offload_wrapper(b.forward)
         return self
 
-    @staticmethod
-    def _ckpt_offload_wrapper(fwd):
+    def _ckpt_offload_wrapper(self, fwd):
         from ..runtime.activation_checkpointing import checkpointing as ck
+        stash = self.stash_attention
 
         def run(*args, **kwargs):
             if not torch.is_grad_enabled():
                 return fwd(*args, **kwargs)
             if any(torch.is_tensor(v) and v.requires_grad for v in kwargs.values()):
                 return ck.checkpoint(fwd, *args, **kwargs)  # still recomputed; such inputs stay on the device
+            # the attention output + LSE are saved (and spilled) too: the recompute replays them and skips the
+            # FlashAttention forward -- at 128k tokens most of a block's recompute for ~1/3 more spilled bytes
             if kwargs:
-                return ck.checkpoint_saved_inputs(functools.partial(fwd, **kwargs), *args)
-            return ck.checkpoint_saved_inputs(fwd, *args)
+                return ck.checkpoint_saved_inputs(functools.partial(fwd, **kwargs), *args, stash_attention=stash)
+            return ck.checkpoint_saved_inputs(fwd, *args, stash_attention=stash)
 
         return run
 

@@ -256,6 +256,26 @@ def flash_attn(q, k, v, causal=True, softmax_scale=None, cu_seqlens=None, window
     return (o, lse) if return_lse else o
 
 
+class AttnStash:
+    """Attention outputs carried from a checkpointed forward to its recompute (FlashAttention is the costliest part of
+    recomputing a block, and its output + LSE are a small part of the block's bytes). ``record``: every attention call
+    appends its (o, lse); ``replay``: every attention call takes the next stored pair instead of running the forward
+    kernel -- the recompute then re-runs only the projections, norms and MLP
+    (runtime/activation_checkpointing/checkpointing.checkpoint_saved_inputs(stash_attention=True))."""
+    mode = None  # None | "record" | "replay"
+    items = None
+
+    @classmethod
+    def active(cls):
+        return cls.mode is not None
+
+
+def _stash_take(T, n_q, D, dtype, device):
+    o, lse = AttnStash.items.pop(0)
+    assert o.shape[0] == T and o.numel() == T * n_q * D and o.dtype == dtype, "attention stash out of order"
+    return o.view(T, n_q, D), lse
+
+
 def _qkv_recipe(proj, NH, D, n_rot, cos, sin, seq_len, pos_ids):
     """The packed qkv tensor attention saved: the projection's recipe, then RoPE in place (as in forward)."""
 
@@ -281,12 +301,16 @@ class _QKVAttnFn(torch.autograd.Function):
         k = qkv[:, n_q:n_q + n_kv]
         v = qkv[:, n_q + n_kv:]
         cu, B, sl, max_len = _cu_info(cu_seqlens, T, seq_len)
-        if native_supported(qkv):
+        if AttnStash.mode == "replay":
+            o, lse = _stash_take(T, n_q, D, qkv.dtype, qkv.device)
+        elif native_supported(qkv):
             o = torch.empty(T, n_q, D, device=qkv.device, dtype=qkv.dtype)
             lse = torch.empty(n_q, T, device=qkv.device, dtype=torch.float32)
             _native_fwd(q, k, v, o, lse, causal, scale, cu, B, sl, max_len, window)
         else:
             o, lse = _ref_attention(q, k, v, causal, scale, cu_seqlens, seq_len, window)
+        if AttnStash.mode == "record":
+            AttnStash.items.append((o, lse))
         if _ap.tracking():  # per-tensor activation plan: qkv = RoPE(projection), recomputable; o / LSE are not
             if tagged is not None and tagged.fn is not None:
                 _ap.tag(qkv, "qkv", fn=_qkv_recipe(tagged.fn, NH, D, n_q + n_kv, cos, sin, seq_len, pos_ids),

@@ -243,31 +243,51 @@ class _SavedInputCheckpoint(torch.autograd.Function):
     (runtime/activation_checkpointing/checkpointing.py:474-486), here asynchronous via the cache's copy stream."""
 
     @staticmethod
-    def forward(ctx, run, n_out_hint, *args):
+    def forward(ctx, run, stash_attention, *args):
+        from ...ops.attention import AttnStash
         ctx.run = run
         ctx.grad_idx = [i for i, a in enumerate(args) if torch.is_tensor(a) and a.requires_grad]
         ctx.others = [None if i in ctx.grad_idx else a for i, a in enumerate(args)]
-        ctx.save_for_backward(*[args[i] for i in ctx.grad_idx])
         ctx.cpu_rng = torch.get_rng_state()
         ctx.dev_rng = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
-        with torch.no_grad():
-            out = run(*args)
+        stash = []
+        prev = (AttnStash.mode, AttnStash.items)
+        if stash_attention:
+            AttnStash.mode, AttnStash.items = "record", stash
+        try:
+            with torch.no_grad():
+                out = run(*args)
+        finally:
+            AttnStash.mode, AttnStash.items = prev
+        ctx.n_stash = len(stash)
+        # the attention outputs go through save_for_backward next to the inputs: an enclosing host activation cache
+        # spills them like the inputs (ckpt_offload), and the recompute replays them instead of re-running attention
+        ctx.save_for_backward(*[args[i] for i in ctx.grad_idx], *[t for pair in stash for t in pair])
         ctx.tuple_out = isinstance(out, tuple)
         return out
 
     @staticmethod
     def backward(ctx, *gouts):
+        from ...ops.attention import AttnStash
         saved = ctx.saved_tensors
+        n_in = len(saved) - 2 * ctx.n_stash
         args = list(ctx.others)
-        for i, t in zip(ctx.grad_idx, saved):
+        for i, t in zip(ctx.grad_idx, saved[:n_in]):
             args[i] = t.detach().requires_grad_(True)
+        stash = [(saved[n_in + 2 * j], saved[n_in + 2 * j + 1]) for j in range(ctx.n_stash)]
         devs = [torch.cuda.current_device()] if ctx.dev_rng is not None else []
-        with torch.random.fork_rng(devices=devs):
-            torch.set_rng_state(ctx.cpu_rng)
-            if ctx.dev_rng is not None:
-                torch.cuda.set_rng_state(ctx.dev_rng)
-            with torch.enable_grad():
-                out = ctx.run(*args)
+        prev = (AttnStash.mode, AttnStash.items)
+        if ctx.n_stash:
+            AttnStash.mode, AttnStash.items = "replay", stash
+        try:
+            with torch.random.fork_rng(devices=devs):
+                torch.set_rng_state(ctx.cpu_rng)
+                if ctx.dev_rng is not None:
+                    torch.cuda.set_rng_state(ctx.dev_rng)
+                with torch.enable_grad():
+                    out = ctx.run(*args)
+        finally:
+            AttnStash.mode, AttnStash.items = prev
         outs = out if ctx.tuple_out else (out, )
         pairs = [(o, g) for o, g in zip(outs, gouts) if torch.is_tensor(o) and o.requires_grad and g is not None]
         if pairs:
@@ -275,10 +295,12 @@ class _SavedInputCheckpoint(torch.autograd.Function):
         return (None, None) + tuple(args[i].grad if i in ctx.grad_idx else None for i in range(len(args)))
 
 
-def checkpoint_saved_inputs(function, *args):
+def checkpoint_saved_inputs(function, *args, stash_attention=False):
     """Recompute ``function(*args)`` in backward; its differentiable tensor inputs are saved through
-    ``save_for_backward`` (host-cache visible, see ``_SavedInputCheckpoint``). Positional arguments only."""
-    return _SavedInputCheckpoint.apply(function, 0, *args)
+    ``save_for_backward`` (host-cache visible, see ``_SavedInputCheckpoint``). Positional arguments only.
+    ``stash_attention``: also keep every attention call's output + LSE (``ops.attention.AttnStash``) and replay them
+    in the recompute, which then skips the FlashAttention forward -- at long context most of a block's recompute."""
+    return _SavedInputCheckpoint.apply(function, bool(stash_attention), *args)
 
 
 # ---------------------------------------------------------------------------------------------

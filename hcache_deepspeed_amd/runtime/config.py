@@ -180,6 +180,9 @@ class HostActCacheConfig:
     # policy "plan" (offload/act_plan.py): per-tensor keep / spill / recompute. The modelled cost of a hidden spill
     # (concurrent kernels slow down while a copy runs), and optional fixed {tensor class: action} overrides
     spill_cost_ms_per_gb: float = 0.6
+    # policy "ckpt_offload": also keep (and spill) each block's attention output + LSE so the recompute skips the
+    # FlashAttention forward
+    stash_attention: bool = True
     forced_actions: Optional[dict] = None
 
 

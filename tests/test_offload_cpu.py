@@ -361,3 +361,42 @@ def test_auto_policy_splits_recompute_plan_by_pcie_budget():
     c._hybrid_state = 1
     c._hybrid_split()
     assert c.plan == set(range(6)) and c.recompute == set(range(6, 10)) and c._hybrid_state == 2
+
+
+@pytest.mark.parametrize("stash", [False, True])
+def test_ckpt_offload_attention_stash_exact(stash):
+    """policy ckpt_offload with stash_attention: the recompute replays the forward's attention output + LSE instead
+    of running attention again -- gradients identical to the plain model; the replay consumes every stashed pair."""
+    import torch
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    from hcache_deepspeed_amd.ops import attention as A
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(num_hidden_layers=3, vocab_size=128, hidden_size=64, intermediate_size=96,
+                              num_attention_heads=4, num_key_value_heads=2, head_dim=16))
+    x = torch.randint(0, 128, (2, 16))
+    loss = m(x, labels=x)
+    loss.backward()
+    ref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    cache = HostActivationCache(torch.device("cpu"), ckpt_offload=True, stash_attention=stash).attach(m)
+    calls = {"fwd": 0}
+    orig = A._ref_attention
+
+    def counting(*a, **k):
+        calls["fwd"] += 1
+        return orig(*a, **k)
+
+    A._ref_attention = counting
+    try:
+        with cache.forward_context():
+            loss2 = m(x, labels=x)
+        loss2.backward()
+    finally:
+        A._ref_attention = orig
+    assert torch.equal(loss, loss2)
+    for n, p in m.named_parameters():
+        torch.testing.assert_close(p.grad, ref[n], rtol=0, atol=0, msg=n)
+    # 3 blocks: forward once each; the recompute runs attention again only without the stash
+    assert calls["fwd"] == (3 if stash else 6), calls
+    assert A.AttnStash.mode is None
