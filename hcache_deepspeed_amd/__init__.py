@@ -10,6 +10,14 @@ Reference parity: deepspeed/__init__.py (``initialize`` :69-230, ``add_config_ar
 ``init_inference`` :284-366, ``tp_model_init`` :369-398).
 """
 import argparse
+import os
+
+# Device->host copies (activation spills, HCache latents) run as the HIP runtime's blit kernel, which otherwise spreads
+# one copy over as many workgroups as it has chunks and takes CUs from the kernels it overlaps: a 32k-token Llama-3-8B
+# step spilling 25 GiB ran its forward 56 % longer. PCIe bounds the copy, so 16 workgroups still saturate it, and with
+# this limit the measured cost of a spill is ~0.01 ms per GB (profiles/r4/copy_engine_ab_r4f.txt). The runtime reads
+# it when HIP initialises (the first device call), so it is set at import; an explicit value is kept.
+os.environ.setdefault("DEBUG_CLR_LIMIT_BLIT_WG", "16")
 
 from .version import __version__, __version_major__, __version_minor__, __version_patch__  # noqa: F401
 from . import comm  # noqa: F401

@@ -1,11 +1,11 @@
-// Device -> pinned-host copy by a kernel with a SMALL, fixed number of workgroups.
+// Device -> pinned-host copy by a kernel with a SMALL, fixed number of workgroups (opt-in: ops/hostcopy.py HDS_D2H_WG).
 //
-// Why: on this ROCm stack a hipMemcpyAsync device->host runs as the runtime's blit kernel (__amd_rocclr_copyBuffer),
-// which spreads over as many workgroups as the copy has chunks. Activation spills overlap compute by design, and a
-// wide blit grid takes CUs from the FlashAttention / GEMM kernels it runs beside: in a 32k-token step that spills
-// ~25 GB, the forward stretched from 708 to 1103 ms while the GPU stayed 99.8 % busy (profiles/r4/). PCIe (~56 GB/s),
-// not the CU count, bounds the copy, so a handful of workgroups streaming 16-byte vectors saturate the link; they hold
-// few registers and no LDS, so the compute kernels' waves keep co-residing on those CUs.
+// On this ROCm stack a hipMemcpyAsync device->host runs as the runtime's blit kernel (__amd_rocclr_copyBuffer), which
+// spreads over as many workgroups as the copy has chunks and takes CUs from the FlashAttention / GEMM kernels an
+// activation spill overlaps: a 32k-token step spilling ~25 GB stretched its forward from 708 to 1103 ms at 99.8 % GPU
+// busy. PCIe (~56 GB/s), not the CU count, bounds the copy, so few workgroups suffice. Measured in situ, though, the
+// runtime blit LIMITED to 8-32 workgroups (DEBUG_CLR_LIMIT_BLIT_WG, set by the package) cost ~0.01 ms of forward per
+// spilled GB and this kernel ~14 (profiles/r4/copy_engine_ab_r4f.txt), so the limited blit is the default.
 //
 // The host buffer is hipHostMalloc memory mapped into the GPU address space; stores are non-temporal (no L2
 // allocation for data the GPU never reads back) and each thread ends with a system-scope fence, so the bytes are in

@@ -1,8 +1,10 @@
 """Device -> pinned-host copies for the activation spills (csrc/kernels/hostcopy.hip).
 
-``d2h_(dst_host, src_dev)`` copies with a kernel of ``HDS_D2H_WG`` workgroups (default 16) on the CURRENT stream
-instead of hipMemcpyAsync, whose device->host path on this ROCm stack is a blit kernel spread over many workgroups
-that slows the compute kernels it overlaps (see the kernel file). ``HDS_D2H_WG=0`` restores ``copy_``.
+``d2h_(dst_host, src_dev)`` copies on the CURRENT stream. Default (``HDS_D2H_WG=0``): ``copy_``, i.e. the runtime's
+blit kernel, with its workgroup count limited at import (``DEBUG_CLR_LIMIT_BLIT_WG``, package ``__init__``).
+``HDS_D2H_WG=n`` runs the own n-workgroup kernel instead (csrc/kernels/hostcopy.hip). Measured in situ (32k plan,
+profiles/r4/copy_engine_ab_r4f.txt) the own kernel cost the overlapped forward ~14 ms per spilled GB against
+~0.01-0.06 for the limited runtime blit at 8-32 workgroups, so it is not the default.
 """
 import os
 
@@ -10,7 +12,7 @@ import torch
 
 from . import native
 
-D2H_WG = int(os.environ.get("HDS_D2H_WG", "16"))
+D2H_WG = int(os.environ.get("HDS_D2H_WG", "0"))
 
 
 def d2h_(dst, src, n_wg=None):

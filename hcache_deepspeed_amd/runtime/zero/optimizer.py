@@ -1348,8 +1348,10 @@ class ZeroOptimizer:
         self.boundary = boundary
         self.in_backward = True
         so = self.state_offload
-        if so is not None and boundary and (so.reload_pos is None or not self._fwd_trace or self._recording):
-            so.reload()  # no planned position: the whole backward hides the H2D
+        if so is not None and boundary:
+            # no compiled position: reload what fits now; the rest follows state by state as backward frees HBM
+            # (state_offload.on_backward_position) and step() waits for everything
+            so.on_backward_position(None)
         for u in self.units:
             u.pending = u.requires_grad_count
             u.grads_reduced = False

@@ -152,7 +152,7 @@ class OptimizerStateOffload:
         if not self.offloaded or self.reloading:
             return
         if self.reload_pos is not None:  # placed by the compiled schedule (compile/passes.plan_state_reload)
-            if pos <= self.reload_pos:
+            if pos is not None and pos <= self.reload_pos:
                 self.reload()
             return
         if not self.cuda:
