@@ -2,7 +2,7 @@
 # the blit limit; GPU tests of the cache
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-export DEBUG_CLR_LIMIT_BLIT_WG=16 HDS_D2H_WG=0
+# the package sets DEBUG_CLR_LIMIT_BLIT_WG=16 itself
 mkdir -p gpurun_out/r4g
 run() {
   "$@"; rc=$?
@@ -19,3 +19,4 @@ run timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --output-form
 run python3 tools/r4/step_timeline.py gpurun_out/r4g/plan32k > gpurun_out/r4g/plan32k_timeline.txt 2>&1
 run python3 tools/r3/trace_step_stats.py gpurun_out/r4g/plan32k > gpurun_out/r4g/plan32k_kernels.txt 2>&1
 find gpurun_out/r4g -name "*.csv" -size +40M -delete
+run timeout -k 10 300 python -u bench.py --micro-batch 10 --steps 4 --warmup 3 --offload-opt-states > gpurun_out/r4g/mb10_offstates100.log 2>&1
