@@ -35,7 +35,8 @@ def main():
     s = s.masked_fill(torch.triu(torch.ones(S, S, device="cuda", dtype=torch.bool), 1), float("-inf"))
     ref = (torch.softmax(s, -1) @ vf).transpose(0, 1)
     base = None
-    for var in (2, 4, 5, 2, 5):
+    vs = [int(x) for x in sys.argv[1].split(',')] if len(sys.argv) > 1 else [2, 4, 5, 2, 5]
+    for var in vs:
         lib.hds_attn_fwd_variant(var)
         o = flash_attn(q, k, v, causal=True)
         t = timeit(lambda: flash_attn(q, k, v, causal=True))
@@ -49,7 +50,7 @@ def main():
     do = torch.randn_like(q)
     qg, kg, vg = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
     grads0 = None
-    for prio in (1,):
+    for prio in (() if len(sys.argv) > 2 else (1,)):
         lib.hds_attn_bwd_prio(prio)
 
         def fb():
