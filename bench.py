@@ -18,6 +18,10 @@ import os
 import sys
 import time
 
+# device->host copies (activation spills) as blit kernels of at most 16 workgroups -- set before torch loads the HIP
+# runtime (hcache_deepspeed_amd/__init__.py)
+os.environ.setdefault("DEBUG_CLR_LIMIT_BLIT_WG", "16")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -262,9 +262,39 @@ __device__ __forceinline__ void stage_tile_dw(char* tile, RowPtr row_ptr, int wi
   }
 }
 
-// store 32-column block dt of a lane's accumulator row (column = 32dt + 8g + 4h + j) with scale; cols >= D skipped
+// store 32-column block dt of a lane's accumulator row (column = 32dt + 8g + 4h + j) with scale; cols >= D skipped.
+// Lanes i and i+32 hold the two halves of every 8-column group of the SAME row, so one v_permlane32_swap per dword
+// pairs group g of both halves in lanes 0-31 and group g+1 in lanes 32-63: two 16-B stores per block instead of four
+// 8-B ones (guide T21: the epilogue tail is store-issue bound). Both lanes of a pair always share the row (and hence
+// the branch taken here and the caller's row-validity test), as the swap requires.
 template <int D>
 __device__ __forceinline__ void store_row_block(bf16* dst, const f32x16& acc, int dt, int h, float mul) {
+#ifndef HDS_NARROW_STORES  // A/B switch (ops/build.py file_flags): the 8-B stores only
+  if constexpr (D % 32 == 0) {
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      u32x2 w[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = (bf16)(acc[4 * g + j] * mul);
+        w[g] = __builtin_bit_cast(u32x2, v4);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto r = __builtin_amdgcn_permlane32_swap(w[k][d], w[k + 1][d], false, false);
+          w[k][d] = r[0];
+          w[k + 1][d] = r[1];
+        }
+        const u32x4 v = {w[k][0], w[k][1], w[k + 1][0], w[k + 1][1]};
+        *reinterpret_cast<u32x4*>(dst + 32 * dt + 8 * k + 8 * h) = v;
+      }
+      return;
+    }
+  }
+#endif
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int col = 32 * dt + 8 * g + 4 * h;

@@ -62,6 +62,7 @@ def build_env(base_env, world_info, node_rank, master_addr, master_port):
                CROSS_RANK=str(node_rank), CROSS_SIZE=str(len(hosts)), LOCAL_SIZE=str(len(world_info[local])))
     env["HIP_VISIBLE_DEVICES"] = ",".join(str(s) for s in world_info[local])
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("DEBUG_CLR_LIMIT_BLIT_WG", "16")  # before the rank loads HIP (hcache_deepspeed_amd/__init__.py)
     return env, mapping[local]
 
 

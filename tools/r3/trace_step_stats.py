@@ -30,7 +30,7 @@ def main(d):
         a = int(r["Start_Timestamp"])
         if a < t0:
             continue
-        name = r["Kernel_Name"].split("(")[0][:90]
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0][:90]
         agg[name][0] += 1
         agg[name][1] += int(r["End_Timestamp"]) - a
     tot = sum(v[1] for v in agg.values())
