@@ -44,8 +44,10 @@ Mechanism:
   less than a spill, then spilling (earliest blocks first, the classes most expensive to recompute first) up to the
   bytes the copy stream drains within ``spill_overlap`` of the forward time measured on the first planned step,
   then recomputing by cost per byte. After every step the measured forward/backward turn-around peak corrects the
-  base estimate, the forward time against the no-spill forward prices what the spills really cost (concurrent
-  copies slow the kernels they overlap), and the plan is recomputed (closed loop).
+  base estimate, the forward time against the no-spill forward measures what the spills really cost (concurrent
+  copies slow the kernels they overlap; a spill whose memory the allocator must wait for stalls it), a step that
+  slowed by more than twice the modelled cost backs the spill capacity off by a quarter, and the plan is recomputed
+  (closed loop).
 
 Reference anchors: FPDT's host chunk spill (sequence/fpdt_layer.py:462-508), CPU activation checkpointing
 (runtime/activation_checkpointing/checkpointing.py:474-486), the DeepCompile offload_activation pass
@@ -217,7 +219,8 @@ class PlannedActivationCache(HostActivationCache):
         self._copy_busy = [0.0, 0]  # ms, bytes of timed calibration copies
         self._copy_evs = []
         self.t_fwd_ms = None
-        self.spill_cost_measured = None  # ms per spilled GB the forward actually slowed down by
+        self.spill_cost_measured = None  # ms per spilled GB the forward actually slowed down by (EMA, reported)
+        self.cap_scale = 1.0  # fraction of the PCIe-time spill capacity the plan may use (backed off when measured)
         self.est_cost_ms = 0.0
         self.step_spill_bytes = 0
         self.step_recomputed = 0
@@ -343,10 +346,18 @@ class PlannedActivationCache(HostActivationCache):
             self.t_fwd_ms = t_last  # forward with no spills: the base of the spill capacity and the spill cost
             self._stage = 3
         elif t_last is not None and self.step_spill_bytes > (1 << 30) and self.t_fwd_ms:
-            # what spilling actually cost: the copies slow the kernels they overlap (measured, not modelled)
+            # what spilling actually cost: the copies slow the kernels they overlap (measured, not modelled). The
+            # cost is not linear in the bytes -- ~0 while the copies hide behind the forward, growing once they do
+            # not (or once the allocator waits on a spill's copy for its memory) -- so a step whose forward slowed
+            # by more than twice the modelled cost backs the spill CAPACITY off by a quarter instead of pricing every
+            # spilled GB higher (which would switch spilling off for good on one slow sample).
             meas = max(0.0, t_last - self.t_fwd_ms) / (self.step_spill_bytes / 1e9)
             self.spill_cost_measured = meas if self.spill_cost_measured is None else \
                 0.5 * (self.spill_cost_measured + meas)
+            if meas > 2 * self.spill_cost:
+                self.cap_scale = max(0.25, 0.75 * self.cap_scale)
+        elif t_last is not None and self.step_spill_bytes <= (1 << 30) and self.t_fwd_ms:
+            self.t_fwd_ms = min(self.t_fwd_ms, t_last)  # a no-spill forward refines the base
         if self._turn_peak is not None:
             # closed loop: the measured turn-around peak corrects the all-off-device base estimate
             kept = sum(b for k, b in self.items.items() if self.actions.get(k, KEEP) == KEEP)
@@ -358,12 +369,12 @@ class PlannedActivationCache(HostActivationCache):
     def spill_capacity(self):
         if not self.pcie_gbps or not self.t_fwd_ms:
             return 0
-        return int(self.spill_overlap * self.t_fwd_ms * 1e-3 * self.pcie_gbps * 1e9)
+        return int(self.cap_scale * self.spill_overlap * self.t_fwd_ms * 1e-3 * self.pcie_gbps * 1e9)
 
     def _replan(self, spill_cap=None):
         cap = self.spill_capacity() if spill_cap is None else spill_cap
         no_spill = range(self.n_layers - self.keep, self.n_layers)
-        cost = max(self.spill_cost, self.spill_cost_measured or 0.0)
+        cost = self.spill_cost
         new, self.est_cost_ms = plan_tensors(self.items, self._peak_all, self.budget, self.rec_ms, cap, cost,
                                              no_spill)
         if new != self.actions:
@@ -595,7 +606,7 @@ class PlannedActivationCache(HostActivationCache):
                   "recomputed_tensors_step": self.step_recomputed, "est_recompute_ms": round(self.est_cost_ms, 1),
                   "recipe_ms": {k: round(v, 3) for k, v in sorted(self.rec_ms.items())},
                   "t_fwd_ms": None if self.t_fwd_ms is None else round(self.t_fwd_ms, 1),
-                  "spill_cost_ms_per_gb": round(max(self.spill_cost, self.spill_cost_measured or 0.0), 3),
+                  "spill_cost_ms_per_gb": round(self.spill_cost, 3), "spill_cap_scale": round(self.cap_scale, 3),
                   "spill_cost_measured": None if self.spill_cost_measured is None else
                   round(self.spill_cost_measured, 3),
                   "spill_cap_gib": round(self.spill_capacity() / 2**30, 1), "replans": self.replans,

@@ -148,3 +148,40 @@ def test_calibration_step_times_recipes_without_consuming():
         torch.testing.assert_close(g[n], ref[n], rtol=0, atol=0, msg=n)
     assert {"norm_out#0", "resid#1", "linear_out#0", "glu_out#0", "qkv#0"} <= set(cache.rec_ms), cache.rec_ms
     assert cache._cal_items and cache.bytes_offloaded > 0
+
+
+def test_closed_loop_backs_off_capacity_not_price():
+    """A spilling step whose forward slowed by more than twice the modelled cost shrinks the spill capacity by a
+    quarter (floor 1/4) and keeps the per-GB price; a no-spill forward refines the base forward time."""
+
+    class _Ev:
+        def __init__(self, ms):
+            self.ms = ms
+
+        def synchronize(self):
+            pass
+
+        def elapsed_time(self, other):
+            return other.ms - self.ms
+
+    c = PlannedActivationCache(torch.device("cpu"), spill_cost_ms_per_gb=0.6)
+    c._stage, c.t_fwd_ms, c.pcie_gbps = 3, 700.0, 56.0
+    c.items, c._peak_all, c.budget, c.actions = {}, 0, 1 << 40, {}
+    cap0 = c.spill_capacity()
+    for slow_ms, scale in ((60.0, 0.75), (5.0, 0.75), (90.0, 0.5625)):
+        c.step_spill_bytes = 29 * 10**9
+        c._fwd_ev = (_Ev(0.0), _Ev(700.0 + slow_ms))
+        c._turn_peak = None
+        c._advance_plan()
+        assert c.cap_scale == pytest.approx(scale)
+        assert c.spill_cost == 0.6
+    assert c.spill_capacity() == pytest.approx(0.5625 * cap0, rel=1e-6)
+    for _ in range(10):
+        c.step_spill_bytes = 29 * 10**9
+        c._fwd_ev = (_Ev(0.0), _Ev(900.0))
+        c._advance_plan()
+    assert c.cap_scale == 0.25
+    c.step_spill_bytes = 0
+    c._fwd_ev = (_Ev(0.0), _Ev(650.0))
+    c._advance_plan()
+    assert c.t_fwd_ms == 650.0
