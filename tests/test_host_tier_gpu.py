@@ -56,6 +56,37 @@ def test_host_activation_cache_matches_resident():
         assert rel < 2e-2, (n, rel)
 
 
+def test_unconsumed_prefetch_is_ordered_before_reuse():
+    """A forward whose backward never runs, with its spilled tensors' H2D prefetches in flight: the next forward's
+    cleanup orders the compute stream after those copies before their device buffers go back to the allocator, so
+    the next step (which reuses the blocks at once) still computes exact gradients (unconsumed prefetch)."""
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(num_hidden_layers=6)).cuda().to(torch.bfloat16)
+    x1 = torch.randint(0, 512, (2, 512), device="cuda")
+    x2 = torch.randint(0, 512, (2, 512), device="cuda")
+    m(x2, labels=x2).backward()
+    ref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    for p in m.parameters():
+        p.grad = None
+    cache = HostActivationCache(torch.device("cuda"), min_bytes=1 << 16, min_layers_resident=1).attach(m)
+    with cache.forward_context():
+        m(x1, labels=x1)  # no backward
+    pending = [o for lst in cache.by_layer.values() for o in lst]
+    assert pending
+    for o in pending:
+        cache._prefetch(o)  # H2D copies in flight, never unpacked
+    assert any(o.dev is not None for o in pending)
+    with cache.forward_context():
+        loss2 = m(x2, labels=x2)
+    assert all(o.dev is None and o.host is None for o in pending)  # released (after their copies)
+    loss2.backward()
+    for n, p in m.named_parameters():
+        rel = ((p.grad.float() - ref[n].float()).norm() / (ref[n].float().norm() + 1e-12)).item()
+        assert rel < 2e-2, (n, rel)
+
+
 def test_ckpt_offload_policy_matches_resident():
     """policy "ckpt_offload": every block recomputed in backward from inputs that were spilled to pinned host memory
     and prefetched back; gradients match the resident run at bf16 resolution."""
