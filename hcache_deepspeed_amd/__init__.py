@@ -15,8 +15,13 @@ import os
 # Device->host copies (activation spills, HCache latents) run as the HIP runtime's blit kernel, which otherwise spreads
 # one copy over as many workgroups as it has chunks and takes CUs from the kernels it overlaps: a 32k-token Llama-3-8B
 # step spilling 25 GiB ran its forward 56 % longer. PCIe bounds the copy, so 16 workgroups still saturate it, and with
-# this limit the measured cost of a spill is ~0.01 ms per GB (profiles/r4/copy_engine_ab_r4f.txt). The runtime reads
-# it when HIP initialises (the first device call), so it is set at import; an explicit value is kept.
+# this limit the measured cost of a spill is ~0.01 ms per GB (profiles/r4/copy_engine_ab_r4f.txt). It only takes
+# effect when it is in the environment before torch loads the HIP runtime (set here after `import torch`, spills
+# measured 2-6 ms/GB: profiles/r4/plan32k_pkg_import_default_r4h.txt), so bench.py and the launcher set it first;
+# this import covers a script that imports the package before torch. An explicit value is kept.
+import sys as _sys
+
+BLIT_LIMIT_EARLY = "DEBUG_CLR_LIMIT_BLIT_WG" in os.environ or "torch" not in _sys.modules
 os.environ.setdefault("DEBUG_CLR_LIMIT_BLIT_WG", "16")
 
 from .version import __version__, __version_major__, __version_minor__, __version_patch__  # noqa: F401

@@ -59,7 +59,7 @@ import time
 import torch
 import torch.nn as nn
 
-from ..utils.logging import log_dist
+from ..utils.logging import log_dist, logger
 from ..ops.hostcopy import d2h_
 from .pinned import PinnedPool
 
@@ -502,6 +502,11 @@ def plan_offload(layer_bytes, peak_all, budget):
 def build_activation_cache(cfg, device):
     """The cache for ``mi355x.host_act_cache`` (``cfg``): policy "plan" is the per-tensor planner
     (offload/act_plan.py), every other policy the block-level cache above."""
+    from .. import BLIT_LIMIT_EARLY
+    if device.type == "cuda" and not BLIT_LIMIT_EARLY:
+        logger.warning("host activation cache: DEBUG_CLR_LIMIT_BLIT_WG was not in the environment before torch was "
+                       "imported, so activation spills run as unlimited blit kernels that slow the overlapped "
+                       "forward; export DEBUG_CLR_LIMIT_BLIT_WG=16 (the launcher does) for spill-heavy plans")
     if getattr(cfg, "policy", "budget") == "plan":
         from .act_plan import PlannedActivationCache
         return PlannedActivationCache.from_config(cfg, device)
