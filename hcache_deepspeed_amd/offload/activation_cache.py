@@ -146,6 +146,7 @@ class HostActivationCache:
         self.late_unpacks = 0
         self.guard_spills = 0
         self.host_capped_bytes = 0
+        self.stashed_blocks = 0  # ckpt_offload blocks whose attention output was stashed in the last forward
         self._capped_this_step = 0
         self._attached = []
         self._cal_bytes = {}  # per-layer eligible bytes measured by the calibration step
@@ -199,12 +200,24 @@ class HostActivationCache:
             if any(torch.is_tensor(v) and v.requires_grad for v in kwargs.values()):
                 return ck.checkpoint(fwd, *args, **kwargs)  # still recomputed; such inputs stay on the device
             # the attention output + LSE are saved (and spilled) too: the recompute replays them and skips the
-            # FlashAttention forward -- at 128k tokens most of a block's recompute for ~1/3 more spilled bytes
+            # FlashAttention forward -- at 128k tokens most of a block's recompute for ~1/3 more spilled bytes. Only
+            # while the pinned-host budget still holds this stash AND the inputs of every block after it: a stash the
+            # host cap keeps on the device would cost HBM that the longest contexts do not have
+            st = stash and self._stash_fits(args)
+            self.stashed_blocks += int(st)
             if kwargs:
-                return ck.checkpoint_saved_inputs(functools.partial(fwd, **kwargs), *args, stash_attention=stash)
-            return ck.checkpoint_saved_inputs(fwd, *args, stash_attention=stash)
+                return ck.checkpoint_saved_inputs(functools.partial(fwd, **kwargs), *args, stash_attention=st)
+            return ck.checkpoint_saved_inputs(fwd, *args, stash_attention=st)
 
         return run
+
+    def _stash_fits(self, args):
+        if self.host_budget is None:
+            return True
+        inputs = sum(a.numel() * a.element_size() for a in args if torch.is_tensor(a))
+        hidden = next((a.numel() * a.element_size() for a in args if torch.is_tensor(a)), 0)
+        rest = max(0, self.n_layers - max(self.cur_layer, 0) - self.keep) * inputs  # later blocks' spilled inputs
+        return self.host_in_use + rest + int(1.02 * hidden) <= self.host_budget  # o (hidden-sized) + LSE
 
     def _recompute_wrapper(self, fwd, i):
         from ..runtime.activation_checkpointing import checkpointing as ck
@@ -278,6 +291,7 @@ class HostActivationCache:
         self.by_layer = {}
         self.layer_bytes = {}
         self._capped_this_step = 0
+        self.stashed_blocks = 0
         timed = self.hybrid and self._hybrid_state == 1 and self.device.type == "cuda"
         if timed:
             self._fwd_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -449,6 +463,7 @@ class HostActivationCache:
                 "pcie_gbps": None if self.pcie_gbps is None else round(self.pcie_gbps, 1),
                 "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
+                "stashed_blocks": self.stashed_blocks,
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits,
                 "peak_gib_all_steps": round(self.peak_seen / 2**30, 1)}
 

@@ -363,10 +363,11 @@ def test_auto_policy_splits_recompute_plan_by_pcie_budget():
     assert c.plan == set(range(6)) and c.recompute == set(range(6, 10)) and c._hybrid_state == 2
 
 
-@pytest.mark.parametrize("stash", [False, True])
+@pytest.mark.parametrize("stash", [False, True, "host_capped"])
 def test_ckpt_offload_attention_stash_exact(stash):
     """policy ckpt_offload with stash_attention: the recompute replays the forward's attention output + LSE instead
-    of running attention again -- gradients identical to the plain model; the replay consumes every stashed pair."""
+    of running attention again -- gradients identical to the plain model; the replay consumes every stashed pair.
+    "host_capped": a pinned-host budget that cannot hold the stashes -- no block stashes, attention is recomputed."""
     import torch
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
     from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
@@ -379,7 +380,9 @@ def test_ckpt_offload_attention_stash_exact(stash):
     loss.backward()
     ref = {n: p.grad.clone() for n, p in m.named_parameters()}
     m.zero_grad(set_to_none=True)
-    cache = HostActivationCache(torch.device("cpu"), ckpt_offload=True, stash_attention=stash).attach(m)
+    cache = HostActivationCache(torch.device("cpu"), ckpt_offload=True, stash_attention=bool(stash),
+                                host_budget_bytes=1 if stash == "host_capped" else None).attach(m)
+    stash = stash is True
     calls = {"fwd": 0}
     orig = A._ref_attention
 
@@ -399,4 +402,5 @@ def test_ckpt_offload_attention_stash_exact(stash):
         torch.testing.assert_close(p.grad, ref[n], rtol=0, atol=0, msg=n)
     # 3 blocks: forward once each; the recompute runs attention again only without the stash
     assert calls["fwd"] == (3 if stash else 6), calls
+    assert cache.stats()["stashed_blocks"] == (3 if stash else 0)
     assert A.AttnStash.mode is None
