@@ -64,6 +64,8 @@ def main():
                     help="host activation cache policy auto: fraction of the forward the spilled blocks' D2H may take")
     ap.add_argument("--act-cache-budget-gib", type=float, default=0.0,
                     help="host activation cache: HBM budget the planner keeps activations under (0: 92%% of HBM)")
+    ap.add_argument("--act-cache-host-gib", type=float, default=0.0,
+                    help="host activation cache: pinned-host budget (0: 40%% of RAM shared by the node's ranks, <= 160)")
     ap.add_argument("--host-act-cache", action="store_true",
                     help="HCache host activation cache (saved activations spill to pinned host memory)")
     ap.add_argument("--offload", choices=["none", "cpu", "nvme"], default="none",
@@ -149,6 +151,7 @@ def main():
         "mi355x": {"zero3_prefetch_depth": args.prefetch, "comm_stats": False, "host_act_cache": {"enabled": bool(args.host_act_cache), "policy": args.act_cache_policy,
                                                                         "spill_overlap": args.act_cache_spill_overlap,
                                                                         "gpu_budget_gib": args.act_cache_budget_gib,
+                                                                        "host_budget_gib": args.act_cache_host_gib,
                                                                         "spill_cost_ms_per_gb": args.act_cache_spill_cost}},
         "steps_per_print": 1000000,
     }

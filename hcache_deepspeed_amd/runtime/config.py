@@ -175,7 +175,7 @@ class HostActCacheConfig:
     spill_overlap: float = 0.5  # policy "auto": fraction of the forward the spilled blocks' D2H may take
     gpu_budget_gib: float = 0.0  # 0: 92% of device memory
     prefetch_layers: int = 4  # spilled blocks whose H2D starts when backward reaches a later block
-    host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: min(40% of host RAM, 160 GiB))
+    host_budget_gib: float = 0.0  # pinned host bytes the cache may hold (0: 40% of host RAM over the node's ranks, <= 160 GiB)
     copy_window_gib: float = 0.0  # queued-but-unfinished copy bytes per direction (0: from the HBM headroom)
     # policy "plan" (offload/act_plan.py): per-tensor keep / spill / recompute. The modelled cost of a hidden spill
     # (concurrent kernels slow down while a copy runs), and optional fixed {tensor class: action} overrides
