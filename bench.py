@@ -66,6 +66,8 @@ def main():
                     help="host activation cache: HBM budget the planner keeps activations under (0: 92%% of HBM)")
     ap.add_argument("--act-cache-host-gib", type=float, default=0.0,
                     help="host activation cache: pinned-host budget (0: 40%% of RAM shared by the node's ranks, <= 160)")
+    ap.add_argument("--no-attn-stash", action="store_true",
+                    help="host activation cache policy ckpt_offload: recompute attention instead of replaying its output")
     ap.add_argument("--host-act-cache", action="store_true",
                     help="HCache host activation cache (saved activations spill to pinned host memory)")
     ap.add_argument("--offload", choices=["none", "cpu", "nvme"], default="none",
@@ -152,6 +154,7 @@ def main():
                                                                         "spill_overlap": args.act_cache_spill_overlap,
                                                                         "gpu_budget_gib": args.act_cache_budget_gib,
                                                                         "host_budget_gib": args.act_cache_host_gib,
+                                                                        "stash_attention": not args.no_attn_stash,
                                                                         "spill_cost_ms_per_gb": args.act_cache_spill_cost}},
         "steps_per_print": 1000000,
     }

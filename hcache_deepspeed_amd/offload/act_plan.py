@@ -279,6 +279,7 @@ class PlannedActivationCache(HostActivationCache):
         self.by_layer = {}
         self.layer_bytes = {}
         self._capped_this_step = 0
+        self._bwd_layer, self._bwd_mark = None, None
         self._handles, self._occ, self._tags = {}, {}, {}
         timed = cuda and self._stage >= 2 and self.forced is None
         if timed:

@@ -153,6 +153,8 @@ class HostActivationCache:
         self._turn_peak = None  # max allocation at the forward/backward turn-around of the last step
         self.plan_adjustments = 0
         self.peak_seen = 0  # max allocation over every step (the planner resets the peak counter per forward)
+        self.bwd_headroom = None  # largest one-block backward transient seen (bytes), kept free by far prefetches
+        self._bwd_layer, self._bwd_mark = None, None
 
     @classmethod
     def from_config(cls, cfg, device):
@@ -292,6 +294,7 @@ class HostActivationCache:
         self.layer_bytes = {}
         self._capped_this_step = 0
         self.stashed_blocks = 0
+        self._bwd_layer, self._bwd_mark = None, None
         timed = self.hybrid and self._hybrid_state == 1 and self.device.type == "cuda"
         if timed:
             self._fwd_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -344,7 +347,8 @@ class HostActivationCache:
             self.throttle_waits += 1
 
     def _pack(self, t):
-        if (not isinstance(t, torch.Tensor) or not t.is_cuda or t.is_leaf or self.cur_layer < 0
+        if (not isinstance(t, torch.Tensor) or not t.is_cuda or self.cur_layer < 0
+                or (t.is_leaf and not getattr(t, "_hds_activation", False))  # parameters, inputs; not the stash
                 or t.numel() * t.element_size() < self.min_bytes):
             return t
         if self.cur_layer >= self.n_layers - self.keep:
@@ -413,6 +417,16 @@ class HostActivationCache:
     def _prefetch_before(self, layer):
         if self._turn_peak is None and self.device.type == "cuda":
             self._turn_peak = torch.cuda.max_memory_allocated(self.device)  # first unpack of the step
+        if self.budget is not None and self.device.type == "cuda" and layer != self._bwd_layer:
+            # backward reached a new block: the peak since the previous block began, over what was allocated then,
+            # is what one block's backward (recompute intermediates + gradients) needs on top of the live tensors
+            now = torch.cuda.memory_allocated(self.device)
+            if self._bwd_mark is not None:
+                pk = torch.cuda.max_memory_allocated(self.device)
+                self.peak_seen = max(self.peak_seen, pk)
+                self.bwd_headroom = max(self.bwd_headroom or 0, pk - self._bwd_mark)
+                torch.cuda.reset_peak_memory_stats(self.device)
+            self._bwd_layer, self._bwd_mark = layer, now
         # j = 0 first: the rest of THIS block's spilled tensors (a block unpacks several; if the first was late, the
         # others must not queue behind the earlier blocks' prefetches -- a 189 ms stall at 128k ckpt_offload)
         for j in range(0, self.prefetch_layers + 1):
@@ -424,13 +438,16 @@ class HostActivationCache:
             for o in lst:
                 self._prefetch(o)
         if self.budget is not None and self.device.type == "cuda":
-            # further ahead, while the HBM the backward has already freed covers the next spilled layer
+            # further ahead, while the HBM the backward has already freed covers the next spilled layer AND leaves
+            # one block's backward transient free (measured; a quarter of the budget until it has been): at 320k
+            # tokens a block's recompute needs ~60 GB that greedy prefetching would otherwise have taken
+            head = self.bwd_headroom if self.bwd_headroom is not None else self.budget // 4
             for lj in sorted((k for k in self.by_layer if k < layer - self.prefetch_layers), reverse=True):
                 need = sum(o.host.numel() * o.host.element_size() for o in self.by_layer[lj]
                            if o.dev is None and o.host is not None)
                 if need == 0:
                     continue
-                if torch.cuda.memory_allocated(self.device) + need > self.budget:
+                if torch.cuda.memory_allocated(self.device) + need + head > self.budget:
                     break
                 for o in self.by_layer[lj]:
                     self._prefetch(o)
@@ -464,6 +481,7 @@ class HostActivationCache:
                 "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
                 "stashed_blocks": self.stashed_blocks,
+                "bwd_headroom_gib": None if self.bwd_headroom is None else round(self.bwd_headroom / 2**30, 1),
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits,
                 "peak_gib_all_steps": round(self.peak_seen / 2**30, 1)}
 

@@ -261,7 +261,12 @@ class _SavedInputCheckpoint(torch.autograd.Function):
             AttnStash.mode, AttnStash.items = prev
         ctx.n_stash = len(stash)
         # the attention outputs go through save_for_backward next to the inputs: an enclosing host activation cache
-        # spills them like the inputs (ckpt_offload), and the recompute replays them instead of re-running attention
+        # spills them like the inputs (ckpt_offload), and the recompute replays them instead of re-running attention.
+        # Made under no_grad they are autograd leaves, which the cache leaves alone (parameters are leaves too): the
+        # mark says these are activations
+        for pair in stash:
+            for t in pair:
+                t._hds_activation = True
         ctx.save_for_backward(*[args[i] for i in ctx.grad_idx], *[t for pair in stash for t in pair])
         ctx.tuple_out = isinstance(out, tuple)
         return out

@@ -87,9 +87,11 @@ def test_unconsumed_prefetch_is_ordered_before_reuse():
         assert rel < 2e-2, (n, rel)
 
 
-def test_ckpt_offload_policy_matches_resident():
+@pytest.mark.parametrize("stash", [True, False])
+def test_ckpt_offload_policy_matches_resident(stash):
     """policy "ckpt_offload": every block recomputed in backward from inputs that were spilled to pinned host memory
-    and prefetched back; gradients match the resident run at bf16 resolution."""
+    and prefetched back; gradients match the resident run at bf16 resolution. With the attention stash its outputs
+    are spilled too (no-grad outputs are autograd leaves; the cache must still move them off the device)."""
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
     from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
     torch.manual_seed(0)
@@ -101,12 +103,20 @@ def test_ckpt_offload_policy_matches_resident():
     for p in m.parameters():
         p.grad = None
     cache = HostActivationCache(torch.device("cuda"), min_bytes=1 << 16, min_layers_resident=1,
-                                ckpt_offload=True).attach(m)
+                                ckpt_offload=True, stash_attention=stash).attach(m)
     with cache.forward_context():
         loss2 = m(x, labels=x)
+    # spilled per block (5 of 6 blocks; the last stays resident): the residual-stream inputs (block 0 has one, the
+    # others h and residual), plus the attention output with the stash (the LSE is below min_bytes here)
+    per_block = {b: sum(o.host.numel() * o.host.element_size() for o in lst) for b, lst in cache.by_layer.items()}
+    hidden = 2 * 512 * m.config.hidden_size * 2
+    assert sorted(per_block) == [0, 1, 2, 3, 4], per_block
+    for b, v in per_block.items():
+        assert v == ((1 if b == 0 else 2) + int(stash)) * hidden, (b, v, hidden)
     loss2.backward()
     st = cache.stats()
     assert st["bytes_offloaded"] > 0 and st["recomputed_layers"] == 6
+    assert st["stashed_blocks"] == (6 if stash else 0)
     assert torch.allclose(loss, loss2)
     for n, p in m.named_parameters():
         rel = ((p.grad.float() - ref[n].float()).norm() / (ref[n].float().norm() + 1e-12)).item()
