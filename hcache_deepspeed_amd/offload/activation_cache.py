@@ -147,6 +147,9 @@ class HostActivationCache:
         self.guard_spills = 0
         self.host_capped_bytes = 0
         self.stashed_blocks = 0  # ckpt_offload blocks whose attention output was stashed in the last forward
+        self.stash_keep_from = 1 << 30  # blocks from here on keep their stash on the device (_update_stash_keep)
+        self._stash_sb = 0
+        self._steps_seen = 0
         self._capped_this_step = 0
         self._attached = []
         self._cal_bytes = {}  # per-layer eligible bytes measured by the calibration step
@@ -214,12 +217,33 @@ class HostActivationCache:
         return run
 
     def _stash_fits(self, args):
+        hidden = next((a.numel() * a.element_size() for a in args if torch.is_tensor(a)), 0)
+        self._stash_sb = int(1.02 * hidden)  # o (hidden-sized) + LSE
+        if self.cur_layer >= self.stash_keep_from:
+            return True  # this block's stash stays on the device (_update_stash_keep)
         if self.host_budget is None:
             return True
         inputs = sum(a.numel() * a.element_size() for a in args if torch.is_tensor(a))
-        hidden = next((a.numel() * a.element_size() for a in args if torch.is_tensor(a)), 0)
         rest = max(0, self.n_layers - max(self.cur_layer, 0) - self.keep) * inputs  # later blocks' spilled inputs
         return self.host_in_use + rest + int(1.02 * hidden) <= self.host_budget  # o (hidden-sized) + LSE
+
+    def _update_stash_keep(self):
+        """ckpt_offload with the attention stash: the stash goes to host memory like the inputs (needed at 320k
+        tokens), but where the HBM holds it, keeping it on the device saves its round trip over PCIe (128k: ~8 %).
+        From the second step on, the HBM the steps so far left unreserved (92 % of the device minus the peak
+        RESERVED bytes, fragmentation included) keeps the stash of the last blocks on the device; it only grows."""
+        self._steps_seen += 1
+        if not (self.ckpt_offload and self.stash_attention and self.device.type == "cuda" and self._stash_sb
+                and self._steps_seen >= 3):
+            return
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        room = int(0.92 * total) - torch.cuda.max_memory_reserved(self.device)
+        if room > self._stash_sb:
+            keep_from = max(0, self.stash_keep_from - room // self._stash_sb)
+            if keep_from != self.stash_keep_from:
+                log_dist(f"host activation cache: attention stash of blocks {keep_from}..{self.n_layers - 1} stays "
+                         f"on the device ({room / 2**30:.1f} GiB of HBM unreserved)", ranks=[0])
+                self.stash_keep_from = keep_from
 
     def _recompute_wrapper(self, fwd, i):
         from ..runtime.activation_checkpointing import checkpointing as ck
@@ -295,6 +319,7 @@ class HostActivationCache:
         self._capped_this_step = 0
         self.stashed_blocks = 0
         self._bwd_layer, self._bwd_mark = None, None
+        self._update_stash_keep()
         timed = self.hybrid and self._hybrid_state == 1 and self.device.type == "cuda"
         if timed:
             self._fwd_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -351,6 +376,8 @@ class HostActivationCache:
                 or (t.is_leaf and not getattr(t, "_hds_activation", False))  # parameters, inputs; not the stash
                 or t.numel() * t.element_size() < self.min_bytes):
             return t
+        if getattr(t, "_hds_activation", False) and self.cur_layer >= self.stash_keep_from:
+            return _Tagged(t, self.cur_layer) if self.by_layer else t  # a stash the HBM holds
         if self.cur_layer >= self.n_layers - self.keep:
             # kept resident, but tagged once something was spilled: backward touching these last blocks is what
             # starts the prefetch of the latest spilled ones
@@ -481,6 +508,7 @@ class HostActivationCache:
                 "late_unpacks": self.late_unpacks,
                 "guard_spills": self.guard_spills, "host_capped_bytes": self.host_capped_bytes,
                 "stashed_blocks": self.stashed_blocks,
+                "stash_on_device_blocks": max(0, self.n_layers - self.stash_keep_from) if self.ckpt_offload else 0,
                 "bwd_headroom_gib": None if self.bwd_headroom is None else round(self.bwd_headroom / 2**30, 1),
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits,
                 "peak_gib_all_steps": round(self.peak_seen / 2**30, 1)}
