@@ -230,19 +230,21 @@ class HostActivationCache:
     def _update_stash_keep(self):
         """ckpt_offload with the attention stash: the stash goes to host memory like the inputs (needed at 320k
         tokens), but where the HBM holds it, keeping it on the device saves its round trip over PCIe (128k: ~8 %).
-        From the second step on, the HBM the steps so far left unreserved (92 % of the device minus the peak
-        RESERVED bytes, fragmentation included) keeps the stash of the last blocks on the device; it only grows."""
+        From the third step on, the HBM the steps so far left free (85 % of the device minus the peak allocation;
+        the margin covers the caching allocator's fragmentation, which at 128k tokens reserves ~80 GiB more than the
+        peak allocation -- reusable, so the reserved peak would understate the room) keeps the stash of the last
+        blocks on the device; it only grows."""
         self._steps_seen += 1
         if not (self.ckpt_offload and self.stash_attention and self.device.type == "cuda" and self._stash_sb
                 and self._steps_seen >= 3):
             return
         total = torch.cuda.get_device_properties(self.device).total_memory
-        room = int(0.92 * total) - torch.cuda.max_memory_reserved(self.device)
+        room = int(0.85 * total) - torch.cuda.max_memory_allocated(self.device)
         if room > self._stash_sb:
-            keep_from = max(0, self.stash_keep_from - room // self._stash_sb)
+            keep_from = max(0, min(self.stash_keep_from, self.n_layers) - room // self._stash_sb)
             if keep_from != self.stash_keep_from:
                 log_dist(f"host activation cache: attention stash of blocks {keep_from}..{self.n_layers - 1} stays "
-                         f"on the device ({room / 2**30:.1f} GiB of HBM unreserved)", ranks=[0])
+                         f"on the device ({room / 2**30:.1f} GiB of HBM free at the peak)", ranks=[0])
                 self.stash_keep_from = keep_from
 
     def _recompute_wrapper(self, fwd, i):
