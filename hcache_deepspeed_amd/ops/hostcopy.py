@@ -1,14 +1,13 @@
 """Device -> pinned-host copies for the activation spills (csrc/kernels/hostcopy.hip).
 
 ``d2h_(dst_host, src_dev)`` copies on the CURRENT stream. Default (``HDS_D2H_WG=0``): ``copy_``, i.e. the runtime's
-blit kernel, with its workgroup count limited at import (``DEBUG_CLR_LIMIT_BLIT_WG``, package ``__init__``).
+blit kernel, with its workgroup count limited by ``DEBUG_CLR_LIMIT_BLIT_WG`` (in the environment before torch loads
+HIP: bench.py, the launcher; package ``__init__``).
 ``HDS_D2H_WG=n`` runs the own n-workgroup kernel instead (csrc/kernels/hostcopy.hip). Measured in situ (32k plan,
 profiles/r4/copy_engine_ab_r4f.txt) the own kernel cost the overlapped forward ~14 ms per spilled GB against
 ~0.01-0.06 for the limited runtime blit at 8-32 workgroups, so it is not the default.
 """
 import os
-
-import torch
 
 from . import native
 
