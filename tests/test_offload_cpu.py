@@ -404,3 +404,52 @@ def test_ckpt_offload_attention_stash_exact(stash):
     assert calls["fwd"] == (3 if stash else 6), calls
     assert cache.stats()["stashed_blocks"] == (3 if stash else 0)
     assert A.AttnStash.mode is None
+
+
+def test_stash_keep_and_host_fit_decisions(monkeypatch):
+    """ckpt_offload attention stash: blocks stash only while the pinned-host budget holds the stash plus every later
+    block's inputs; from the third step the last blocks keep their stash on the device as far as the measured peak
+    leaves room (85 % of HBM), and that only grows."""
+    import types
+    import torch
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    GB = 1 << 30
+    c = HostActivationCache(torch.device("cpu"), ckpt_offload=True, stash_attention=True, min_layers_resident=1,
+                            host_budget_bytes=100 * GB)
+    c.n_layers = 10
+
+    class _T:  # stand-in tensor: only sizes matter
+        def __init__(self, n):
+            self.n = n
+
+        def numel(self):
+            return self.n
+
+        def element_size(self):
+            return 1
+
+    monkeypatch.setattr(torch, "is_tensor", lambda a: isinstance(a, (_T, torch.Tensor)))
+    args = (_T(4 * GB), _T(4 * GB))  # h and residual: 8 GB of inputs, 4 GB hidden -> ~4.08 GB stash
+    c.cur_layer, c.host_in_use = 0, 0
+    assert c._stash_fits(args)  # 9 blocks x 8 GB + 4.08 <= 100
+    c.cur_layer, c.host_in_use = 3, 50 * GB  # 50 + 6 x 8 + 4.08 > 100
+    assert not c._stash_fits(args)
+    # device keep: steps 1-2 never, then as much as 85 % of HBM minus the peak allows, monotone
+    total = 100 * GB
+    peak = {"v": 70 * GB}
+    c.device = torch.device("cuda")
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: types.SimpleNamespace(total_memory=total))
+    monkeypatch.setattr(torch.cuda, "max_memory_allocated", lambda d=None: peak["v"])
+    import hcache_deepspeed_amd.offload.activation_cache as ac
+    monkeypatch.setattr(ac, "log_dist", lambda *a, **k: None)
+    c._stash_sb = 4 * GB
+    c._update_stash_keep()
+    c._update_stash_keep()
+    assert c.stash_keep_from >= c.n_layers  # not before the third step
+    c._update_stash_keep()  # room 85 - 70 = 15 GB -> 3 blocks
+    assert c.stash_keep_from == 7
+    peak["v"] = 84 * GB
+    c._update_stash_keep()  # room 1 GB: no change (only grows)
+    assert c.stash_keep_from == 7
+    c.cur_layer = 8
+    assert c._stash_fits(args)  # kept on the device: no host check
