@@ -32,18 +32,32 @@ def _f(x):
 # ------------------------------------------------------------------------------------------
 # flat functional forms
 # ------------------------------------------------------------------------------------------
+def _native_lp(p, lp_out):
+    """The flat kernels write their low-precision copy of the updated parameters as bf16: hand them only a bf16
+    target. Any other ``lp_out`` (fp32 training's compute copy, fp16) is refreshed from ``p`` after the kernel --
+    unless it IS ``p``. Returns (kernel target, tensor to copy into afterwards)."""
+    if lp_out is None or lp_out.dtype == torch.bfloat16:
+        return lp_out, None
+    if lp_out.dtype == p.dtype and lp_out.data_ptr() == p.data_ptr():
+        return None, None
+    return None, lp_out
+
+
 def adam_flat(p, g, m, v, step, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, adamw=True, bias_correction=True,
               lp_out=None, grad_scale=1.0, dev_scale=None, found_inf=None):
     b1, b2 = betas
     bc1 = 1 - b1**step if bias_correction else 1.0
     bc2 = 1 - b2**step if bias_correction else 1.0
     if native.use_native(p):
+        lp, after = _native_lp(p, lp_out)
         native.check(
             native.kernels().hds_adam_flat(native.dt(p), native.dt(g), p.data_ptr(), g.data_ptr(), m.data_ptr(),
-                                           v.data_ptr(), native.ptr(lp_out), p.numel(), _f(lr), _f(b1), _f(b2),
+                                           v.data_ptr(), native.ptr(lp), p.numel(), _f(lr), _f(b1), _f(b2),
                                            _f(eps), _f(weight_decay), _f(bc1), _f(bc2), int(adamw), _f(grad_scale),
                                            native.ptr(dev_scale), native.ptr(found_inf), native.stream()),
             "adam_flat")
+        if after is not None:
+            after.copy_(p)
         return
     if found_inf is not None and bool(found_inf.item()):
         return
@@ -67,11 +81,14 @@ def lion_flat(p, g, m, lr, betas=(0.9, 0.99), weight_decay=0.0, lp_out=None, gra
               found_inf=None):
     b1, b2 = betas
     if native.use_native(p):
+        lp, after = _native_lp(p, lp_out)
         native.check(
             native.kernels().hds_lion_flat(native.dt(p), native.dt(g), p.data_ptr(), g.data_ptr(), m.data_ptr(),
-                                           native.ptr(lp_out), p.numel(), _f(lr), _f(b1), _f(b2), _f(weight_decay),
+                                           native.ptr(lp), p.numel(), _f(lr), _f(b1), _f(b2), _f(weight_decay),
                                            _f(grad_scale), native.ptr(dev_scale), native.ptr(found_inf),
                                            native.stream()), "lion_flat")
+        if after is not None:
+            after.copy_(p)
         return
     if found_inf is not None and bool(found_inf.item()):
         return
@@ -89,11 +106,14 @@ def lion_flat(p, g, m, lr, betas=(0.9, 0.99), weight_decay=0.0, lp_out=None, gra
 def adagrad_flat(p, g, s, lr, eps=1e-10, weight_decay=0.0, lp_out=None, grad_scale=1.0, dev_scale=None,
                  found_inf=None):
     if native.use_native(p):
+        lp, after = _native_lp(p, lp_out)
         native.check(
             native.kernels().hds_adagrad_flat(native.dt(p), native.dt(g), p.data_ptr(), g.data_ptr(), s.data_ptr(),
-                                              native.ptr(lp_out), p.numel(), _f(lr), _f(eps), _f(weight_decay),
+                                              native.ptr(lp), p.numel(), _f(lr), _f(eps), _f(weight_decay),
                                               _f(grad_scale), native.ptr(dev_scale), native.ptr(found_inf),
                                               native.stream()), "adagrad_flat")
+        if after is not None:
+            after.copy_(p)
         return
     sc = grad_scale * (dev_scale.item() if dev_scale is not None else 1.0)
     pf = p.float()

@@ -820,3 +820,30 @@ def test_flash_bwd_pipelined_matches_plain_gpu(case):
         for g, r in zip(grads[1], (qf.grad, kf.grad, vf.grad)):
             rel = ((g - r).norm() / r.norm()).item()
             assert rel < 2e-2, (case, rel)
+
+
+@pytest.mark.parametrize("lp_kind", ["bf16", "fp32", "fp32_alias", "fp16"])
+def test_adam_flat_lp_out_dtypes_gpu(lp_kind):
+    """The flat optimizer kernels write a bf16 parameter copy; any other compute copy (fp32 training, fp16) must come
+    out equal to the updated fp32 parameters, never a bf16 bit pattern written into a wider buffer."""
+    from hcache_deepspeed_amd.ops.optimizers import adam_flat
+    torch.manual_seed(0)
+    n = 10_000 + 3
+    p = torch.randn(n, device="cuda")
+    g = torch.randn(n, device="cuda")
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    ref_p = p.clone().cpu()
+    if lp_kind == "fp32_alias":
+        lp = p
+    else:
+        lp = torch.zeros(n, device="cuda", dtype={"bf16": torch.bfloat16, "fp32": torch.float32,
+                                                  "fp16": torch.float16}[lp_kind])
+    adam_flat(p, g, m, v, 1, 1e-2, lp_out=lp, weight_decay=0.01)
+    gc = g.cpu()
+    mm = 0.1 * gc
+    vv = 0.001 * gc * gc
+    upd = (mm / 0.1) / ((vv / 0.001).sqrt() + 1e-8) + 0.01 * ref_p
+    want = ref_p - 1e-2 * upd
+    torch.testing.assert_close(p.cpu(), want, rtol=1e-5, atol=1e-6)
+    tol = {"bf16": 1e-2, "fp16": 1e-3}.get(lp_kind, 1e-6)
+    torch.testing.assert_close(lp.float().cpu(), want, rtol=tol, atol=tol)
