@@ -42,7 +42,7 @@ def _staged(fn_name):
     return call
 
 
-def _run(rank, world, d, steps=3, symmetric=False):
+def _run(rank, world, d, steps=3, symmetric=False, stage=3, dtype="bf16"):
     import hcache_deepspeed_amd as hds
     import hcache_deepspeed_amd.comm as hcomm
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
@@ -57,8 +57,10 @@ def _run(rank, world, d, steps=3, symmetric=False):
     m = LlamaForCausalLM(tiny(**CFG))  # same full weights on every rank; initialize() partitions them
     mb = 4 // world
     cfg = {"train_micro_batch_size_per_gpu": mb, "bf16": {"enabled": True}, "gradient_clipping": 1.0,
-           "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "zero_optimization": {"stage": 3},
+           "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "zero_optimization": {"stage": stage},
            "mi355x": {"comm_stats": True}}
+    if dtype != "bf16":
+        cfg.pop("bf16")
     if symmetric:
         cfg["compile"] = {"symmetric_memory": True}
     eng, _, _, _ = hds.initialize(model=m, config=cfg)
@@ -81,7 +83,7 @@ def _run(rank, world, d, steps=3, symmetric=False):
         losses.append(float(loss))
     if on_gpu:
         torch.cuda.synchronize()
-    if world > 1:
+    if world > 1 and stage == 3:
         summ = z.comm_stats.summary()
         assert summ["collectives"]["all_gather"]["count"] > 0
         assert summ["collectives"]["reduce_scatter"]["count"] > 0
@@ -93,7 +95,7 @@ def _run(rank, world, d, steps=3, symmetric=False):
     ls = torch.tensor(losses)
     torch.distributed.all_reduce(ls)
     if rank == 0:
-        tag = "s" if symmetric else ""
+        tag = ("s" if symmetric else "") + ("" if (stage, dtype) == (3, "bf16") else f"_z{stage}{dtype}")
         torch.save({"losses": (ls / world).tolist(), "weights": full}, os.path.join(d, f"w{world}{tag}.pt"))
 
 
@@ -196,3 +198,20 @@ def test_zero3_symmetric_memory_skipped_collective_fails_loudly(tmp_path):
     run_distributed(_run_skip, 2, d, timeout=300)
     for r in range(2):
         assert torch.load(os.path.join(d, f"skip{r}.pt"), weights_only=True)["ok"]
+
+
+@pytest.mark.parametrize("stage,dtype", [(1, "bf16"), (2, "bf16"), (2, "fp32")])
+def test_zero12_device_path_world2_matches_world1(tmp_path, stage, dtype):
+    """ZeRO-1 / ZeRO-2 (flat reduce-scatter of the gradients, sharded optimizer states, all-gather of the updated
+    parameters) on device tensors at world 2, and fp32 training (the compute copy is the master's dtype)."""
+    d = str(tmp_path)
+    run_distributed(_run, 1, d, 3, False, stage, dtype)
+    run_distributed(_run, 2, d, 3, False, stage, dtype)
+    a = torch.load(os.path.join(d, f"w1_z{stage}{dtype}.pt"), weights_only=True)
+    b = torch.load(os.path.join(d, f"w2_z{stage}{dtype}.pt"), weights_only=True)
+    tol = 2e-2 if dtype == "bf16" else 2e-3
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert abs(la - lb) <= tol * abs(la), (a["losses"], b["losses"])
+    for n, w in a["weights"].items():
+        rel = float((b["weights"][n] - w).norm() / w.norm().clamp_min(1e-12))
+        assert rel < tol, (n, rel)
