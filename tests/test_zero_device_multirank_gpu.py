@@ -61,6 +61,8 @@ def _run(rank, world, d, steps=3, symmetric=False, stage=3, dtype="bf16"):
            "mi355x": {"comm_stats": True}}
     if dtype != "bf16":
         cfg.pop("bf16")
+    if dtype == "fp16":
+        cfg["fp16"] = {"enabled": True, "loss_scale": 0, "initial_scale_power": 12}
     if symmetric:
         cfg["compile"] = {"symmetric_memory": True}
     eng, _, _, _ = hds.initialize(model=m, config=cfg)
@@ -200,16 +202,17 @@ def test_zero3_symmetric_memory_skipped_collective_fails_loudly(tmp_path):
         assert torch.load(os.path.join(d, f"skip{r}.pt"), weights_only=True)["ok"]
 
 
-@pytest.mark.parametrize("stage,dtype", [(1, "bf16"), (2, "bf16"), (2, "fp32")])
+@pytest.mark.parametrize("stage,dtype", [(1, "bf16"), (2, "bf16"), (2, "fp32"), (3, "fp16"), (1, "fp16")])
 def test_zero12_device_path_world2_matches_world1(tmp_path, stage, dtype):
     """ZeRO-1 / ZeRO-2 (flat reduce-scatter of the gradients, sharded optimizer states, all-gather of the updated
-    parameters) on device tensors at world 2, and fp32 training (the compute copy is the master's dtype)."""
+    parameters) on device tensors at world 2; fp32 training (the compute copy is the master's dtype) and fp16 with
+    dynamic loss scaling (fp16 compute copy refreshed from the fp32 master)."""
     d = str(tmp_path)
     run_distributed(_run, 1, d, 3, False, stage, dtype)
     run_distributed(_run, 2, d, 3, False, stage, dtype)
     a = torch.load(os.path.join(d, f"w1_z{stage}{dtype}.pt"), weights_only=True)
     b = torch.load(os.path.join(d, f"w2_z{stage}{dtype}.pt"), weights_only=True)
-    tol = 2e-2 if dtype == "bf16" else 2e-3
+    tol = 2e-3 if dtype == "fp32" else 2e-2
     for la, lb in zip(a["losses"], b["losses"]):
         assert abs(la - lb) <= tol * abs(la), (a["losses"], b["losses"])
     for n, w in a["weights"].items():
