@@ -42,7 +42,7 @@ def _staged(fn_name):
     return call
 
 
-def _run(rank, world, d, steps=3, symmetric=False, stage=3, dtype="bf16"):
+def _run(rank, world, d, steps=3, symmetric=False, stage=3, dtype="bf16", zpp=False):
     import hcache_deepspeed_amd as hds
     import hcache_deepspeed_amd.comm as hcomm
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
@@ -63,6 +63,11 @@ def _run(rank, world, d, steps=3, symmetric=False, stage=3, dtype="bf16"):
         cfg.pop("bf16")
     if dtype == "fp16":
         cfg["fp16"] = {"enabled": True, "loss_scale": 0, "initial_scale_power": 12}
+    if zpp:  # ZeRO++: int8 weight all-gather (qwZ) and the quantized gradient all-to-all reduce (qgZ)
+        cfg["zero_optimization"].update(zero_quantized_weights=True, zero_quantized_gradients=True)
+        from tests.test_moe_device_multirank_gpu import _staged_all_to_all
+        hcomm.all_to_all_single = _staged_all_to_all()
+        hcomm.comm.all_to_all_single = hcomm.all_to_all_single
     if symmetric:
         cfg["compile"] = {"symmetric_memory": True}
     eng, _, _, _ = hds.initialize(model=m, config=cfg)
@@ -88,7 +93,8 @@ def _run(rank, world, d, steps=3, symmetric=False, stage=3, dtype="bf16"):
     if world > 1 and stage == 3:
         summ = z.comm_stats.summary()
         assert summ["collectives"]["all_gather"]["count"] > 0
-        assert summ["collectives"]["reduce_scatter"]["count"] > 0
+        if not zpp:  # qgZ reduces gradients by all-to-all instead
+            assert summ["collectives"]["reduce_scatter"]["count"] > 0
     full = {n: safe_get_full_fp32_param(p).float().cpu() for n, p in eng.module.named_parameters()}
     if symmetric and world > 1 and on_gpu:
         calls = {k: sum(sm.calls[k] for sm in z._symm.values()) for k in ("all_gather", "reduce_scatter")}
@@ -97,7 +103,8 @@ def _run(rank, world, d, steps=3, symmetric=False, stage=3, dtype="bf16"):
     ls = torch.tensor(losses)
     torch.distributed.all_reduce(ls)
     if rank == 0:
-        tag = ("s" if symmetric else "") + ("" if (stage, dtype) == (3, "bf16") else f"_z{stage}{dtype}")
+        tag = ("s" if symmetric else "") + ("" if (stage, dtype) == (3, "bf16") else f"_z{stage}{dtype}") + \
+            ("_zpp" if zpp else "")
         torch.save({"losses": (ls / world).tolist(), "weights": full}, os.path.join(d, f"w{world}{tag}.pt"))
 
 
@@ -218,3 +225,18 @@ def test_zero12_device_path_world2_matches_world1(tmp_path, stage, dtype):
     for n, w in a["weights"].items():
         rel = float((b["weights"][n] - w).norm() / w.norm().clamp_min(1e-12))
         assert rel < tol, (n, rel)
+
+
+def test_zeropp_quantized_device_path_world2_follows_world1(tmp_path):
+    """ZeRO++ qwZ + qgZ at world 2 on device tensors: the int8 quantize / dequantize kernels in the weight gather and
+    the gradient all-to-all reduce run on the GPU; training follows plain world-1 ZeRO-3 within quantization noise."""
+    d = str(tmp_path)
+    run_distributed(_run, 1, d)
+    run_distributed(_run, 2, d, 3, False, 3, "bf16", True)
+    a = torch.load(os.path.join(d, "w1.pt"), weights_only=True)
+    b = torch.load(os.path.join(d, "w2_zpp.pt"), weights_only=True)
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert abs(la - lb) <= 5e-2 * abs(la), (a["losses"], b["losses"])
+    for n, w in a["weights"].items():
+        rel = float((b["weights"][n] - w).norm() / w.norm().clamp_min(1e-12))
+        assert rel < 5e-2, (n, rel)
