@@ -173,9 +173,16 @@ class RaggedTransformer:
         V = lm.shape[0]
         vs = (V + self.tp - 1) // self.tp
         self.vocab = V
-        self.lm_head = t(lm[r * vs:(r + 1) * vs])
+
+        def vocab_shard(x):  # equal row counts on every rank (zero rows pad an uneven last shard): the logits
+            s = x[r * vs:(r + 1) * vs]  # all-gather needs equal sizes; the padding columns are cut at ``vocab``
+            if s.shape[0] < vs:
+                s = torch.cat([s, s.new_zeros((vs - s.shape[0], ) + tuple(s.shape[1:]))])
+            return s
+
+        self.lm_head = t(vocab_shard(lm))
         lb = sd.get("lm_head.b")
-        self.lm_head_b = t(lb[r * vs:(r + 1) * vs]) if lb is not None else None
+        self.lm_head_b = t(vocab_shard(lb)) if lb is not None else None
         self.layers = []
         for Ls in sd["layers"]:
             L = _Layer()
