@@ -144,6 +144,32 @@ class _Timer:
             _STATS[self.key] += time.perf_counter() - self.t0
 
 
+def _rng_snapshot():
+    """Forward-time RNG states a recompute must replay: the CPU and device generators and the model-parallel tracker's
+    named states (reference checkpointing.py:539,645-660 -- dropout inside model-parallel regions draws from the
+    tracker, so without it the recomputed masks differ from the forward's and the gradients are silently wrong)."""
+    dev = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
+    return torch.get_rng_state(), dev, get_cuda_rng_tracker().get_states()
+
+
+@contextlib.contextmanager
+def _replay_rng(ctx):
+    """Run the recompute under the forward's RNG states; afterwards restore the backward-time states (CPU, device and
+    tracker) so the recompute consumes no randomness of the surrounding program."""
+    devs = [torch.cuda.current_device()] if ctx.dev_rng is not None else []
+    tracker = get_cuda_rng_tracker()
+    bwd_tracker = tracker.get_states()
+    with torch.random.fork_rng(devices=devs):
+        torch.set_rng_state(ctx.cpu_rng)
+        if ctx.dev_rng is not None:
+            torch.cuda.set_rng_state(ctx.dev_rng)
+        tracker.set_states(dict(ctx.tracker_rng))
+        try:
+            yield
+        finally:
+            tracker.set_states(bwd_tracker)
+
+
 class _PartitionedCheckpoint(torch.autograd.Function):
     """Reentrant checkpoint that keeps 1/mp of each floating input (see module docstring)."""
 
@@ -172,8 +198,7 @@ class _PartitionedCheckpoint(torch.autograd.Function):
                 keep.append(a)
         ctx.keep = keep
         ctx.save_for_backward(*saved)
-        ctx.cpu_rng = torch.get_rng_state()
-        ctx.dev_rng = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
+        ctx.cpu_rng, ctx.dev_rng, ctx.tracker_rng = _rng_snapshot()
         _STATS["calls"] += 1
         with torch.no_grad(), _Timer("fwd_s"):
             out = run(*args)
@@ -194,11 +219,7 @@ class _PartitionedCheckpoint(torch.autograd.Function):
             full = part.new_empty(part.numel() * mp)
             dist.all_gather_into_tensor(full, part.contiguous(), group=ctx.group)
             args.append(full[:n].view(shape).requires_grad_(rg))
-        devs = [torch.cuda.current_device()] if ctx.dev_rng is not None else []
-        with torch.random.fork_rng(devices=devs), _Timer("recompute_s"):
-            torch.set_rng_state(ctx.cpu_rng)
-            if ctx.dev_rng is not None:
-                torch.cuda.set_rng_state(ctx.dev_rng)
+        with _replay_rng(ctx), _Timer("recompute_s"):
             with torch.enable_grad():
                 out = ctx.run(*args)
         outs = out if ctx.tuple_out else (out, )
@@ -228,8 +249,34 @@ def checkpoint(function, *args, **kwargs):
                 nb = a.numel() * a.element_size()
                 _STATS["saved_bytes"] += nb
                 _STATS["full_bytes"] += nb
+    if get_cuda_rng_tracker().get_states() and "context_fn" not in kwargs:
+        kwargs["context_fn"] = _tracker_context_fn
     with ctx, _Timer("fwd_s"):
         return _tc.checkpoint(function, *args, use_reentrant=False, **kwargs)
+
+
+def _tracker_context_fn():
+    """torch non-reentrant checkpoint ``context_fn``: the forward snapshots the model-parallel RNG tracker, the
+    recompute runs under that snapshot and restores the backward-time states after (torch itself replays only the
+    CPU / device generators)."""
+    snap = {}
+    tracker = get_cuda_rng_tracker()
+
+    @contextlib.contextmanager
+    def fwd():
+        snap["s"] = tracker.get_states()
+        yield
+
+    @contextlib.contextmanager
+    def rec():
+        bwd = tracker.get_states()
+        tracker.set_states(dict(snap["s"]))
+        try:
+            yield
+        finally:
+            tracker.set_states(bwd)
+
+    return fwd(), rec()
 
 
 non_reentrant_checkpoint = checkpoint
@@ -248,8 +295,7 @@ class _SavedInputCheckpoint(torch.autograd.Function):
         ctx.run = run
         ctx.grad_idx = [i for i, a in enumerate(args) if torch.is_tensor(a) and a.requires_grad]
         ctx.others = [None if i in ctx.grad_idx else a for i, a in enumerate(args)]
-        ctx.cpu_rng = torch.get_rng_state()
-        ctx.dev_rng = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
+        ctx.cpu_rng, ctx.dev_rng, ctx.tracker_rng = _rng_snapshot()
         stash = []
         prev = (AttnStash.mode, AttnStash.items)
         if stash_attention:
@@ -280,15 +326,11 @@ class _SavedInputCheckpoint(torch.autograd.Function):
         for i, t in zip(ctx.grad_idx, saved[:n_in]):
             args[i] = t.detach().requires_grad_(True)
         stash = [(saved[n_in + 2 * j], saved[n_in + 2 * j + 1]) for j in range(ctx.n_stash)]
-        devs = [torch.cuda.current_device()] if ctx.dev_rng is not None else []
         prev = (AttnStash.mode, AttnStash.items)
         if ctx.n_stash:
             AttnStash.mode, AttnStash.items = "replay", stash
         try:
-            with torch.random.fork_rng(devices=devs):
-                torch.set_rng_state(ctx.cpu_rng)
-                if ctx.dev_rng is not None:
-                    torch.cuda.set_rng_state(ctx.dev_rng)
+            with _replay_rng(ctx):
                 with torch.enable_grad():
                     out = ctx.run(*args)
         finally:
