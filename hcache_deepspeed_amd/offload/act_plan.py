@@ -269,10 +269,12 @@ class PlannedActivationCache(HostActivationCache):
         global _ACTIVE
         cuda = self.device.type == "cuda"
         self._end_of_step()
+        if cuda:
+            self._take_step_peak()  # the previous step's full peak, across the per-block resets of its backward
         if cuda and self.forced is None and self.budget is not None:
             self._advance_plan()
             self._turn_peak = None
-            self.peak_seen = max(self.peak_seen, torch.cuda.max_memory_allocated(self.device))
+        if cuda:
             torch.cuda.reset_peak_memory_stats(self.device)
         self.cur_layer = -1
         self._release_stale()
@@ -324,7 +326,7 @@ class PlannedActivationCache(HostActivationCache):
         if self._stage == 1:
             # the peak with every item off the device: the measured one minus what calibration kept (the last
             # blocks, and tensors the pinned-host cap left on the GPU)
-            self._peak_all = torch.cuda.max_memory_allocated(self.device) - self._cal_kept
+            self._peak_all = self.last_step_peak - self._cal_kept
             ms, nb = self._copy_busy
             for a, b, n in self._copy_evs:
                 b.synchronize()

@@ -156,6 +156,10 @@ class HostActivationCache:
         self._turn_peak = None  # max allocation at the forward/backward turn-around of the last step
         self.plan_adjustments = 0
         self.peak_seen = 0  # max allocation over every step (the planner resets the peak counter per forward)
+        # the allocator's peak counter is reset per forward AND per backward block (bwd_headroom); the running max of
+        # the step across those resets is what every calibration must read, not the raw counter
+        self._step_max = 0
+        self.last_step_peak = 0  # full peak of the previous step (set at the next forward)
         self.bwd_headroom = None  # largest one-block backward transient seen (bytes), kept free by far prefetches
         self._bwd_layer, self._bwd_mark = None, None
 
@@ -239,7 +243,7 @@ class HostActivationCache:
                 and self._steps_seen >= 3):
             return
         total = torch.cuda.get_device_properties(self.device).total_memory
-        room = int(0.85 * total) - torch.cuda.max_memory_allocated(self.device)
+        room = int(0.85 * total) - self.last_step_peak  # the previous step's full peak (read before the reset)
         if room > self._stash_sb:
             keep_from = max(0, min(self.stash_keep_from, self.n_layers) - room // self._stash_sb)
             if keep_from != self.stash_keep_from:
@@ -261,13 +265,34 @@ class HostActivationCache:
         if torch.is_grad_enabled():
             self.cur_layer = i
 
+    def _peak_fold(self):
+        """The allocator's peak since its last reset, folded into the running max of this step."""
+        pk = torch.cuda.max_memory_allocated(self.device)
+        self._step_max = max(self._step_max, pk)
+        return pk
+
+    def _peak_reset(self):
+        self._peak_fold()
+        torch.cuda.reset_peak_memory_stats(self.device)
+
+    def _take_step_peak(self):
+        """Start of a forward: the whole previous step's peak (every reset inside it included) -> ``last_step_peak``,
+        and a fresh running max for the step that starts now."""
+        if self.device.type == "cuda":
+            self.last_step_peak = max(self._step_max, torch.cuda.max_memory_allocated(self.device))
+            self.peak_seen = max(self.peak_seen, self.last_step_peak)
+        self._step_max = 0
+        return self.last_step_peak
+
     @contextlib.contextmanager
     def forward_context(self):
+        if self.device.type == "cuda":
+            self._take_step_peak()
         if self.budget is not None and self.device.type == "cuda":
             if self._calibrating:  # the previous step spilled everything: plan from what it measured
                 # tensors the host cap kept on the GPU were all alive at the forward/backward turn-around, so the
                 # "everything spilled" peak is the measured one minus them (plan_offload adds kept layers back)
-                peak = torch.cuda.max_memory_allocated(self.device) - self._capped_this_step
+                peak = self.last_step_peak - self._capped_this_step
                 self.plan = calibrated_plan(self.layer_bytes, peak + self._capped_this_step, self._capped_this_step,
                                             self.budget)
                 self._calibrating = False
@@ -297,7 +322,7 @@ class HostActivationCache:
                              f"{self.budget / 2**30:.1f} GiB -> {'recomputing' if self.policy_recompute else 'spilling'} "
                              f"{len(new)} layers", ranks=[0])
             self._turn_peak = None
-            self.peak_seen = max(self.peak_seen, torch.cuda.max_memory_allocated(self.device))
+        if self.device.type == "cuda":
             torch.cuda.reset_peak_memory_stats(self.device)
         self.cur_layer = -1
         for lst in self.by_layer.values():  # a forward whose backward never ran: return its host buffers
@@ -451,10 +476,9 @@ class HostActivationCache:
             # is what one block's backward (recompute intermediates + gradients) needs on top of the live tensors
             now = torch.cuda.memory_allocated(self.device)
             if self._bwd_mark is not None:
-                pk = torch.cuda.max_memory_allocated(self.device)
-                self.peak_seen = max(self.peak_seen, pk)
+                pk = self._peak_fold()
                 self.bwd_headroom = max(self.bwd_headroom or 0, pk - self._bwd_mark)
-                torch.cuda.reset_peak_memory_stats(self.device)
+                self._peak_reset()
             self._bwd_layer, self._bwd_mark = layer, now
         # j = 0 first: the rest of THIS block's spilled tensors (a block unpacks several; if the first was late, the
         # others must not queue behind the earlier blocks' prefetches -- a 189 ms stall at 128k ckpt_offload)

@@ -439,17 +439,62 @@ def test_stash_keep_and_host_fit_decisions(monkeypatch):
     peak = {"v": 70 * GB}
     c.device = torch.device("cuda")
     monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: types.SimpleNamespace(total_memory=total))
-    monkeypatch.setattr(torch.cuda, "max_memory_allocated", lambda d=None: peak["v"])
     import hcache_deepspeed_amd.offload.activation_cache as ac
     monkeypatch.setattr(ac, "log_dist", lambda *a, **k: None)
     c._stash_sb = 4 * GB
+    c.last_step_peak = peak["v"]
     c._update_stash_keep()
     c._update_stash_keep()
     assert c.stash_keep_from >= c.n_layers  # not before the third step
     c._update_stash_keep()  # room 85 - 70 = 15 GB -> 3 blocks
     assert c.stash_keep_from == 7
-    peak["v"] = 84 * GB
+    c.last_step_peak = 84 * GB
     c._update_stash_keep()  # room 1 GB: no change (only grows)
     assert c.stash_keep_from == 7
     c.cur_layer = 8
     assert c._stash_fits(args)  # kept on the device: no host check
+
+
+def test_step_peak_survives_per_block_resets(monkeypatch):
+    """The cache resets the allocator's peak counter at every forward and at every backward block (bwd_headroom).
+    The previous step's FULL peak (the max across those resets) is what the stash decision, the calibration and
+    peak_gib_all_steps read -- driven through forward_context, whose reset precedes the stash decision."""
+    import types
+    import torch
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    import hcache_deepspeed_amd.offload.activation_cache as ac
+    GB = 1 << 30
+    alloc = {"cur": 10 * GB, "peak": 10 * GB}
+
+    def set_alloc(v):
+        alloc["cur"] = v
+        alloc["peak"] = max(alloc["peak"], v)
+
+    def reset(d=None):
+        alloc["peak"] = alloc["cur"]
+
+    monkeypatch.setattr(torch.cuda, "max_memory_allocated", lambda d=None: alloc["peak"])
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda d=None: alloc["cur"])
+    monkeypatch.setattr(torch.cuda, "reset_peak_memory_stats", reset)
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: types.SimpleNamespace(total_memory=100 * GB))
+    monkeypatch.setattr(ac, "log_dist", lambda *a, **k: None)
+    c = HostActivationCache(torch.device("cpu"), ckpt_offload=True, stash_attention=True, min_layers_resident=1,
+                            gpu_budget_bytes=90 * GB)
+    c.device = torch.device("cuda")
+    c.n_layers, c._stash_sb = 10, 4 * GB
+    for step in range(2):
+        with c.forward_context():
+            set_alloc(60 * GB)  # forward turn-around: the step's real peak
+        # backward: block 9 then 8 -- each new block folds and resets the counter; later blocks peak lower
+        c._prefetch_before(9)
+        set_alloc(30 * GB)
+        c._prefetch_before(8)
+        set_alloc(20 * GB)
+        c._prefetch_before(7)
+        set_alloc(10 * GB)
+    with c.forward_context():  # the 3rd forward: decides from step 2's full peak (60), not the last block's (20)
+        pass
+    assert c.last_step_peak == 60 * GB
+    assert c.stats()["peak_gib_all_steps"] == 60.0
+    # room 85 - 60 = 25 GB -> 6 blocks of 4 GB keep their stash on the device
+    assert c.stash_keep_from == 10 - 6
