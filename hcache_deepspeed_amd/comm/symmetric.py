@@ -44,9 +44,36 @@ class SymmetricMemoryError(RuntimeError):
     """A symmetric-memory collective timed out waiting for a peer: results since then are not trustworthy."""
 
 
+_same_node = {}  # id(group) -> every rank of the group runs on this host
+
+
+def _host_id():
+    """This host's identity: hostname + kernel boot id (containers of different machines may share a hostname)."""
+    import socket
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return f"{socket.gethostname()}/{boot}"
+
+
+def same_node(group=None):
+    """True iff every rank of ``group`` runs on this host (IPC handles do not cross nodes). Collective the first time
+    per group (an all_gather_object of the host ids), cached after."""
+    key = id(group)
+    if key not in _same_node:
+        ids = [None] * dist.get_world_size(group)
+        dist.all_gather_object(ids, _host_id(), group=group)
+        _same_node[key] = len(set(ids)) == 1
+    return _same_node[key]
+
+
 def supported(group=None):
-    """Symmetric memory needs a GPU, an initialised process group of <= 8 ranks."""
-    return torch.cuda.is_available() and dist.is_initialized() and 1 < dist.get_world_size(group) <= MAX_RANKS
+    """Symmetric memory needs a GPU and an initialised process group of <= 8 ranks, all on this node. Collective
+    (``same_node``): every rank of the group must call it."""
+    return (torch.cuda.is_available() and dist.is_initialized() and 1 < dist.get_world_size(group) <= MAX_RANKS
+            and same_node(group))
 
 
 class SymmetricMemory:
@@ -96,8 +123,10 @@ class SymmetricMemory:
         """Raise ``SymmetricMemoryError`` if any completed collective of this buffer timed out."""
         e = self.error_nowait()
         if e:
-            raise SymmetricMemoryError(f"symmetric-memory collective on rank {self.rank} timed out waiting for peer "
-                                       f"{e - 1} (world {self.world}); results of this buffer since then are invalid")
+            what = (f"peer {(e & 0xFF) - 1} timed out and poisoned this buffer" if e & 0x100 else
+                    f"timed out waiting for peer {e - 1}")
+            raise SymmetricMemoryError(f"symmetric-memory collective on rank {self.rank}: {what} (world {self.world}); "
+                                       f"results of this buffer since then are invalid")
 
     @staticmethod
     def _dev(dev_status):
@@ -190,10 +219,22 @@ def release_all():
     _cache.clear()
 
 
+def _agree_broken(group):
+    """Called by a rank whose buffer failed. The failing rank poisoned every peer's buffer (symm_comm.hip), so each
+    peer fails its next symmetric call too and arrives here: the ranks meet in one torch.distributed collective and
+    only then switch the group to RCCL together -- never one rank on RCCL while another still waits in the symmetric
+    protocol. The agreement is a MAX of 1 over the group (host tensor on gloo)."""
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    flag = torch.ones(1, dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    _broken.add((id(group), "small_allreduce"))
+
+
 def small_all_reduce(x, group=None, max_kb=None):
     """In-place sum of ``x`` over ``group``: the one-shot symmetric all-reduce for contiguous GPU messages of at
-    most ``max_kb`` KiB (default ``HDS_SYMM_ALLREDUCE_KB``) on a group of <= 8 ranks, RCCL otherwise. The choice
-    depends only on the message size and the group, so every rank of a tensor-parallel group takes the same path."""
+    most ``max_kb`` KiB (default ``HDS_SYMM_ALLREDUCE_KB``) on a group of <= 8 ranks on one node, RCCL otherwise. The
+    choice depends only on the message size and the group, so every rank of a tensor-parallel group takes the same
+    path; after a timeout the switch to RCCL is agreed collectively (``_agree_broken``) and the call raises."""
     kb = SMALL_ALLREDUCE_KB if max_kb is None else max_kb
     nb = x.numel() * x.element_size()
     if (kb > 0 and x.is_cuda and x.is_contiguous() and x.numel() % 8 == 0 and 0 < nb <= kb * 1024
@@ -203,8 +244,9 @@ def small_all_reduce(x, group=None, max_kb=None):
         try:
             sm.all_reduce(x)
         except SymmetricMemoryError:
-            # loud: the caller's earlier results may be stale; later calls of this group take RCCL
-            _broken.add((id(group), "small_allreduce"))
+            # loud: the caller's earlier results may be stale; once every rank of the group has failed too (the
+            # poison makes sure they do), later calls of this group take RCCL on every rank
+            _agree_broken(group)
             _cache.pop((id(group), "small_allreduce"), None)
             sm.abandon()
             raise

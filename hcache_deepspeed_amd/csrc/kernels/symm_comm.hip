@@ -47,11 +47,24 @@ struct SymmArgs {
   int32_t* dev_status;    // device flag (may be null): error code on timeout
 };
 
+__device__ __forceinline__ uint32_t* err_ptr(char* base) { return reinterpret_cast<uint32_t*>(base + kErrOff); }
+
 __device__ __forceinline__ void report(const SymmArgs& a, uint32_t code) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(a.base[a.rank] + kErrOff), code, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err_ptr(a.base[a.rank]), code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (a.host_status) __hip_atomic_store(a.host_status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (a.dev_status) __hip_atomic_store(a.dev_status, (int32_t)code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// a rank that timed out poisons every peer's error word (kPeerErr | 1 + its rank): the peers' next collective on the
+// buffer fails at once instead of waiting for a rank that has left the protocol, so EVERY rank reaches the host-side
+// agreement (comm/symmetric.py) before any of them switches to RCCL
+constexpr uint32_t kPeerErr = 0x100u;
+
+__device__ __forceinline__ void poison_peers(const SymmArgs& a) {
+  for (int r = 0; r < a.world; ++r)
+    if (r != a.rank)
+      __hip_atomic_store(err_ptr(a.base[r]), kPeerErr | (1u + (uint32_t)a.rank), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ uint32_t* flag_ptr(char* base, int src, int blk) {
@@ -74,8 +87,11 @@ __device__ __forceinline__ void exchange(const SymmArgs& a) {
       if (r == t) peer = a.base[r];
     __hip_atomic_store(flag_ptr(peer, a.rank, b), a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = flag_ptr(a.base[a.rank], t, b);
+    // a failed (or poisoned) buffer does not wait: its result is invalid either way, and the sticky word is
+    // re-reported below
+    const bool failed = __hip_atomic_load(err_ptr(a.base[a.rank]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
     bool ok = false;
-    for (int it = 0; it < kSpinMax; ++it) {
+    for (int it = 0; !failed && it < kSpinMax; ++it) {
       const uint32_t v = __hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       if ((int32_t)(v - a.epoch) >= 0) {
         ok = true;
@@ -83,7 +99,10 @@ __device__ __forceinline__ void exchange(const SymmArgs& a) {
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (!ok) report(a, 1u + (uint32_t)t);
+    if (!ok && !failed) {
+      report(a, 1u + (uint32_t)t);
+      poison_peers(a);
+    }
   }
   if (t == 0) {  // a buffer that timed out before stays failed: re-report, so no later step trusts it
     const uint32_t prev = __hip_atomic_load(reinterpret_cast<uint32_t*>(a.base[a.rank] + kErrOff), __ATOMIC_RELAXED,

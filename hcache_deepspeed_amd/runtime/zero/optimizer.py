@@ -1571,6 +1571,11 @@ class ZeroOptimizer:
         for sm in self._symm.values():
             sm.abandon()
         self._symm, self._symm_flag_ev = {}, None
+        # the device skipped that step's update: its step count must not advance Adam's bias correction
+        for group in self.param_groups:
+            group["step"] = max(0, group.get("step", 0) - 1)
+        log_dist(f"symmetric memory: the previous step was skipped on the device (collective timeout, code {code})",
+                 ranks=[0])
         raise SymmetricMemoryError(f"a ZeRO symmetric-memory unit collective timed out (code {code}); that step was "
                                    f"skipped on every rank and the unit collectives now use RCCL")
 
@@ -1579,7 +1584,9 @@ class ZeroOptimizer:
         flag = self._symm_err.clone()
         if self.dp_world > 1:
             dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.dp_group)
-        torch.maximum(self._inf_buf, flag, out=self._inf_buf)
+        if self.loss_scaler.dynamic:
+            torch.maximum(self._inf_buf, flag, out=self._inf_buf)  # skip on overflow OR a failed collective
+        self._symm_skip = flag  # static scaling: only the collective failure skips (inf/NaN grads do not, as without)
         self._symm_flag_host.copy_(flag, non_blocking=True)
         self._symm_flag_ev = torch.cuda.Event()
         self._symm_flag_ev.record()
@@ -1608,7 +1615,7 @@ class ZeroOptimizer:
                 log_dist(f"overflow: skipping step, loss scale -> {self.loss_scaler.loss_scale}", ranks=[0])
                 self.zero_grad()
                 return False
-        found_inf = self._inf_buf if (self.loss_scaler.dynamic or symm) else None
+        found_inf = self._inf_buf if self.loss_scaler.dynamic else (self._symm_skip if symm else None)
         for gi, group in enumerate(self.param_groups):
             group["step"] = group.get("step", 0) + 1
         if self.kind == "generic":
