@@ -208,6 +208,21 @@ def main():
         return loss
 
     progress = os.environ.get("HDS_BENCH_PROGRESS") == "1"  # long-context sweeps: a line per step on stderr
+    if progress and rank == 0:
+        # steps of minutes (>= 256k tokens): a line every 8 blocks entered -- forward AND backward recomputes -- so a
+        # supervisor that kills silent commands sees the run move
+        t_run = time.perf_counter()
+        blocks = [b for m in model.modules() if isinstance(m, torch.nn.ModuleList) for b in m]
+
+        def _block_progress(i):
+            def pre(mod, args):
+                if i % 8 == 0:
+                    print(f"[bench] t={time.perf_counter() - t_run:.0f}s block {i} "
+                          f"({'grad' if torch.is_grad_enabled() else 'no-grad'})", file=sys.stderr, flush=True)
+            return pre
+
+        for i, b in enumerate(blocks):
+            b.register_forward_pre_hook(_block_progress(i))
 
     def step_progress(tag, i, t_start):
         if progress and rank == 0:

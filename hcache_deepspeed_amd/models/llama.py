@@ -204,11 +204,18 @@ class LlamaMLP(nn.Module):
         self._register_load_state_dict_pre_hook(_fuse_hf_keys(("gate_proj", "up_proj"), "gate_up_proj"))
 
     fpdt_chunks = 0  # >1: sequence-chunked MLP with per-chunk recompute (parallel/fpdt.enable_fpdt)
+    # long context: above this many tokens the MLP runs in sequence chunks of this many rows, each recomputed in
+    # backward (parallel/fpdt.fpdt_gated_ffn) -- at 512k tokens the gate|up output alone is 28 GiB, its SwiGLU output
+    # and transpose another 28, and [tokens, 2I] would pass 2^31 elements. 0: never
+    chunk_rows = int(os.environ.get("HDS_MLP_CHUNK_ROWS", "65536"))
 
     def forward(self, x):
-        if self.fpdt_chunks > 1:
+        nc = self.fpdt_chunks
+        if nc <= 1 and self.chunk_rows and x.shape[0] > self.chunk_rows:
+            nc = -(-x.shape[0] // self.chunk_rows)
+        if nc > 1:
             from ..parallel.fpdt import fpdt_gated_ffn
-            return fpdt_gated_ffn(x, self.gate_up_proj.weight, self.down_proj.weight, self.fpdt_chunks, self.act)
+            return fpdt_gated_ffn(x, self.gate_up_proj.weight, self.down_proj.weight, nc, self.act)
         # ZeRO linears on both sides: the SwiGLU kernels also write the transposes the two weight gradients read
         # (runtime/zero/linear.py), instead of separate HBM transposes in the backward
         t = (torch.is_grad_enabled() and getattr(self.down_proj, "_hds_mel", False)
@@ -225,8 +232,13 @@ class LlamaDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.mlp = LlamaMLP(cfg)
 
-    def forward(self, h, residual, cos, sin, seq_len, cu_seqlens=None, pos_ids=None):
-        """h: output of the previous block (added to ``residual`` inside the fused norm)."""
+    def forward(self, h, residual, cos, sin, seq_len, cu_seqlens=None, pos_ids=None, summed=False):
+        """h: output of the previous block (added to ``residual`` inside the fused norm).
+
+        ``summed``: the block boundary is the summed residual stream s (``h`` = s, ``residual`` None) and the block
+        returns ONE tensor, s + attn + mlp. A checkpointed block then saves one [tokens, hidden] input instead of
+        two (h and residual), which halves what ckpt_offload spills and prefetches per block; the extra add is one
+        elementwise pass."""
         if residual is None:
             x = self.input_layernorm(h)
             residual = h
@@ -234,6 +246,8 @@ class LlamaDecoderLayer(nn.Module):
             x, residual = self.input_layernorm(h, residual)
         a = self.self_attn(x, cos, sin, seq_len, cu_seqlens, pos_ids)
         x, residual = self.post_attention_layernorm(a, residual)
+        if summed:
+            return residual + self.mlp(x)
         return self.mlp(x), residual
 
 
@@ -246,6 +260,10 @@ class LlamaModel(nn.Module):
         self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, i) for i in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.gradient_checkpointing = False
+        # block boundary = the summed residual stream (one saved tensor per checkpointed block, see
+        # LlamaDecoderLayer.forward); set by the host activation cache's ckpt_offload policy, and used by plain
+        # activation checkpointing
+        self.summed_boundary = False
 
     def rope(self, device, max_pos):
         return rope_tables(max(max_pos, self.cfg.max_position_embeddings), self.cfg.head_dim, self.cfg.rope_theta,
@@ -268,10 +286,18 @@ class LlamaModel(nn.Module):
             h, _ = self.norm(h, residual)
             return h
         residual = None
+        ckpt = self.gradient_checkpointing and self.training
+        if (self.summed_boundary or ckpt) and layer_hook is None and torch.is_grad_enabled():
+            for layer in self.layers:
+                if ckpt:
+                    h = _ckpt(layer, h, None, cos, sin, S, cu_seqlens, pos_ids, True)
+                else:
+                    h = layer(h, None, cos, sin, S, cu_seqlens, pos_ids, True)
+            return self.norm(h)
         for i, layer in enumerate(self.layers):
             if layer_hook is not None:
                 layer_hook(i, h, residual)
-            if self.gradient_checkpointing and self.training:
+            if ckpt:
                 h, residual = _ckpt(layer, h, residual, cos, sin, S, cu_seqlens, pos_ids)
             else:
                 h, residual = layer(h, residual, cos, sin, S, cu_seqlens, pos_ids)

@@ -191,6 +191,11 @@ class HostActivationCache:
             if isinstance(m, nn.ModuleList):
                 blocks.extend(list(m))
         self.n_layers = len(blocks)
+        if self.ckpt_offload:
+            # models that support it checkpoint the summed residual stream: one spilled tensor per block, not two
+            for m in model.modules():
+                if hasattr(m, "summed_boundary"):
+                    m.summed_boundary = True
         for i, b in enumerate(blocks):
             self._attached.append(b.register_forward_pre_hook(lambda mod, args, i=i: self._enter(i)))
             if self.policy_recompute:
