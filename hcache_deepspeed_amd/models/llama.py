@@ -204,14 +204,16 @@ class LlamaMLP(nn.Module):
         self._register_load_state_dict_pre_hook(_fuse_hf_keys(("gate_proj", "up_proj"), "gate_up_proj"))
 
     fpdt_chunks = 0  # >1: sequence-chunked MLP with per-chunk recompute (parallel/fpdt.enable_fpdt)
-    # long context: above this many tokens the MLP runs in sequence chunks of this many rows, each recomputed in
-    # backward (parallel/fpdt.fpdt_gated_ffn) -- at 512k tokens the gate|up output alone is 28 GiB, its SwiGLU output
-    # and transpose another 28, and [tokens, 2I] would pass 2^31 elements. 0: never
+    # long context: above ``chunk_min_tokens`` tokens the MLP runs in sequence chunks of ``chunk_rows`` rows, each
+    # recomputed in backward (parallel/fpdt.fpdt_gated_ffn) -- at 512k tokens the gate|up output alone is 28 GiB and
+    # its SwiGLU output + transpose another 28. Below the threshold the whole-sequence MLP is faster (no second
+    # gate|up GEMM, NT-layout weight gradients; 128k: 8 % per step) and fits. 0: never
     chunk_rows = int(os.environ.get("HDS_MLP_CHUNK_ROWS", "65536"))
+    chunk_min_tokens = int(os.environ.get("HDS_MLP_CHUNK_MIN_TOKENS", str(256 * 1024)))
 
     def forward(self, x):
         nc = self.fpdt_chunks
-        if nc <= 1 and self.chunk_rows and x.shape[0] > self.chunk_rows:
+        if nc <= 1 and self.chunk_rows and x.shape[0] > max(self.chunk_rows, self.chunk_min_tokens):
             nc = -(-x.shape[0] // self.chunk_rows)
         if nc > 1:
             from ..parallel.fpdt import fpdt_gated_ffn

@@ -239,13 +239,13 @@ class HostActivationCache:
     def _update_stash_keep(self):
         """ckpt_offload with the attention stash: the stash goes to host memory like the inputs (needed at 320k
         tokens), but where the HBM holds it, keeping it on the device saves its round trip over PCIe (128k: ~8 %).
-        From the third step on, the HBM the steps so far left free (85 % of the device minus the peak allocation;
+        From the second step on, the HBM the previous step left free (85 % of the device minus the peak allocation;
         the margin covers the caching allocator's fragmentation, which at 128k tokens reserves ~80 GiB more than the
         peak allocation -- reusable, so the reserved peak would understate the room) keeps the stash of the last
         blocks on the device; it only grows."""
         self._steps_seen += 1
         if not (self.ckpt_offload and self.stash_attention and self.device.type == "cuda" and self._stash_sb
-                and self._steps_seen >= 3):
+                and self._steps_seen >= 2):
             return
         total = torch.cuda.get_device_properties(self.device).total_memory
         room = int(0.85 * total) - self.last_step_peak  # the previous step's full peak (read before the reset)

@@ -36,6 +36,7 @@ def test_long_context_paths_match_plain(mode, monkeypatch):
         m.gradient_checkpointing_enable()
     if mode in ("mlp_chunks", "summed_chunks"):
         monkeypatch.setattr(LlamaMLP, "chunk_rows", 16)  # 48 tokens -> 3 chunks
+        monkeypatch.setattr(LlamaMLP, "chunk_min_tokens", 0)
     loss, g = _grads(m, x)
     torch.testing.assert_close(loss, ref_loss, rtol=1e-6, atol=1e-6)
     for n in ref:
@@ -74,6 +75,7 @@ def _zero3_losses(rank, world, chunk_rows, summed):
     import hcache_deepspeed_amd as ds
     from hcache_deepspeed_amd.models import llama
     llama.LlamaMLP.chunk_rows = chunk_rows
+    llama.LlamaMLP.chunk_min_tokens = 0
     torch.manual_seed(0)
     with ds.zero.Init():
         m = LlamaForCausalLM(tiny(num_hidden_layers=2, vocab_size=97, hidden_size=32, intermediate_size=64,

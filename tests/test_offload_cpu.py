@@ -408,7 +408,7 @@ def test_ckpt_offload_attention_stash_exact(stash):
 
 def test_stash_keep_and_host_fit_decisions(monkeypatch):
     """ckpt_offload attention stash: blocks stash only while the pinned-host budget holds the stash plus every later
-    block's inputs; from the third step the last blocks keep their stash on the device as far as the measured peak
+    block's inputs; from the second step the last blocks keep their stash on the device as far as the measured peak
     leaves room (85 % of HBM), and that only grows."""
     import types
     import torch
@@ -444,8 +444,7 @@ def test_stash_keep_and_host_fit_decisions(monkeypatch):
     c._stash_sb = 4 * GB
     c.last_step_peak = peak["v"]
     c._update_stash_keep()
-    c._update_stash_keep()
-    assert c.stash_keep_from >= c.n_layers  # not before the third step
+    assert c.stash_keep_from >= c.n_layers  # not before the second step
     c._update_stash_keep()  # room 85 - 70 = 15 GB -> 3 blocks
     assert c.stash_keep_from == 7
     c.last_step_peak = 84 * GB
@@ -482,7 +481,7 @@ def test_step_peak_survives_per_block_resets(monkeypatch):
                             gpu_budget_bytes=90 * GB)
     c.device = torch.device("cuda")
     c.n_layers, c._stash_sb = 10, 4 * GB
-    for step in range(2):
+    for step in range(1):
         with c.forward_context():
             set_alloc(60 * GB)  # forward turn-around: the step's real peak
         # backward: block 9 then 8 -- each new block folds and resets the counter; later blocks peak lower
@@ -492,7 +491,7 @@ def test_step_peak_survives_per_block_resets(monkeypatch):
         set_alloc(20 * GB)
         c._prefetch_before(7)
         set_alloc(10 * GB)
-    with c.forward_context():  # the 3rd forward: decides from step 2's full peak (60), not the last block's (20)
+    with c.forward_context():  # the 2nd forward: decides from step 1's full peak (60), not the last block's (20)
         pass
     assert c.last_step_peak == 60 * GB
     assert c.stats()["peak_gib_all_steps"] == 60.0
