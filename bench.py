@@ -276,6 +276,11 @@ def main():
             sync()
             zopt.comm_stats = None
         mine = {"rank": rank, "peak_mem_gib": round(mem, 1), "timed_steps_instrumented": timed_events is not None}
+        ue = getattr(zopt, "unit_events", None)
+        if ue is not None:  # ZeRO-3 fetch / wait / prefetch events of the last micro-step (counts, numel, host ms)
+            mine["unit_events"] = ue.summary()
+        if getattr(zopt, "comm_selection", None) is not None:  # startup transport measurement + routing
+            mine["transport_selection"] = zopt.comm_selection
         if cs is not None:
             summ = cs.summary()
             mine["exposed_comm_ms_per_step"] = round(summ["exposed_ms"] / args.gas, 2)
@@ -302,7 +307,9 @@ def main():
                 "timed_steps_instrumented": any(r["timed_steps_instrumented"] for r in per_rank),
                 "exposed_comm_ms_per_step_max": max(r.get("exposed_comm_ms_per_step", 0.0) for r in per_rank),
                 "peak_mem_gib_per_rank": [r["peak_mem_gib"] for r in per_rank],
-                "rank0": per_rank[0]}
+                "rank0": per_rank[0],
+                "unit_events_rank0": per_rank[0].get("unit_events"),
+                "transport_selection": per_rank[0].get("transport_selection")}
         for kind in ("all_gather", "reduce_scatter"):
             bws = [r.get("collectives", {}).get(kind, {}).get("busbw_GBps") for r in per_rank]
             bws = [b for b in bws if b]

@@ -206,6 +206,12 @@ class MI355XConfig:
     comm_high_priority: bool = True
     # per-step exposed-communication / busbw accounting of the ZeRO collectives (runtime/zero/comm_stats.py)
     comm_stats: bool = False
+    # ZeRO-3 unit collectives: "auto" measures rccl / native / symmetric per size class at dp > 1 and routes each
+    # class to the fastest (runtime/zero/transport.py); "auto:rccl,symmetric" limits the candidates; "rccl" keeps
+    # torch.distributed
+    zero_comm_transport: str = "auto"
+    # the ZeRO-3 fetch / wait / prefetch events also start / stop the engine timers (reference ENABLE_PROFILER)
+    zero3_event_timers: bool = False
     host_act_cache: HostActCacheConfig = field(default_factory=HostActCacheConfig)
 
 
@@ -328,6 +334,8 @@ class DeepSpeedConfig:
             zero3_max_reduce_inflight=int(m.get("zero3_max_reduce_inflight", 2)),
             zero3_unit_bucket_mb=_auto_or(m.get("zero3_unit_bucket_mb", "auto"), float),
             comm_stats=bool(m.get("comm_stats", False)),
+            zero_comm_transport=str(m.get("zero_comm_transport", "auto")),
+            zero3_event_timers=bool(m.get("zero3_event_timers", False)),
             direct_wgrad=bool(m.get("direct_wgrad", True)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
             comm_high_priority=bool(m.get("comm_high_priority", True)),

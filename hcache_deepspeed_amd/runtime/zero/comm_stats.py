@@ -143,6 +143,12 @@ class UnitEventProfiler:
         if self.timers is not None:
             self.timers(name).start()
 
+    def cancel_event(self, name):
+        """Drop a started event that moved nothing (the reference records prefetch events only when it issues)."""
+        ev = self.event_counters.get(name)
+        if ev is not None:
+            ev._t0 = None
+
     def stop_event(self, name, num_elem):
         ev = self.event_counters.get(name)
         if ev is None or ev._t0 is None:

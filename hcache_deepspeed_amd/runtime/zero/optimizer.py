@@ -322,6 +322,15 @@ class ZeroOptimizer:
                                             [self.store.numel], group=self.dp_group, what="ZeRO unit layout")
         log_dist(f"ZeRO stage {self.stage}: {len(self.units)} flat units, {nparams / 1e6:.1f}M params, "
                  f"dp={self.dp_world}, shard={self.store.numel / 1e6:.1f}M elems, optimizer={self.kind}", ranks=[0])
+        # reference partitioned_param_coordinator.py:305-346,406-413: fetch / wait / prefetch events with the elements
+        # each moved, per micro-step (unit_events_last: the previous micro-step's summary)
+        from .comm_stats import UnitEventProfiler
+        self.unit_events = UnitEventProfiler(timers if getattr(self.mi, "zero3_event_timers", False) else None)
+        self.unit_events_last = None
+        self.comm_selection = None
+        if str(getattr(self.mi, "zero_comm_transport", "auto")).startswith("auto") and self.dp_world > 1 and \
+                not self.offload_param:
+            self.select_transports()
 
     # ------------------------------------------------------------------------------------
     # construction
@@ -768,9 +777,22 @@ class ZeroOptimizer:
             if self._last_pre_uid != u.uid:  # a bucket unit's later modules do not re-enter the trace
                 self._last_pre_uid = u.uid
                 self._record_and_prefetch(u)
-            self._gather(u, wait=True)
+            self._fetch(u, "forward")
 
         return pre
+
+    def _fetch(self, u, phase):
+        """The unit needed now: submit its all-gather if nothing prefetched it, then wait -- counted as the
+        reference coordinator's ``{phase}_fetch_submit`` / ``{phase}_fetch_wait`` events (elements = shard numel)."""
+        ev = self.unit_events
+        if u.status == NOT_AVAILABLE and self._partitioned(u):
+            ev.start_event(f"{phase}_fetch_submit")
+            self._gather(u, wait=False)
+            ev.stop_event(f"{phase}_fetch_submit", u.shard)
+        inflight = u.status == INFLIGHT
+        ev.start_event(f"{phase}_fetch_wait")
+        self._gather(u, wait=True)
+        ev.stop_event(f"{phase}_fetch_wait", u.shard if inflight else 0)
 
     def _make_ext_pre(self, u):
 
@@ -883,6 +905,7 @@ class ZeroOptimizer:
             log_dist("native_comm: CPU run, keeping torch.distributed", ranks=[0])
             return False
         self._native = {}
+        self._route = None  # forced: every unit collective of every group on the native communicator
         return True
 
     def _ncomm(self, group):
@@ -891,6 +914,8 @@ class ZeroOptimizer:
             return None
         key = id(group)
         if key not in cache:
+            if getattr(self, "_route", None):
+                return None  # measured routing: native communicators exist only for the groups it won
             from ...comm.native_rccl import RcclCommunicator
             cache[key] = RcclCommunicator(group)
         return cache[key]
@@ -1016,7 +1041,14 @@ class ZeroOptimizer:
         if not need or not all(symmetric.supported(g) for g, _ in need.values()):
             log_dist("symmetric_memory: no intra-node group of <= 8 ranks, keeping RCCL", ranks=[0])
             return False
-        self._symm = {key: symmetric.SymmetricMemory(g, nb) for key, (g, nb) in need.items()}
+        self._install_symm({key: symmetric.SymmetricMemory(g, nb) for key, (g, nb) in need.items()})
+        self._route = None  # forced: symmetric wherever a buffer fits
+        return True
+
+    def _install_symm(self, bufs):
+        """Symmetric buffers {(kind, id(group)): SymmetricMemory} for the unit collectives, their priority streams and
+        the device error flag the step folds (see below)."""
+        self._symm = dict(bufs)
         self._symm_streams = {k: torch.cuda.Stream(device=self.device, priority=-1) for k in ("ag", "rs")}
         # a timed-out exchange raises this device flag (symm_comm.hip): step() folds it, reduced over the data-parallel
         # group, into the skip flag -- the step that consumed stale peer data never updates the weights -- and raises
@@ -1026,7 +1058,39 @@ class ZeroOptimizer:
         self._symm_flag_ev = None
         log_dist(f"symmetric_memory: {len(self._symm)} buffers, "
                  f"{sum(sm.cap for sm in self._symm.values()) * 2 / 2**20:.0f} MiB per rank", ranks=[0])
+
+    def select_transports(self):
+        """``mi355x.zero_comm_transport`` = "auto" at data-parallel size > 1: time rccl / native / symmetric on every
+        unit all-gather and reduce-scatter size class and route each class to the fastest (runtime/zero/transport.py).
+        Collective. The measured table is ``self.comm_selection``."""
+        from .transport import log_table, select_unit_transports
+        if self.stage != 3 or not self.partitioned or getattr(self, "_symm", None) or \
+                getattr(self, "_native", None) is not None:
+            return False  # ZeRO-1/2, nothing partitioned, or a transport forced by compile.* switches
+        mode = str(getattr(self.mi, "zero_comm_transport", "auto"))
+        cands = tuple(t.strip() for t in mode.split(":", 1)[1].split(",")) if ":" in mode else None
+        route, comms, table = select_unit_transports(self.units, self.device, self.dtype, self.comm_dtype,
+                                                     **({"transports": ("rccl", ) + tuple(
+                                                         t for t in cands if t != "rccl")} if cands else {}))
+        self.comm_selection = table
+        if not route:
+            return False
+        self._route = route
+        symm = {(k, g): c for (tr, k, g), c in comms.items() if tr == "symmetric"}
+        if symm:
+            self._install_symm(symm)
+        nat = {g: c for (tr, k, g), c in comms.items() if tr == "native"}
+        if nat:
+            self._native = nat
+        log_table(table)
         return True
+
+    def _transport(self, kind, group, nbytes):
+        r = getattr(self, "_route", None)
+        if not r:
+            return None  # no measured route: whatever enable_symmetric_comm / enable_native_comm set up, else RCCL
+        from .transport import route_for
+        return route_for(r, kind, id(group), nbytes)
 
     def _symm_issue(self, kind, group, nbytes, fn):
         sm = getattr(self, "_symm", {}).get((kind, id(group)))
@@ -1042,22 +1106,27 @@ class ZeroOptimizer:
         return _SymmWork(e0, e1)
 
     def _all_gather(self, out, inp, group):
-        w = self._symm_issue("ag", group, inp.numel() * inp.element_size(),
-                             lambda sm: sm.all_gather_into_tensor(out, inp, dev_status=self._symm_err, check=False))
-        if w is not None:
-            return w
-        c = self._ncomm(group)
+        nb = inp.numel() * inp.element_size()
+        tr = self._transport("ag", group, nb)
+        if tr in (None, "symmetric"):
+            w = self._symm_issue("ag", group, nb,
+                                 lambda sm: sm.all_gather_into_tensor(out, inp, dev_status=self._symm_err, check=False))
+            if w is not None:
+                return w
+        c = self._ncomm(group) if tr in (None, "native") else None
         if c is not None:
             return c.all_gather_into_tensor(out, inp, async_op=True)
         return dist.all_gather_into_tensor(out, inp, group=group, async_op=True)
 
     def _reduce_scatter(self, out, inp, group):
-        if out.numel() % 8 == 0 and inp.dtype == out.dtype:
-            w = self._symm_issue("rs", group, inp.numel() * inp.element_size(),
+        nb = inp.numel() * inp.element_size()
+        tr = self._transport("rs", group, nb)
+        if tr in (None, "symmetric") and out.numel() % 8 == 0 and inp.dtype == out.dtype:
+            w = self._symm_issue("rs", group, nb,
                                  lambda sm: sm.reduce_scatter_tensor(out, inp, dev_status=self._symm_err, check=False))
             if w is not None:
                 return w
-        c = self._ncomm(group)
+        c = self._ncomm(group) if tr in (None, "native") else None
         if c is not None:
             return c.reduce_scatter_tensor(out, inp, async_op=True)
         return dist.reduce_scatter_tensor(out, inp, group=group, async_op=True)
@@ -1143,7 +1212,7 @@ class ZeroOptimizer:
         return bool(self._fwd_trace) and not self._recording and self._fwd_trace[-1] == u.uid
 
     def _pre_backward(self, u):
-        self._gather(u, wait=True)
+        self._fetch(u, "backward")
         if self.partitioned and self._fwd_trace and not self._recording:
             t = self._fwd_trace
             try:
@@ -1161,8 +1230,18 @@ class ZeroOptimizer:
 
     def _issue(self, uids):
         """Compiled schedule: issue the all-gathers planned for this trace position."""
+        name = f"{'backward' if self.in_backward else 'forward'}_prefetch_submit"
+        self.unit_events.start_event(name)
+        issued = 0
         for uid in uids:
-            self._gather(self.units[uid], wait=False)
+            u = self.units[uid]
+            if u.status == NOT_AVAILABLE and self._partitioned(u):
+                issued += u.shard
+            self._gather(u, wait=False)
+        if issued:
+            self.unit_events.stop_event(name, issued)
+        else:
+            self.unit_events.cancel_event(name)
 
     def install_schedule(self, sched):
         """Install a DeepCompile ``CompiledSchedule`` (compile/passes.py): planned prefetch positions replace
@@ -1177,7 +1256,9 @@ class ZeroOptimizer:
         """Issue all-gathers for the next units of ``upcoming`` (uids in use order). Bounded by
         ``zero3_prefetch_depth`` units, or -- when the config names them -- by stage3_prefetch_bucket_size
         elements per prefetch window and stage3_max_live_parameters gathered elements."""
-        n = tot = 0
+        n = tot = issued = 0
+        name = f"{'backward' if self.in_backward else 'forward'}_prefetch_submit"
+        self.unit_events.start_event(name)
         for uid in upcoming:
             u = self.units[uid]
             if self.prefetch_numel is not None:
@@ -1188,9 +1269,15 @@ class ZeroOptimizer:
             if u.status == NOT_AVAILABLE and self.max_live_numel is not None and \
                     self._live_numel() + u.padded > self.max_live_numel:
                 break
+            if u.status == NOT_AVAILABLE and self._partitioned(u):
+                issued += u.shard
             self._gather(u, wait=False)
             n += 1
             tot += u.numel
+        if issued:
+            self.unit_events.stop_event(name, issued)
+        else:
+            self.unit_events.cancel_event(name)
 
     def _compute_reuse_keep(self):
         """Units whose next use (in backward) is within stage3_max_reuse_distance gathered elements stay
@@ -1390,6 +1477,9 @@ class ZeroOptimizer:
     # forward bracket (called by the engine around module.forward)
     # ------------------------------------------------------------------------------------
     def pre_forward(self):
+        if self.unit_events.event_counters:
+            self.unit_events_last = self.unit_events.summary()
+            self.unit_events.reset_events()
         self._last_pre_uid = None
         self._trace_pos = 0
         self._trace_ok = bool(self._fwd_trace) and not self._recording

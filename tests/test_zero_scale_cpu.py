@@ -162,26 +162,41 @@ def test_zero3_coordinator_limits_world2():
 
 
 def test_bench_torchrun_cpu_dry_run():
-    """bench.py exactly as the driver launches it for N>1, on CPU/gloo with the tiny preset."""
+    """bench.py exactly as the driver launches it for N>1 (world 8, as the driver's largest run), on CPU/gloo with
+    the tiny preset."""
+    W = 8
     env = dict(os.environ, OMP_NUM_THREADS="1", HDS_TUNABLEOP="0", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
-           "127.0.0.1", "--master-port", "29731", os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(W), "--master-addr",
+           "127.0.0.1", "--master-port", "29731", os.path.join(ROOT, "bench.py"), "--gpus", str(W), "--steps", "2",
            "--warmup", "1", "--model", "tiny", "--seq", "64", "--micro-batch", "2"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 4 and out["steps"] == 2 and out["warmup"] == 1
-    assert out["config"]["global_batch"] == 8 and out["config"]["parallelism"] == "zero3-dp4"
+    assert out["n_gpus"] == W and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["global_batch"] == 2 * W and out["config"]["parallelism"] == f"zero3-dp{W}"
     assert out["value"] > 0 and out["extra"]["valid"] is False
     # communication evidence the driver's N>1 runs carry (exposed wait, per-collective traffic, per-rank HBM)
     comm = out["extra"]["comm"]
-    assert comm["ranks"] == 4 and len(comm["peak_mem_gib_per_rank"]) == 4
+    assert comm["ranks"] == W and len(comm["peak_mem_gib_per_rank"]) == W
     assert comm["exposed_comm_ms_per_step_max"] >= 0
     coll = comm["rank0"]["collectives"]
     assert coll["all_gather"]["count"] > 0 and coll["reduce_scatter"]["count"] > 0
-    assert coll["all_gather"]["bytes"] > 0 and coll["reduce_scatter"]["world"] == 4
+    assert coll["all_gather"]["bytes"] > 0 and coll["reduce_scatter"]["world"] == W
+    # ZeRO-3 unit events of the instrumented micro-step (reference coordinator events): fetches and waits in both
+    # phases, prefetches once the trace is known, with the elements they moved
+    ev = comm["unit_events_rank0"]
+    for name in ("forward_fetch_wait", "backward_fetch_wait", "forward_prefetch_submit"):
+        assert ev[name]["count"] > 0, (name, ev)
+    assert ev["forward_prefetch_submit"]["numel"] > 0
+    # startup transport measurement: every unit all-gather / reduce-scatter size class timed, one choice each (CPU:
+    # only torch.distributed is available; native / symmetric drop out with a reason)
+    sel = comm["transport_selection"]
+    rows = [r for r in sel if "choice" in r]
+    assert {r["kind"] for r in rows} == {"ag", "rs"}
+    assert all(r["choice"] == "rccl" and r["ms"]["rccl"] > 0 and r["world"] == W for r in rows)
+    assert {r["transport"] for r in sel if r.get("available") is False} == {"native", "symmetric"}
     # the timed steps run uninstrumented; the evidence comes from one extra step and isolated collectives after them
     assert comm["timed_steps_instrumented"] is False and comm["rank0"]["timed_steps_instrumented"] is False
     iso = comm["rank0"]["unit_collectives_isolated"]
