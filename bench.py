@@ -223,6 +223,23 @@ def main():
 
         for i, b in enumerate(blocks):
             b.register_forward_pre_hook(_block_progress(i))
+        ac0 = getattr(engine, "_activation_cache", None)
+        if ac0 is not None:
+            # a checkpointed block's recompute calls its forward directly (no module hooks): report the backward's
+            # position from the cache, and only when it MOVED -- a hung step still goes silent
+            import threading
+
+            def _heartbeat():
+                last = None
+                while True:
+                    time.sleep(20)
+                    st = (ac0.bwd_layer_seen, ac0.cur_layer)
+                    if st != last:
+                        last = st
+                        print(f"[bench] t={time.perf_counter() - t_run:.0f}s backward at block {st[0]}, forward "
+                              f"block {st[1]}", file=sys.stderr, flush=True)
+
+            threading.Thread(target=_heartbeat, daemon=True).start()
 
     def step_progress(tag, i, t_start):
         if progress and rank == 0:

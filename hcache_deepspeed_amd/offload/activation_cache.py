@@ -162,6 +162,7 @@ class HostActivationCache:
         self.last_step_peak = 0  # full peak of the previous step (set at the next forward)
         self.bwd_headroom = None  # largest one-block backward transient seen (bytes), kept free by far prefetches
         self._bwd_layer, self._bwd_mark = None, None
+        self.bwd_layer_seen = None
 
     @classmethod
     def from_config(cls, cfg, device):
@@ -351,6 +352,7 @@ class HostActivationCache:
         self._capped_this_step = 0
         self.stashed_blocks = 0
         self._bwd_layer, self._bwd_mark = None, None
+        self.bwd_layer_seen = None
         self._update_stash_keep()
         timed = self.hybrid and self._hybrid_state == 1 and self.device.type == "cuda"
         if timed:
@@ -474,6 +476,7 @@ class HostActivationCache:
     _DEBUG = os.environ.get("HDS_ACT_CACHE_DEBUG") == "1"
 
     def _prefetch_before(self, layer):
+        self.bwd_layer_seen = layer  # progress marker (bench.py heartbeat): the block backward has reached
         if self._turn_peak is None and self.device.type == "cuda":
             self._turn_peak = torch.cuda.max_memory_allocated(self.device)  # first unpack of the step
         if self.budget is not None and self.device.type == "cuda" and layer != self._bwd_layer:
