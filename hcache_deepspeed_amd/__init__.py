@@ -21,7 +21,19 @@ import os
 # this import covers a script that imports the package before torch. An explicit value is kept.
 import sys as _sys
 
-BLIT_LIMIT_EARLY = "DEBUG_CLR_LIMIT_BLIT_WG" in os.environ or "torch" not in _sys.modules
+
+def _hip_runtime_loaded():
+    """Is the HIP runtime library already mapped into this process (torch loads it at import)?"""
+    try:
+        with open("/proc/self/maps") as f:
+            return any("libamdhip64" in line for line in f)
+    except OSError:
+        return "torch" in _sys.modules
+
+
+# the limit is in effect if the runtime is not loaded yet (set just below, read when it loads) or if the variable was
+# already in the environment at this point -- set by the launcher, bench.py, or the user before importing torch
+BLIT_LIMIT_EARLY = "DEBUG_CLR_LIMIT_BLIT_WG" in os.environ or not _hip_runtime_loaded()
 os.environ.setdefault("DEBUG_CLR_LIMIT_BLIT_WG", "16")
 
 from .version import __version__, __version_major__, __version_minor__, __version_patch__  # noqa: F401

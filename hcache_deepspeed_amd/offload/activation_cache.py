@@ -281,6 +281,12 @@ class HostActivationCache:
         self._peak_fold()
         torch.cuda.reset_peak_memory_stats(self.device)
 
+    def step_peak(self):
+        """Peak allocation of the step running now (since its forward began), across the per-block resets."""
+        if self.device.type != "cuda":
+            return 0
+        return max(self._step_max, torch.cuda.max_memory_allocated(self.device))
+
     def _take_step_peak(self):
         """Start of a forward: the whole previous step's peak (every reset inside it included) -> ``last_step_peak``,
         and a fresh running max for the step that starts now."""
@@ -594,14 +600,40 @@ def plan_offload(layer_bytes, peak_all, budget):
     return set(layers[:k])
 
 
+class BlitLimitError(RuntimeError):
+    """The host activation cache would spill through unlimited runtime blit kernels (see ``check_blit_limit``)."""
+
+
+def check_blit_limit(cfg, device_type, limit_in_effect=None):
+    """Refuse a spilling host activation cache when DEBUG_CLR_LIMIT_BLIT_WG did not reach the HIP runtime.
+
+    Spills are device->host copies, which this ROCm stack runs as blit kernels spread over as many workgroups as the
+    copy has chunks: they take CUs from the forward they overlap (32k tokens, 25 GiB spilled: 10,309 instead of
+    13,949 tok/s, profiles/r4/copy_engine_ab_r4f.txt). The runtime reads the workgroup limit once, when it loads --
+    i.e. at ``import torch`` -- so a script that imported torch before this package, without the variable exported,
+    would silently lose ~25 %. Rather than that, fail loudly with the fix. Policy "recompute" spills nothing and is
+    allowed; ``host_act_cache.allow_unlimited_blit`` (or HDS_ALLOW_UNLIMITED_BLIT=1) accepts the slower spills."""
+    if device_type != "cuda":
+        return
+    if limit_in_effect is None:
+        from .. import BLIT_LIMIT_EARLY as limit_in_effect
+    if limit_in_effect or getattr(cfg, "policy", "budget") == "recompute":
+        return
+    if getattr(cfg, "allow_unlimited_blit", False) or os.environ.get("HDS_ALLOW_UNLIMITED_BLIT") == "1":
+        logger.warning("host activation cache: spills run as unlimited blit kernels (DEBUG_CLR_LIMIT_BLIT_WG was not "
+                       "in the environment when torch loaded the HIP runtime); accepted by allow_unlimited_blit")
+        return
+    raise BlitLimitError(
+        "host activation cache: DEBUG_CLR_LIMIT_BLIT_WG was not in the environment when torch loaded the HIP runtime, "
+        "so activation spills would run as unlimited blit kernels and slow the overlapped forward by ~25 %. Export "
+        "DEBUG_CLR_LIMIT_BLIT_WG=16 before starting Python (the hcache_deepspeed_amd launcher does), or import "
+        "hcache_deepspeed_amd before torch, or set mi355x.host_act_cache.allow_unlimited_blit=true to accept it.")
+
+
 def build_activation_cache(cfg, device):
     """The cache for ``mi355x.host_act_cache`` (``cfg``): policy "plan" is the per-tensor planner
     (offload/act_plan.py), every other policy the block-level cache above."""
-    from .. import BLIT_LIMIT_EARLY
-    if device.type == "cuda" and not BLIT_LIMIT_EARLY:
-        logger.warning("host activation cache: DEBUG_CLR_LIMIT_BLIT_WG was not in the environment before torch was "
-                       "imported, so activation spills run as unlimited blit kernels that slow the overlapped "
-                       "forward; export DEBUG_CLR_LIMIT_BLIT_WG=16 (the launcher does) for spill-heavy plans")
+    check_blit_limit(cfg, device.type)
     if getattr(cfg, "policy", "budget") == "plan":
         from .act_plan import PlannedActivationCache
         return PlannedActivationCache.from_config(cfg, device)

@@ -184,6 +184,8 @@ class HostActCacheConfig:
     # FlashAttention forward
     stash_attention: bool = True
     forced_actions: Optional[dict] = None
+    # accept spills through unlimited runtime blit kernels (DEBUG_CLR_LIMIT_BLIT_WG missing when HIP loaded)
+    allow_unlimited_blit: bool = False
 
 
 AUTO = -1

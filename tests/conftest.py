@@ -1,7 +1,11 @@
 import os
 import sys
 
-import pytest
+# the GPU tests spill activations: the blit workgroup limit must reach the HIP runtime, i.e. be in the environment
+# before any test module imports torch (hcache_deepspeed_amd.offload.activation_cache.check_blit_limit)
+os.environ.setdefault("DEBUG_CLR_LIMIT_BLIT_WG", "16")
+
+import pytest  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

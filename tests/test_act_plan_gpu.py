@@ -84,3 +84,51 @@ def test_planner_through_engine_under_budget():
     assert st["recipe_ms"], st
     assert st["recompute_gib_planned"] > 0 or st["spill_gib_planned"] > 0, st
     assert st["late_unpacks"] == 0, st
+
+
+@pytest.mark.parametrize("policy", ["plan", "budget", "recompute"])
+def test_budget_is_a_cap(policy):
+    """A FEASIBLE HBM budget below the unbudgeted peak: after calibration every step's peak allocation (the running max
+    across the cache's per-block peak resets) stays within the budget, and the plan frees activations to get there."""
+    import hcache_deepspeed_amd as hds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    os.environ.setdefault("MASTER_PORT", "29564")
+
+    def engine(act_cfg):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(num_hidden_layers=8, hidden_size=512, intermediate_size=1536, vocab_size=512))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "bf16": {"enabled": True},
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "zero_optimization": {"stage": 3}}
+        if act_cfg:
+            cfg["mi355x"] = {"host_act_cache": act_cfg}
+        return hds.initialize(model=m, config=cfg)[0]
+
+    x = torch.randint(0, 512, (2, 4096), device="cuda")
+    eng = engine(None)
+    for i in range(2):
+        if i == 1:  # after one step: weights, optimizer states and gradient buffers exist, activations are gone
+            torch.cuda.synchronize()
+            base = torch.cuda.memory_allocated()
+            torch.cuda.reset_peak_memory_stats()
+        loss = eng(x, labels=x)
+        eng.backward(loss)
+        eng.step()
+    torch.cuda.synchronize()
+    full = torch.cuda.max_memory_allocated()
+    del eng, loss
+    torch.cuda.empty_cache()
+    budget = base + int(0.6 * (full - base))  # 40 % of the step's activation HBM must go
+    eng = engine({"enabled": True, "policy": policy, "min_layers_resident": 1, "gpu_budget_gib": budget / 2**30})
+    cache = eng._activation_cache
+    peaks = []
+    for _ in range(6):
+        loss = eng(x, labels=x)
+        eng.backward(loss)
+        eng.step()
+        torch.cuda.synchronize()
+        peaks.append(cache.step_peak())
+    st = cache.stats()
+    # steps 0-1 calibrate / time the plan; from then on the cap holds (1 MiB of slack: allocator rounding)
+    over = [p - budget for p in peaks[2:] if p > budget + (1 << 20)]
+    assert not over, (policy, [round(p / 2**20, 1) for p in peaks], round(budget / 2**20, 1), st)
+    assert max(peaks[2:]) < full, (peaks, full)

@@ -497,3 +497,42 @@ def test_step_peak_survives_per_block_resets(monkeypatch):
     assert c.stats()["peak_gib_all_steps"] == 60.0
     # room 85 - 60 = 25 GB -> 6 blocks of 4 GB keep their stash on the device
     assert c.stash_keep_from == 10 - 6
+
+
+def test_blit_limit_check_branches(monkeypatch):
+    """A spilling host activation cache refuses to start when DEBUG_CLR_LIMIT_BLIT_WG did not reach the HIP runtime
+    (a script that imported torch first); recompute-only, the explicit opt-out and the in-effect case pass."""
+    import types
+    from hcache_deepspeed_amd.offload.activation_cache import BlitLimitError, check_blit_limit
+    monkeypatch.delenv("HDS_ALLOW_UNLIMITED_BLIT", raising=False)
+    cfg = types.SimpleNamespace(policy="ckpt_offload", allow_unlimited_blit=False)
+    check_blit_limit(cfg, "cuda", limit_in_effect=True)
+    check_blit_limit(cfg, "cpu", limit_in_effect=False)  # CPU tensors: no blit kernels
+    with pytest.raises(BlitLimitError, match="DEBUG_CLR_LIMIT_BLIT_WG"):
+        check_blit_limit(cfg, "cuda", limit_in_effect=False)
+    for pol in ("budget", "plan", "auto", "all"):
+        with pytest.raises(BlitLimitError):
+            check_blit_limit(types.SimpleNamespace(policy=pol), "cuda", limit_in_effect=False)
+    check_blit_limit(types.SimpleNamespace(policy="recompute"), "cuda", limit_in_effect=False)
+    check_blit_limit(types.SimpleNamespace(policy="plan", allow_unlimited_blit=True), "cuda", limit_in_effect=False)
+    monkeypatch.setenv("HDS_ALLOW_UNLIMITED_BLIT", "1")
+    check_blit_limit(cfg, "cuda", limit_in_effect=False)
+
+
+@pytest.mark.parametrize("order,env,expect", [("torch_first", False, False), ("torch_first", True, True),
+                                              ("package_first", False, True)])
+def test_blit_limit_detection_by_import_order(order, env, expect):
+    """BLIT_LIMIT_EARLY: True iff the variable reached the HIP runtime -- the package imported before torch (it sets
+    the variable before the runtime library loads), or the variable exported beforehand."""
+    import subprocess
+    import sys
+    imports = "import torch; import hcache_deepspeed_amd as h" if order == "torch_first" else \
+        "import hcache_deepspeed_amd as h; import torch"
+    e = {k: v for k, v in os.environ.items() if k != "DEBUG_CLR_LIMIT_BLIT_WG"}
+    if env:
+        e["DEBUG_CLR_LIMIT_BLIT_WG"] = "16"
+    r = subprocess.run([sys.executable, "-c", imports + "; print('EARLY', h.BLIT_LIMIT_EARLY)"], env=e,
+                       capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert f"EARLY {expect}" in r.stdout, r.stdout
