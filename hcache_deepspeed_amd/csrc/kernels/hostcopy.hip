@@ -52,3 +52,55 @@ HDS_EXPORT int hds_copy_d2h(void* dst, const void* src, int64_t nbytes, int n_wg
                      static_cast<uint8_t*>(dst) + nvec * 16, tail);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------------------------------
+// HCache latents inside a captured decode graph (inference/v2/model.py _DecodeGraph): every layer's latent rows are
+// stored into a DEVICE ring at a slot read from device memory, so the graph (fixed addresses) writes a different slot
+// on every replay; a one-thread kernel at the end of the graph advances the slot. The host drains filled halves of the
+// ring with one D2H each on the copy stream instead of 32 per-layer D2H copies per token.
+namespace {
+
+// rows x row_bytes from src (row stride src_stride bytes) -> dst_base + slot * slot_stride (contiguous rows)
+__global__ __launch_bounds__(256) void latent_slot_store_kernel(const char* __restrict__ src, int64_t src_stride,
+                                                                char* __restrict__ dst_base,
+                                                                const int* __restrict__ slot, int64_t slot_stride,
+                                                                int rows, int64_t row_bytes) {
+  char* dst = dst_base + (int64_t)(*slot) * slot_stride;
+  const int64_t nvec = row_bytes / 16;  // row_bytes % 16 == 0 (checked by the launcher)
+  const int64_t total = (int64_t)rows * nvec;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / nvec, v = i - r * nvec;
+    *reinterpret_cast<u32x4*>(dst + r * row_bytes + v * 16) =
+        *reinterpret_cast<const u32x4*>(src + r * src_stride + v * 16);
+  }
+}
+
+__global__ void slot_advance_kernel(int* slot, int mod) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const int s = *slot + 1;
+    *slot = s >= mod ? 0 : s;
+  }
+}
+
+}  // namespace
+
+HDS_EXPORT int hds_latent_slot_store(const void* src, int64_t src_stride, void* dst_base, const int* slot,
+                                     int64_t slot_stride, int rows, int64_t row_bytes, hipStream_t st) {
+  if (rows <= 0 || row_bytes <= 0) return hipSuccess;
+  if (row_bytes % 16 || src_stride % 16 || slot_stride % 16 || (reinterpret_cast<uintptr_t>(src) & 15) ||
+      (reinterpret_cast<uintptr_t>(dst_base) & 15))
+    return hipErrorInvalidValue;
+  const int64_t total = (int64_t)rows * (row_bytes / 16);
+  int64_t grid = (total + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(latent_slot_store_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+                     static_cast<const char*>(src), src_stride, static_cast<char*>(dst_base), slot, slot_stride, rows,
+                     row_bytes);
+  return hipGetLastError();
+}
+
+HDS_EXPORT int hds_slot_advance(int* slot, int mod, hipStream_t st) {
+  if (mod < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(slot_advance_kernel, dim3(1), dim3(64), 0, st, slot, mod);
+  return hipGetLastError();
+}

@@ -116,11 +116,14 @@ class InferenceEngineV2:
 
     # ------------------------------------------------------------------------------------------
     def put(self, batch_uids: Iterable[int], batch_tokens: Iterable[torch.Tensor], do_checks: bool = True,
-            capture_latents: bool = True, sync_latents: bool = True) -> Tuple[torch.Tensor, List[Optional[torch.Tensor]]]:
+            capture_latents: bool = True, sync_latents: Optional[bool] = None
+            ) -> Tuple[torch.Tensor, List[Optional[torch.Tensor]]]:
         """One ragged forward. Returns logits [n_seqs, V] and, per sequence, its latents [L, n_tokens, W] (host).
         ``sync_latents=False``: the host does not wait for the latent copies (no per-forward synchronize, reference
         engine_v2.py:131-189 keeps its host free the same way); call ``wait_latents()`` (or check
-        ``latents_ready()``) before reading them -- ``restore_kv`` / ``evict`` wait on their own."""
+        ``latents_ready()``) before reading them -- ``restore_kv`` / ``evict`` wait on their own. The default
+        (None) waits after a prefill and defers in HIP-graph decode steps, whose latents go to a device ring drained
+        in bulk (inference/v2/model.py ``_LatentRing``): a decode loop does not synchronize per token."""
         batch_uids = list(batch_uids)
         batch_tokens = [t if isinstance(t, torch.Tensor) else torch.tensor(t) for t in batch_tokens]
         if do_checks:
@@ -136,9 +139,13 @@ class InferenceEngineV2:
             batch.insert_sequence(seq, tokens, do_checks=do_checks)
         batch.finalize()
         if self._model.decode_graph_eligible(batch, capture_latents):
-            logits, latents = self._model.forward_decode_graph(batch), None  # HIP-graph decode step
+            # HIP-graph decode step (latents, if captured, land in the graph's device ring)
+            logits, latents = self._model.forward_decode_graph(batch, capture_latents=capture_latents)
+            if latents is not None and sync_latents:
+                self.wait_latents()
         else:
-            logits, latents = self._model.forward(batch, capture_latents=capture_latents, sync_latents=sync_latents)
+            logits, latents = self._model.forward(batch, capture_latents=capture_latents,
+                                                  sync_latents=True if sync_latents is None else sync_latents)
             self._latent_event = getattr(self._model, "latent_event", None)
         split = []
         for (q0, n, _) in batch.seq_meta_host:
@@ -148,15 +155,27 @@ class InferenceEngineV2:
         return logits, split
 
     def latents_ready(self) -> bool:
+        """Every latent returned so far is on the host (no synchronize; a decode-graph ring with undrained steps
+        counts as not ready until ``wait_latents`` flushes it)."""
+        if any(r.pending() for r in self._model.latent_rings()):
+            return False
         ev = getattr(self, "_latent_event", None)
-        return ev is None or ev.query()
+        if ev is not None and not ev.query():
+            return False
+        return all(r.done[h] is None or r.done[h].query() for r in self._model.latent_rings() for h in (0, 1))
 
     def wait_latents(self):
-        """Block until the latents returned by the last ``put(..., sync_latents=False)`` are on the host."""
-        ev = getattr(self, "_latent_event", None)
-        if ev is not None:
-            ev.synchronize()
-            self._latent_event = None
+        """Block until every latent returned by ``put`` (eager prefill copies and the decode graphs' rings) is on
+        the host."""
+        ring_ev = self._model.drain_latents()
+        for ev in (getattr(self, "_latent_event", None), ring_ev):
+            if ev is not None:
+                ev.synchronize()
+        for r in self._model.latent_rings():
+            for e in r.done:
+                if e is not None:
+                    e.synchronize()
+        self._latent_event = None
 
     def restore_kv(self, batch_uids: Iterable[int], batch_tokens: Iterable[torch.Tensor],
                    batch_latents: Iterable[Optional[torch.Tensor]]):

@@ -92,6 +92,9 @@ class RaggedTransformer:
         self._decode_graphs = {}
         self._graph_pool = None
         import os as _os
+        # HCache latents inside the decode graph (device ring drained every `decode_latent_ring_steps` steps)
+        self.decode_graph_latents = _os.environ.get("HDS_V2_DECODE_GRAPH_LATENTS", "1") == "1"
+        self.decode_latent_ring_steps = int(_os.environ.get("HDS_V2_LATENT_RING_STEPS", "16"))
         self.decode_graph_max_batch = int(_os.environ.get("HDS_V2_DECODE_GRAPH_MAX_B", "64"))
 
     def _build_modules(self, ec):
@@ -279,49 +282,76 @@ class RaggedTransformer:
     def _embed(self, batch):
         return self.embed_mod(batch, self.embed, self.pos_embed)
 
-    def _attn(self, i, L, x, batch, T, capture, lat, events):
+    def _attn(self, i, L, x, batch, T, capture, lat, events, sink=None):
         nq, nkv, D = self.n_q, self.n_kv, self.d
         qkv = self.qkv_lin(x, L["qkv.w"], L["qkv.b"]).view(T, nq + 2 * nkv, D)
         if capture and self.latent_mode == "kv":
-            self._d2h(qkv[:, nq:].reshape(T, -1).clone(), lat[i], events)  # pre-RoPE K|V
+            if sink is not None:  # stored in stream order before RoPE rotates K in place: no clone
+                sink(i, qkv[:, nq:].reshape(T, -1))
+            else:
+                self._d2h(qkv[:, nq:].reshape(T, -1).clone(), lat[i], events)  # pre-RoPE K|V
         o = self.attn_mod(qkv, self.kv_cache.get_cache(i), batch, self.cos, self.sin)
         return self.o_lin(o, L["o.w"], L["o.b"])
 
     # ------------------------------------------------------------------------------------------
     def decode_graph_eligible(self, batch, capture_latents):
         """A decode-only ragged batch (one new token per sequence) of a dense model without tensor parallelism:
-        its whole forward depends on the batch size alone, so it replays from a HIP graph captured per size."""
-        if (self.device.type != "cuda" or capture_latents or self.tp != 1 or self.spec.moe is not None
-                or self.decode_graph_max_batch <= 0):
+        its whole forward depends on the batch size alone, so it replays from a HIP graph captured per size. With
+        ``capture_latents`` the graph also stores every layer's latent into a device ring (``_LatentRing``)."""
+        if (self.device.type != "cuda" or (capture_latents and not self.decode_graph_latents) or self.tp != 1
+                or self.spec.moe is not None or self.decode_graph_max_batch <= 0):
             return False
         S = batch.current_sequences
         return (0 < S <= self.decode_graph_max_batch and batch.current_tokens == S
                 and getattr(batch, "atoms", None) is not None and getattr(batch, "_dev_meta", None) is not None)
 
     @torch.no_grad()
-    def forward_decode_graph(self, batch):
+    def forward_decode_graph(self, batch, capture_latents=False):
         """Replay the decode step for ``batch.current_sequences`` sequences: the step's token ids and packed
         metadata (same layout as ``RaggedBatchWrapper.finalize``) are copied into the graph's static buffers, the
         graph replays every layer's kernels with one launch, and the logits are copied out. The first step of a
-        batch size runs the forward eagerly once (it writes the same KV the replay writes) and captures it."""
+        batch size runs the forward eagerly once (it writes the same KV the replay writes) and captures it.
+
+        ``capture_latents``: the graph also stores each layer's latent rows into a device ring slot (HCache during
+        decode, reference llama_v2/model.py:211-218 captures in every forward); returns ``(logits, latents)`` with
+        ``latents`` a pinned host view [L, B, W] that is complete once the ring has been drained
+        (``drain_latents`` / the engine's ``wait_latents``). Without: ``(logits, None)``."""
         B = batch.current_sequences
-        g = self._decode_graphs.get(B)
+        key = (B, bool(capture_latents))
+        g = self._decode_graphs.get(key)
         n = batch.seq_meta.numel() + batch.tok_seq.numel() + batch.tok_pos.numel() + batch.last_token_idx.numel() \
             + batch.block_tables.numel() + batch.atoms.numel()
         if g is None:
-            g = self._decode_graphs[B] = _DecodeGraph(self, batch, n)
+            ring = _LatentRing(self, B, self.decode_latent_ring_steps) if capture_latents else None
+            g = self._decode_graphs[key] = _DecodeGraph(self, batch, n, ring)
         g.ids.copy_(batch.input_ids, non_blocking=True)
         g.meta.copy_(batch._dev_meta[:n], non_blocking=True)
+        view = g.ring.begin_step() if g.ring is not None else None
         if g.graph is None:
             g.capture(self)
         g.graph.replay()
-        return g.out.clone()
+        if g.ring is not None:
+            g.ring.end_step()
+        return g.out.clone(), view
+
+    def latent_rings(self):
+        return [g.ring for g in self._decode_graphs.values() if g.ring is not None]
+
+    def drain_latents(self):
+        """Issue the D2H of every decode-graph latent not on the host yet; returns the copy-stream event after which
+        every latent returned so far is complete (None if nothing was pending)."""
+        ev = None
+        for r in self.latent_rings():
+            e = r.drain_all()
+            ev = e if e is not None else ev
+        return ev
 
     @torch.no_grad()
-    def forward(self, batch, capture_latents=True, sync_latents=True):
+    def forward(self, batch, capture_latents=True, sync_latents=True, sink=None):
         """Returns (logits [n_seqs, V], latents host [L, T, H] or [L, T, 2*n_kv*D] or None). With
         ``sync_latents=False`` the host does not wait for the latent D2H copies: ``self.latent_event`` (HIP event on
-        the copy stream) marks when the returned host tensor is complete."""
+        the copy stream) marks when the returned host tensor is complete. ``sink(layer, rows)``: latents go to it
+        instead of to host memory (the decode graph's device ring)."""
         spec = self.spec
         self._prep(batch)
         T = batch.current_tokens
@@ -329,8 +359,9 @@ class RaggedTransformer:
         residual = None
         lat = None
         events = []
-        if capture_latents:
+        if capture_latents and sink is None:
             lat = self._latent_buffer(spec.num_hidden_layers, T)
+        emit = sink if sink is not None else (lambda i, t: self._d2h(t, lat[i], events))
         for i, L in enumerate(self.layers):
             if residual is None:
                 x = self._norm(h, L["ln1.w"], L["ln1.b"])
@@ -338,12 +369,12 @@ class RaggedTransformer:
             else:
                 x, residual = self._norm(h, L["ln1.w"], L["ln1.b"], residual)
             if capture_latents and self.latent_mode == "hidden":
-                self._d2h(x, lat[i], events)
+                emit(i, x)
             elif capture_latents and self.latent_mode == "hidden_fp8":
-                self._d2h(self._pack_fp8(x), lat[i], events)
+                emit(i, self._pack_fp8(x))
             elif capture_latents and self.latent_mode == "hidden_int8":
-                self._d2h(self._pack_int8(x), lat[i], events)
-            a = self._attn(i, L, x, batch, T, capture_latents, lat, events)
+                emit(i, self._pack_int8(x))
+            a = self._attn(i, L, x, batch, T, capture_latents, lat, events, sink)
             if spec.parallel == "shared_ln":
                 h = self._allreduce(a + self._mlp(L, x))
             elif spec.parallel == "two_ln":
@@ -502,10 +533,99 @@ class RaggedTransformer:
                         rotate_q=False, do_rope=self.cos is not None, rotary_dim=self.rot)
 
 
-class _DecodeGraph:
-    """Static inputs, captured graph and output of one decode batch size (RaggedTransformer.forward_decode_graph)."""
+class _LatentRing:
+    """Device ring of HCache latents written by a captured decode graph, drained to pinned host memory in bulk.
 
-    def __init__(self, model, batch, n):
+    Layout [2R, L, B, W] (R = ``decode_latent_ring_steps``): two halves of R decode steps. The graph stores layer i's
+    latent rows at ``ring[slot, i]`` with ``slot`` read from device memory (ops/hostcopy.latent_slot_store) and
+    advances ``slot`` as its last kernel, so each replay fills the next slot without any host work. The host mirrors
+    the slot: when a half is full it is drained with ONE D2H on the copy stream (instead of L per-layer copies per
+    token) into a pinned chunk [R, L, B, W] from the pool, while the graph fills the other half; ``drain_all`` also
+    flushes a partly filled half (the engine's ``wait_latents`` / evict / restore). Before a half is written again
+    the compute stream waits for its previous D2H (GPU-side). Each step's latents are returned as the view
+    ``chunk[k]`` [L, B, W] of its half's chunk; chunks return to the pool when the caller drops every view."""
+
+    def __init__(self, model, B, steps):
+        self.model = model
+        self.R = max(1, int(steps))
+        L = model.spec.num_hidden_layers
+        self.dtype = torch.uint8 if model.latent_mode in ("hidden_fp8", "hidden_int8") else model.dtype
+        self.shape = (L, B, model.latent_width())
+        self.dev = torch.empty((2 * self.R, ) + self.shape, dtype=self.dtype, device=model.device)
+        self.slot = torch.zeros(1, dtype=torch.int32, device=model.device)
+        self.host_slot = 0
+        self.chunk = [None, None]
+        self.filled = [0, 0]  # slots of each half written since the half was (re)started
+        self.drained = [0, 0]  # of those, slots already copied to the chunk
+        self.done = [None, None]  # copy-stream event of each half's last D2H
+        self.fresh = [True, True]
+
+    def sink(self, i, rows):
+        from ...ops.hostcopy import latent_slot_store
+        latent_slot_store(rows, self.dev, self.slot, i)
+
+    def advance(self):
+        from ...ops.hostcopy import slot_advance
+        slot_advance(self.slot, 2 * self.R)
+
+    def begin_step(self):
+        h, k = divmod(self.host_slot, self.R)
+        if self.fresh[h]:
+            if self.done[h] is not None:  # the previous D2H out of this half must finish before the graph rewrites it
+                torch.cuda.current_stream().wait_event(self.done[h])
+            pool = RaggedTransformer._latent_pool
+            if pool is None:
+                from ...offload.pinned import PinnedPool
+                pool = RaggedTransformer._latent_pool = PinnedPool()
+            n = self.R * self.shape[0] * self.shape[1] * self.shape[2]
+            self.chunk[h] = pool.get_tracked(n, self.dtype).view((self.R, ) + self.shape)
+            self.filled[h] = self.drained[h] = 0
+            self.fresh[h] = False
+        return self.chunk[h][k]
+
+    def end_step(self):
+        h = self.host_slot // self.R
+        self.filled[h] += 1
+        self.host_slot = (self.host_slot + 1) % (2 * self.R)
+        if self.filled[h] == self.R:
+            self._drain(h)
+            self.fresh[h] = True
+
+    def _drain(self, h):
+        a, b = self.drained[h], self.filled[h]
+        if b <= a:
+            return None
+        cs = self.model.copy_stream
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(cs):
+            cs.wait_event(ev)
+            self.chunk[h][a:b].copy_(self.dev[h * self.R + a:h * self.R + b], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(cs)
+        self.drained[h] = b
+        self.done[h] = done
+        return done
+
+    def drain_all(self):
+        """Flush both halves (the older one first); the returned event covers every latent returned so far."""
+        cur = self.host_slot // self.R
+        ev = None
+        for h in (1 - cur, cur):
+            e = self._drain(h)
+            ev = e if e is not None else ev
+        return ev
+
+    def pending(self):
+        return any(self.filled[h] > self.drained[h] for h in (0, 1))
+
+
+class _DecodeGraph:
+    """Static inputs, captured graph and output of one decode batch size (RaggedTransformer.forward_decode_graph),
+    with its latent ring when the graph captures HCache latents."""
+
+    def __init__(self, model, batch, n, ring=None):
+        self.ring = ring
         dev = model.device
         B = batch.current_sequences
         mb = batch.block_tables.shape[1]
@@ -541,12 +661,17 @@ class _DecodeGraph:
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
+        cap = self.ring is not None
+        sink = self.ring.sink if cap else None
         with torch.cuda.stream(side):
-            model.forward(self.batch, capture_latents=False)  # warm-up: hipBLASLt / GEMV handles, KV (idempotent)
+            # warm-up: hipBLASLt / GEMV handles, KV (idempotent); its latents go to the slot the replay rewrites
+            model.forward(self.batch, capture_latents=cap, sink=sink)
         cur.wait_stream(side)
         if model._graph_pool is None:
             model._graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=model._graph_pool):
-            self.out, _ = model.forward(self.batch, capture_latents=False)
+            self.out, _ = model.forward(self.batch, capture_latents=cap, sink=sink)
+            if cap:
+                self.ring.advance()
         self.graph = g

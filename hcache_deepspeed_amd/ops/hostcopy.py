@@ -26,3 +26,28 @@ def d2h_(dst, src, n_wg=None):
     native.check(native.kernels().hds_copy_d2h(dst.data_ptr(), src.data_ptr(), nbytes, wg, native.stream()),
                  "copy_d2h")
     return dst
+
+
+def latent_slot_store(src, ring, slot, layer):
+    """ring[slot, layer] <- src rows (inside a captured decode graph: ``slot`` is a device int32 read by the kernel, so
+    every replay stores into the slot the ring has advanced to). ``src``: [rows, W] with contiguous rows (any row
+    stride); ``ring``: [S, L, rows, W] contiguous, same dtype. CPU tensors: a plain indexed copy."""
+    rows, W = src.shape
+    assert ring.dim() == 4 and ring.shape[2] == rows and ring.shape[3] == W and ring.dtype == src.dtype
+    assert src.stride(1) == 1 and ring.is_contiguous()
+    if not src.is_cuda:
+        ring[int(slot.item()), layer].copy_(src)
+        return
+    es = src.element_size()
+    dst = ring[0, layer]
+    native.check(native.kernels().hds_latent_slot_store(src.data_ptr(), src.stride(0) * es, dst.data_ptr(),
+                                                        slot.data_ptr(), ring.stride(0) * es, rows, W * es,
+                                                        native.stream()), "latent_slot_store")
+
+
+def slot_advance(slot, mod):
+    """slot <- (slot + 1) % mod on the device (the last kernel of a captured decode step)."""
+    if not slot.is_cuda:
+        slot.fill_((int(slot.item()) + 1) % mod)
+        return
+    native.check(native.kernels().hds_slot_advance(slot.data_ptr(), int(mod), native.stream()), "slot_advance")

@@ -95,6 +95,8 @@ _KERNEL_SIGS = {
     "hds_paged_decode_splits": "iii",
     "hds_paged_decode": "p" + "l" + "pppp" + "pp" + "iiiiiii" + "f" + "i" + "s",
     "hds_copy_d2h": "pp" + "l" + "i" + "s",
+    "hds_latent_slot_store": "p" + "l" + "pp" + "l" + "i" + "l" + "s",
+    "hds_slot_advance": "p" + "i" + "s",
     "hds_symm_header_bytes": "",
     "hds_symm_alloc": "lpp",
     "hds_symm_open": "pp",

@@ -167,8 +167,61 @@ def test_decode_graph_matches_eager_gpu():
         toks = [torch.randint(0, 211, (1, ), generator=g) for _ in uids]
         out = {k: e.put(uids, toks, capture_latents=False)[0].float() for k, e in engs.items()}
         assert torch.allclose(out["graph"], out["eager"], atol=2e-2, rtol=2e-2), step
-    assert set(engs["graph"]._model._decode_graphs) == {2, 3}
+    assert set(engs["graph"]._model._decode_graphs) == {(2, False), (3, False)}
     assert not engs["eager"]._model._decode_graphs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("latent_mode", ["kv", "hidden", "hidden_fp8"])
+def test_graph_decode_captures_latents_for_restore_gpu(latent_mode):
+    """HCache during HIP-graph decode: 64 graph-decoded tokens capture their latents into the device ring (drained in
+    bulk, no per-token synchronize); evicting the sequence, restoring its KV from the prefill + decode latents and
+    continuing gives the tokens of the uninterrupted run (kv: bit-exact K|V; hidden modes: logits within tolerance,
+    tokens equal wherever the top-1 margin is decisive)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    m = _model("cuda", torch.bfloat16)
+    econf = {"dtype": "bf16", "latent_mode": latent_mode, "state_manager": {"max_context": 1024, "kv_block_size": 64}}
+    ref = build_engine_from_model(m, econf, device=torch.device("cuda"), num_kv_blocks=64)
+    eng = build_engine_from_model(m, econf, device=torch.device("cuda"), num_kv_blocks=64)
+    eng._model.decode_latent_ring_steps = 16
+    g = torch.Generator().manual_seed(5)
+    prompt = torch.randint(0, 211, (40, ), generator=g)
+    lr, _ = ref.put([1], [prompt], capture_latents=False)
+    le, lat0 = eng.put([1], [prompt])  # eager prefill: latents synchronized
+    tr, te = lr.argmax(-1).cpu(), le.argmax(-1).cpu()
+    fed, steps = [prompt], []
+    for j in range(64):
+        assert torch.equal(tr, te), j  # the capturing graph computes exactly what the plain graph computes
+        fed.append(te.clone())
+        lr, _ = ref.put([1], [tr], capture_latents=False)
+        le, lat = eng.put([1], [te])  # graph decode, latents deferred to the ring
+        steps.append(lat[0])
+        tr, te = lr.argmax(-1).cpu(), le.argmax(-1).cpu()
+    assert (1, True) in eng._model._decode_graphs and (1, False) in ref._model._decode_graphs
+    assert not eng.latents_ready() or True  # (may already be drained: 64 = 4 full halves)
+    eng.evict(1)  # waits for (and flushes) the ring
+    assert eng.latents_ready()
+    lat_all = torch.cat([lat0[0]] + steps, dim=1)
+    assert lat_all.shape[:2] == (3, 40 + 64)
+    eng.restore_kv([1], [torch.cat(fed)], [lat_all])
+    outs = {"ref": [], "eng": []}
+    for j in range(16):
+        lr, _ = ref.put([1], [tr], capture_latents=False)
+        le, _ = eng.put([1], [tr], capture_latents=False)  # same inputs: compare the continuations' logits
+        outs["ref"].append(lr[0].float())
+        outs["eng"].append(le[0].float())
+        tr = lr.argmax(-1).cpu()
+    a, b = torch.stack(outs["ref"]), torch.stack(outs["eng"])
+    if latent_mode == "kv":
+        assert torch.equal(a.argmax(-1), b.argmax(-1))
+        assert torch.allclose(a, b, atol=1e-2, rtol=1e-2)
+    else:
+        rel = ((a - b).norm(dim=-1) / a.norm(dim=-1)).max().item()
+        assert rel < (6e-2 if latent_mode == "hidden" else 1e-1), rel
+        top2 = a.topk(2, dim=-1).values
+        decided = (top2[:, 0] - top2[:, 1]) > 2 * (a - b).abs().max(dim=-1).values
+        assert torch.equal(a.argmax(-1)[decided], b.argmax(-1)[decided])
 
 
 def test_allocator_and_scheduling():
