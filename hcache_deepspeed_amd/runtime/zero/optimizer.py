@@ -1687,7 +1687,9 @@ class ZeroOptimizer:
         symm = bool(getattr(self, "_symm", None))
         if symm:
             self._symm_check_failed()
-        self._states_resident()
+        so = self.state_offload
+        if so is not None:
+            so.wait_tails()  # split states: heads resident, tails reloaded -- the kernels run per piece below
         inv = 1.0 / (self.layout_world_for_avg() * self.loss_scaler.loss_scale)
         self._norm_buf.zero_()
         self._inf_buf.zero_()
@@ -1718,21 +1720,31 @@ class ZeroOptimizer:
             if getattr(self, "param_offload_gpu_step", False):
                 lp_flat = torch.empty(s.numel, dtype=self.dtype, device=self.device)
                 self._step_lp = lp_flat
+            cuts = so.cuts() if so is not None else ()
+
+            def sv(k, lo, hi):  # [lo, hi) of a state inside one piece (byte-granular state offload splits them)
+                if so is not None and so.split:
+                    return so.view(k, lo, hi)
+                return (s.master if k == "master" else s.states[k])[lo:hi]
+
             for sg in s.segments:
                 g = self._seg_group(sg)
-                p32, gr, lp = s.seg(s.master, sg), s.seg(s.grad, sg), s.seg(lp_flat, sg)
-                if self.kind == "adam":
-                    fused.adam_flat(p32, gr, s.seg(s.states["exp_avg"], sg), s.seg(s.states["exp_avg_sq"], sg),
-                                    g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
-                                    g.get("weight_decay", 0.0), self.adamw, g.get("bias_correction", True),
-                                    lp_out=lp, grad_scale=1.0, dev_scale=coef, found_inf=found_inf)
-                elif self.kind == "lion":
-                    fused.lion_flat(p32, gr, s.seg(s.states["exp_avg"], sg), g["lr"] * g.get("lr_mult", 1.0),
-                                    tuple(g.get("betas", (0.9, 0.99))), g.get("weight_decay", 0.0), lp_out=lp,
-                                    dev_scale=coef, found_inf=found_inf)
-                elif self.kind == "adagrad":
-                    fused.adagrad_flat(p32, gr, s.seg(s.states["sum"], sg), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
-                                       g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
+                lo0, hi0 = sg.store_off, sg.store_off + sg.numel
+                bounds = [lo0] + [c for c in cuts if lo0 < c < hi0] + [hi0]
+                for lo, hi in zip(bounds[:-1], bounds[1:]):
+                    p32, gr, lp = sv("master", lo, hi), s.grad[lo:hi], lp_flat[lo:hi]
+                    if self.kind == "adam":
+                        fused.adam_flat(p32, gr, sv("exp_avg", lo, hi), sv("exp_avg_sq", lo, hi),
+                                        g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
+                                        g.get("weight_decay", 0.0), self.adamw, g.get("bias_correction", True),
+                                        lp_out=lp, grad_scale=1.0, dev_scale=coef, found_inf=found_inf)
+                    elif self.kind == "lion":
+                        fused.lion_flat(p32, gr, sv("exp_avg", lo, hi), g["lr"] * g.get("lr_mult", 1.0),
+                                        tuple(g.get("betas", (0.9, 0.99))), g.get("weight_decay", 0.0), lp_out=lp,
+                                        dev_scale=coef, found_inf=found_inf)
+                    elif self.kind == "adagrad":
+                        fused.adagrad_flat(p32, gr, sv("sum", lo, hi), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
+                                           g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
         tmp = self.__dict__.pop("_step_lp", None)
         if tmp is not None:
             self._publish_lp(tmp)
@@ -1930,6 +1942,7 @@ class ZeroOptimizer:
 
     def _master_to_lp(self):
         self._lp_wait()
+        self._states_resident()  # whole flat master (byte-granular state offload keeps it split)
         self.store.lp.copy_(self.store.master)
         for u in self.units:
             if getattr(u, "dev_shard", None) is not None:
@@ -1948,6 +1961,7 @@ class ZeroOptimizer:
 
     def _lp_to_master(self):
         self._lp_wait()
+        self._states_resident()
         self.store.master.copy_(self.store.lp)
 
     # ------------------------------------------------------------------------------------
@@ -1966,6 +1980,7 @@ class ZeroOptimizer:
         params are also gathered over their EP group and named/stacked by global expert id)."""
         from ...checkpoint.zero_to_fp32 import expert_global_name
         out = {}
+        self._states_resident()
         for u in self.units:
             m = self.store.master[u.store_off:u.store_off + u.shard]
             full = torch.empty(u.padded, dtype=torch.float32, device=self.device)

@@ -150,7 +150,7 @@ def test_state_reload_placement():
     assert pos == 4
 
 
-def _state_offload_run(rank, world, stage, out):
+def _state_offload_run(rank, world, stage, out, ratio=1.0):
     import os
     import hcache_deepspeed_amd as ds
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
@@ -163,7 +163,7 @@ def _state_offload_run(rank, world, stage, out):
                "compile": {"offload_opt_states": off}}
         eng, _, _, _ = ds.initialize(model=m, config=cfg)
         if off:
-            eng.compile()
+            eng.compile(compile_kwargs={"offload_states_ratio": ratio})
         z = eng.optimizer
         g = torch.Generator().manual_seed(5 + rank)
         losses = []
@@ -174,9 +174,14 @@ def _state_offload_run(rank, world, stage, out):
                 eng.backward(loss)
                 eng.step()
                 losses.append(float(loss))
-            if off:  # between steps the moments and the fp32 master live on the host only
-                assert z.store.states["exp_avg"].numel() == 0 and z.store.master.numel() == 0
-                assert z.state_offload.n_offloads == step + 2  # offloaded at compile(), then after every step
+            if off:  # between steps the moments' and the fp32 master's tails live on the host only
+                so = z.state_offload
+                n = z.store.numel
+                a = so.a
+                assert a == (0 if ratio == 1.0 else min(n, (round((1 - ratio) * n) + 63) // 64 * 64)), (a, n)
+                assert z.store.states["exp_avg"].numel() == a and z.store.master.numel() == a
+                assert so.state_bytes() == 3 * 4 * (n - a) and not so.tail
+                assert so.n_offloads == step + 2  # offloaded at compile(), then after every step
         if off:
             assert z.state_offload.n_reloads == 3  # the states start off the device: every step reloads them
         res[off] = losses
@@ -187,11 +192,12 @@ def _state_offload_run(rank, world, stage, out):
     assert torch.equal(res["wFalse"], res["wTrue"])
 
 
-@pytest.mark.parametrize("stage,world", [(3, 1), (3, 2), (1, 2)])
-def test_offload_adam_states_keeps_trajectory(stage, world):
+@pytest.mark.parametrize("stage,world,ratio", [(3, 1, 1.0), (3, 2, 1.0), (1, 2, 1.0), (3, 1, 0.3), (3, 2, 0.55)])
+def test_offload_adam_states_keeps_trajectory(stage, world, ratio):
     """Optimizer states and the fp32 master offloaded after every step and reloaded in the next backward: the
-    training trajectory is bit-identical to keeping them resident (GAS=2: only the boundary step moves them)."""
-    run_distributed(_state_offload_run, world, stage, None)
+    training trajectory is bit-identical to keeping them resident (GAS=2: only the boundary step moves them). With
+    ratio < 1 exactly that fraction of every state (its tail) moves and the step runs per piece (byte-granular)."""
+    run_distributed(_state_offload_run, world, stage, None, ratio)
 
 
 def test_param_offload_plan():
@@ -255,3 +261,47 @@ def test_offload_parameters_keeps_trajectory(world):
     schedule, some kept on the device by the pass under a budget, combined with optimizer-state offload: the training
     trajectory and final weights are bit-identical to the resident run."""
     run_distributed(_param_offload_run, world, None)
+
+
+def _split_ckpt_run(rank, world, path):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+
+    def make(off):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(**TINY))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "bf16": {"enabled": True},
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}, "zero_optimization": {"stage": 3},
+               "compile": {"offload_opt_states": off}}
+        eng = ds.initialize(model=m, config=cfg)[0]
+        if off:
+            eng.compile(compile_kwargs={"offload_states_ratio": 0.5})
+        return eng
+
+    g = torch.Generator().manual_seed(11)
+    xs = [torch.randint(0, TINY["vocab_size"], (2, 12), generator=g) for _ in range(3)]
+
+    def step(eng, x):
+        loss = eng(x, labels=x)
+        eng.backward(loss)
+        eng.step()
+        return float(loss)
+
+    a = make(True)
+    for x in xs[:2]:
+        step(a, x)
+    assert a.optimizer.state_offload.split
+    a.save_checkpoint(path, tag="t")  # materializes the split states for the checkpoint
+    assert not a.optimizer.state_offload.split
+    la = step(a, xs[2])  # re-split by this step's offload
+    assert a.optimizer.state_offload.split
+    b = make(False)
+    b.load_checkpoint(path, tag="t")
+    lb = step(b, xs[2])
+    assert la == lb, (la, lb)
+
+
+def test_split_state_offload_checkpoint_roundtrip(tmp_path):
+    """Byte-granular state offload: a checkpoint taken while the states are split holds the whole flat states (head
+    and tail); an engine without offload resumes from it on the same trajectory."""
+    run_distributed(_split_ckpt_run, 1, str(tmp_path))
