@@ -78,7 +78,7 @@ def main():
     ap.add_argument("--offload-opt-states", action="store_true",
                     help="DeepCompile offload_adam_states: Adam moments + fp32 master on pinned host between steps")
     ap.add_argument("--offload-states-ratio", type=float, default=1.0,
-                    help="with --offload-opt-states: fraction of the optimizer-state bytes to offload (largest first)")
+                    help="with --offload-opt-states: fraction of every moved state (its tail) kept on the host between steps")
     ap.add_argument("--offload-params-compile", type=float, default=None, metavar="BUDGET_GIB",
                     help="DeepCompile offload_parameters on the GPU-optimizer engine; the pass keeps shards on the "
                          "device within BUDGET_GIB of HBM (0: every shard on the host)")
