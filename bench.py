@@ -229,15 +229,24 @@ def main():
             # position from the cache, and only when it MOVED -- a hung step still goes silent
             import threading
 
+            ac0.track_progress = True
+
+            def _gpu_block():  # the latest backward block whose first kernels the GPU has reached
+                done = None
+                for layer, ev in list(getattr(ac0, "bwd_events", [])):
+                    if ev.query():
+                        done = layer
+                return done
+
             def _heartbeat():
                 last = None
                 while True:
                     time.sleep(20)
-                    st = (ac0.bwd_layer_seen, ac0.cur_layer)
+                    st = (ac0.bwd_layer_seen, _gpu_block(), ac0.cur_layer)
                     if st != last:
                         last = st
-                        print(f"[bench] t={time.perf_counter() - t_run:.0f}s backward at block {st[0]}, forward "
-                              f"block {st[1]}", file=sys.stderr, flush=True)
+                        print(f"[bench] t={time.perf_counter() - t_run:.0f}s backward: host at block {st[0]}, GPU at "
+                              f"block {st[1]}; forward block {st[2]}", file=sys.stderr, flush=True)
 
             threading.Thread(target=_heartbeat, daemon=True).start()
 

@@ -378,7 +378,7 @@ class PlannedActivationCache(HostActivationCache):
         cap = self.spill_capacity() if spill_cap is None else spill_cap
         no_spill = range(self.n_layers - self.keep, self.n_layers)
         cost = self.spill_cost
-        new, self.est_cost_ms = plan_tensors(self.items, self._peak_all, self.budget, self.rec_ms, cap, cost,
+        new, self.est_cost_ms = plan_tensors(self.items, self._peak_all, self.plan_budget(), self.rec_ms, cap, cost,
                                              no_spill)
         if new != self.actions:
             self.replans += 1

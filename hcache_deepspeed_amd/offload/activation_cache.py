@@ -160,6 +160,10 @@ class HostActivationCache:
         # the step across those resets is what every calibration must read, not the raw counter
         self._step_max = 0
         self.last_step_peak = 0  # full peak of the previous step (set at the next forward)
+        # how far a step's peak rose above its forward/backward turn-around peak (backward transients: recompute,
+        # prefetched spills, gradients): the plans keep the turn-around peak under budget - bwd_extra, so the WHOLE
+        # step stays under the budget (max over the steps seen: conservative)
+        self.bwd_extra = 0
         self.bwd_headroom = None  # largest one-block backward transient seen (bytes), kept free by far prefetches
         self._bwd_layer, self._bwd_mark = None, None
         self.bwd_layer_seen = None
@@ -293,8 +297,14 @@ class HostActivationCache:
         if self.device.type == "cuda":
             self.last_step_peak = max(self._step_max, torch.cuda.max_memory_allocated(self.device))
             self.peak_seen = max(self.peak_seen, self.last_step_peak)
+            if self._turn_peak is not None:
+                self.bwd_extra = max(self.bwd_extra, self.last_step_peak - self._turn_peak)
         self._step_max = 0
         return self.last_step_peak
+
+    def plan_budget(self):
+        """The budget the forward-side plans aim the turn-around peak at (see ``bwd_extra``)."""
+        return None if self.budget is None else self.budget - self.bwd_extra
 
     @contextlib.contextmanager
     def forward_context(self):
@@ -306,7 +316,7 @@ class HostActivationCache:
                 # "everything spilled" peak is the measured one minus them (plan_offload adds kept layers back)
                 peak = self.last_step_peak - self._capped_this_step
                 self.plan = calibrated_plan(self.layer_bytes, peak + self._capped_this_step, self._capped_this_step,
-                                            self.budget)
+                                            self.plan_budget())
                 self._calibrating = False
                 self._cal_bytes = dict(self.layer_bytes)
                 if self.policy_recompute:  # the same over-budget layers, recomputed instead of spilled
@@ -323,7 +333,7 @@ class HostActivationCache:
                 self._hybrid_split()
             elif self._turn_peak is not None:
                 cur = self.recompute if self.policy_recompute else self.plan
-                new = refine_plan(cur, self._cal_bytes, self._turn_peak, self.budget)
+                new = refine_plan(cur, self._cal_bytes, self._turn_peak, self.plan_budget())
                 if new != cur:
                     self.plan_adjustments += 1
                     if self.policy_recompute:
@@ -359,6 +369,7 @@ class HostActivationCache:
         self.stashed_blocks = 0
         self._bwd_layer, self._bwd_mark = None, None
         self.bwd_layer_seen = None
+        self.bwd_events = []
         self._update_stash_keep()
         timed = self.hybrid and self._hybrid_state == 1 and self.device.type == "cuda"
         if timed:
@@ -481,8 +492,15 @@ class HostActivationCache:
 
     _DEBUG = os.environ.get("HDS_ACT_CACHE_DEBUG") == "1"
 
+    track_progress = False  # bench.py heartbeat: one event per backward block, to report the GPU's position
+
     def _prefetch_before(self, layer):
-        self.bwd_layer_seen = layer  # progress marker (bench.py heartbeat): the block backward has reached
+        if layer != self.bwd_layer_seen:
+            self.bwd_layer_seen = layer  # progress marker (host side: autograd runs ahead of the GPU)
+            if self.track_progress and self.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+                self.bwd_events = (getattr(self, "bwd_events", []) + [(layer, ev)])[-64:]
         if self._turn_peak is None and self.device.type == "cuda":
             self._turn_peak = torch.cuda.max_memory_allocated(self.device)  # first unpack of the step
         if self.budget is not None and self.device.type == "cuda" and layer != self._bwd_layer:
@@ -551,7 +569,9 @@ class HostActivationCache:
                 "stash_on_device_blocks": max(0, self.n_layers - self.stash_keep_from) if self.ckpt_offload else 0,
                 "bwd_headroom_gib": None if self.bwd_headroom is None else round(self.bwd_headroom / 2**30, 1),
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits,
-                "peak_gib_all_steps": round(self.peak_seen / 2**30, 1)}
+                "peak_gib_all_steps": round(self.peak_seen / 2**30, 1),
+                "last_step_peak_gib": round(self.last_step_peak / 2**30, 2),
+                "bwd_extra_gib": round(self.bwd_extra / 2**30, 2)}
 
 
 def refine_plan(plan, layer_bytes, turn_peak, budget, margin=1 << 30):
