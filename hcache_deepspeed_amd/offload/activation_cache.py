@@ -118,7 +118,11 @@ class HostActivationCache:
                 copy_window_bytes = int(max(4 << 30, head - (6 << 30)))
         self.copy_window = int(copy_window_bytes)
         self._d2h_q, self._h2d_q = [], []
+        # host waits on the copy window: the HOST blocks until the oldest queued spill drained. The GPU keeps
+        # running the kernels queued before it (autograd is ahead of the device), so this is host time, not a device
+        # stall, as long as the queue ahead of the copy is not empty (throttle_wait_s: total host seconds waited)
         self.throttle_waits = 0
+        self.throttle_wait_s = 0.0
         # pinned host bytes the cache may hold at once (the calibration step spills every eligible layer; at long
         # context that alone can exceed the host's memory): beyond it tensors stay on the GPU
         self.host_budget = host_budget_bytes
@@ -419,7 +423,9 @@ class HostActivationCache:
             q.pop(0)
         while q and sum(b for _, b in q) + nbytes > self.copy_window:
             ev, _ = q.pop(0)
+            t0 = time.perf_counter()
             ev.synchronize()
+            self.throttle_wait_s += time.perf_counter() - t0
             self.throttle_waits += 1
 
     def _pack(self, t):
@@ -569,6 +575,7 @@ class HostActivationCache:
                 "stash_on_device_blocks": max(0, self.n_layers - self.stash_keep_from) if self.ckpt_offload else 0,
                 "bwd_headroom_gib": None if self.bwd_headroom is None else round(self.bwd_headroom / 2**30, 1),
                 "copy_window_gib": round(self.copy_window / 2**30, 1), "throttle_waits": self.throttle_waits,
+                "throttle_wait_s": round(self.throttle_wait_s, 2),
                 "peak_gib_all_steps": round(self.peak_seen / 2**30, 1),
                 "last_step_peak_gib": round(self.last_step_peak / 2**30, 2),
                 "bwd_extra_gib": round(self.bwd_extra / 2**30, 2)}
