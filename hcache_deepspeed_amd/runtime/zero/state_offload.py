@@ -84,7 +84,7 @@ class OptimizerStateOffload:
 
     def view(self, k, lo, hi):
         """[lo, hi) of state ``k`` (``k`` = "master" or a moment key) inside ONE piece (never across a cut)."""
-        if not self.split:
+        if not self.split or k not in self.host:  # not split, or a state this executor does not move
             return self._get(k)[lo:hi]
         a = self.a
         if hi <= a:
