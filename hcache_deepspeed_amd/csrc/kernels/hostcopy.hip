@@ -60,18 +60,21 @@ HDS_EXPORT int hds_copy_d2h(void* dst, const void* src, int64_t nbytes, int n_wg
 // ring with one D2H each on the copy stream instead of 32 per-layer D2H copies per token.
 namespace {
 
-// rows x row_bytes from src (row stride src_stride bytes) -> dst_base + slot * slot_stride (contiguous rows)
+// rows x row_bytes from src (row stride src_stride bytes) -> dst_base + slot * slot_stride (contiguous rows), in
+// VT-sized pieces: 16 B when every row and stride is a multiple of 16, else 4 B (the packed fp8 / int8 latents are
+// H + 4 and H + H/32 bytes per row)
+template <typename VT>
 __global__ __launch_bounds__(256) void latent_slot_store_kernel(const char* __restrict__ src, int64_t src_stride,
                                                                 char* __restrict__ dst_base,
                                                                 const int* __restrict__ slot, int64_t slot_stride,
                                                                 int rows, int64_t row_bytes) {
   char* dst = dst_base + (int64_t)(*slot) * slot_stride;
-  const int64_t nvec = row_bytes / 16;  // row_bytes % 16 == 0 (checked by the launcher)
+  const int64_t nvec = row_bytes / (int64_t)sizeof(VT);
   const int64_t total = (int64_t)rows * nvec;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / nvec, v = i - r * nvec;
-    *reinterpret_cast<u32x4*>(dst + r * row_bytes + v * 16) =
-        *reinterpret_cast<const u32x4*>(src + r * src_stride + v * 16);
+    *reinterpret_cast<VT*>(dst + r * row_bytes + v * (int64_t)sizeof(VT)) =
+        *reinterpret_cast<const VT*>(src + r * src_stride + v * (int64_t)sizeof(VT));
   }
 }
 
@@ -87,15 +90,21 @@ __global__ void slot_advance_kernel(int* slot, int mod) {
 HDS_EXPORT int hds_latent_slot_store(const void* src, int64_t src_stride, void* dst_base, const int* slot,
                                      int64_t slot_stride, int rows, int64_t row_bytes, hipStream_t st) {
   if (rows <= 0 || row_bytes <= 0) return hipSuccess;
-  if (row_bytes % 16 || src_stride % 16 || slot_stride % 16 || (reinterpret_cast<uintptr_t>(src) & 15) ||
-      (reinterpret_cast<uintptr_t>(dst_base) & 15))
-    return hipErrorInvalidValue;
-  const int64_t total = (int64_t)rows * (row_bytes / 16);
+  const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst_base) |
+                       (uintptr_t)row_bytes | (uintptr_t)src_stride | (uintptr_t)slot_stride;
+  if (al & 3) return hipErrorInvalidValue;
+  const bool wide = (al & 15) == 0;
+  const int64_t total = (int64_t)rows * (row_bytes / (wide ? 16 : 4));
   int64_t grid = (total + 255) / 256;
   if (grid > 1024) grid = 1024;
-  hipLaunchKernelGGL(latent_slot_store_kernel, dim3((unsigned)grid), dim3(256), 0, st,
-                     static_cast<const char*>(src), src_stride, static_cast<char*>(dst_base), slot, slot_stride, rows,
-                     row_bytes);
+  if (wide)
+    hipLaunchKernelGGL(latent_slot_store_kernel<u32x4>, dim3((unsigned)grid), dim3(256), 0, st,
+                       static_cast<const char*>(src), src_stride, static_cast<char*>(dst_base), slot, slot_stride, rows,
+                       row_bytes);
+  else
+    hipLaunchKernelGGL(latent_slot_store_kernel<uint32_t>, dim3((unsigned)grid), dim3(256), 0, st,
+                       static_cast<const char*>(src), src_stride, static_cast<char*>(dst_base), slot, slot_stride, rows,
+                       row_bytes);
   return hipGetLastError();
 }
 

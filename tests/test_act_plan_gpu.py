@@ -121,12 +121,17 @@ def test_budget_is_a_cap(policy):
     eng = engine({"enabled": True, "policy": policy, "min_layers_resident": 1, "gpu_budget_gib": budget / 2**30})
     cache = eng._activation_cache
     peaks = []
-    for _ in range(6):
+    for i in range(6):
         loss = eng(x, labels=x)
         eng.backward(loss)
         eng.step()
         torch.cuda.synchronize()
         peaks.append(cache.step_peak())
+        tp = cache._turn_peak
+        print(f"[budget-cap {policy}] step {i}: peak {peaks[-1] / 2**20:.1f} MiB, turn-around "
+              f"{(tp or 0) / 2**20:.1f}, budget {budget / 2**20:.1f}, base {base / 2**20:.1f}, full {full / 2**20:.1f}, "
+              f"bwd_extra {cache.bwd_extra / 2**20:.1f}, plan {getattr(cache, 'plan', None)}, "
+              f"recompute {sorted(getattr(cache, 'recompute', []))}", flush=True)
     st = cache.stats()
     # steps 0-1 calibrate / time the plan; from then on the cap holds (1 MiB of slack: allocator rounding)
     over = [p - budget for p in peaks[2:] if p > budget + (1 << 20)]
