@@ -2,7 +2,7 @@
 # --act-cache-host-gib (round 4 needed 225 GiB pinned)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r5g
+O=gpurun_out/${R5G_OUT:-r5g}; O=gpurun_out/$(basename $O)
 mkdir -p $O
 run() {
   "$@"; rc=$?
