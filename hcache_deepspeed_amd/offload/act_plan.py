@@ -300,6 +300,9 @@ class PlannedActivationCache(HostActivationCache):
         if cuda and self._turn_peak is None:
             self._turn_peak = torch.cuda.max_memory_allocated(self.device)
 
+    def _was_calibrating(self):
+        return self._stage == 1
+
     def _end_of_step(self):
         self.step_spill_bytes, self.step_recomputed = self._spill_acc, self._rec_acc
         self._spill_acc = self._rec_acc = 0

@@ -111,11 +111,15 @@ class HostActivationCache:
         # window keeps it inside the HBM the budget leaves free (the host waits only when it would not fit). The
         # backward needs no window: prefetch buffers are allocated and consumed on the compute stream and the
         # copy stream waits for them (see _prefetch), so their blocks recycle in stream order.
+        # Under an HBM budget the bytes in flight count AGAINST the budget: a spilled tensor's HBM returns only once its
+        # D2H has drained. Round 4 sized the window from the HBM outside the budget (52 GiB at a 230 GiB budget on
+        # 288 GiB), which let in-flight spills carry the step to 250 GiB. Now it is a small slice of the budget
+        # (budget / 32, 64 MiB .. 4 GiB: at 230 GiB, 4 GiB = ~75 ms of PCIe backlog), and the plans, closed-looped on the
+        # measured peaks, keep those bytes inside the budget.
         if copy_window_bytes is None:
             copy_window_bytes = 16 << 30
             if gpu_budget_bytes is not None and device.type == "cuda":
-                head = torch.cuda.get_device_properties(device).total_memory - gpu_budget_bytes
-                copy_window_bytes = int(max(4 << 30, head - (6 << 30)))
+                copy_window_bytes = int(min(4 << 30, max(64 << 20, gpu_budget_bytes // 32)))
         self.copy_window = int(copy_window_bytes)
         self._d2h_q, self._h2d_q = [], []
         # host waits on the copy window: the HOST blocks until the oldest queued spill drained. The GPU keeps
@@ -301,10 +305,15 @@ class HostActivationCache:
         if self.device.type == "cuda":
             self.last_step_peak = max(self._step_max, torch.cuda.max_memory_allocated(self.device))
             self.peak_seen = max(self.peak_seen, self.last_step_peak)
-            if self._turn_peak is not None:
+            if self._turn_peak is not None and not self._was_calibrating():
+                # (not from a calibration step: everything was spilled, so its backward prefetched everything back)
                 self.bwd_extra = max(self.bwd_extra, self.last_step_peak - self._turn_peak)
         self._step_max = 0
         return self.last_step_peak
+
+    def _was_calibrating(self):
+        """The step that just ended spilled every eligible tensor to measure (not a planned step)."""
+        return bool(self._calibrating)
 
     def plan_budget(self):
         """The budget the forward-side plans aim the turn-around peak at (see ``bwd_extra``)."""
