@@ -172,6 +172,7 @@ class HostActivationCache:
         # prefetched spills, gradients): the plans keep the turn-around peak under budget - bwd_extra, so the WHOLE
         # step stays under the budget (max over the steps seen: conservative)
         self.bwd_extra = 0
+        self._bwd_extra_cal, self._bwd_extra_planned = 0, None
         self.bwd_headroom = None  # largest one-block backward transient seen (bytes), kept free by far prefetches
         self._bwd_layer, self._bwd_mark = None, None
         self.bwd_layer_seen = None
@@ -305,9 +306,16 @@ class HostActivationCache:
         if self.device.type == "cuda":
             self.last_step_peak = max(self._step_max, torch.cuda.max_memory_allocated(self.device))
             self.peak_seen = max(self.peak_seen, self.last_step_peak)
-            if self._turn_peak is not None and not self._was_calibrating():
-                # (not from a calibration step: everything was spilled, so its backward prefetched everything back)
-                self.bwd_extra = max(self.bwd_extra, self.last_step_peak - self._turn_peak)
+            if self._turn_peak is not None:
+                # the calibration step (everything spilled, prefetched back in backward) gives a conservative first
+                # value; from the first planned step on, the max over the planned steps replaces it
+                extra = max(0, self.last_step_peak - self._turn_peak)
+                if self._was_calibrating():
+                    self._bwd_extra_cal = extra
+                else:
+                    self._bwd_extra_planned = max(self._bwd_extra_planned or 0, extra)
+                self.bwd_extra = (self._bwd_extra_planned if self._bwd_extra_planned is not None else
+                                  self._bwd_extra_cal)
         self._step_max = 0
         return self.last_step_peak
 
