@@ -268,6 +268,8 @@ def main():
     retries0 = torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) if on_gpu else 0
     zopt = engine.optimizer
     timed_events = getattr(zopt, "comm_stats", None)  # None: the timed steps record no comm accounting events
+    ac_t = getattr(engine, "_activation_cache", None)
+    n_peaks0 = len(ac_t.step_peak_history) if ac_t is not None else 0
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = train_step(args.warmup + i)
@@ -286,6 +288,12 @@ def main():
              6 * cfg_model.active_params() + 12 * cfg_model.num_hidden_layers * S * cfg_model.hidden_size) * tokens
     mfu = flops / dt / (2.5e15 * world)
     mem = torch.cuda.max_memory_allocated(dev) / 2**30 if on_gpu else 0.0
+    timed_peak = None
+    if ac_t is not None and on_gpu:
+        # the cache resets the allocator's peak counter per forward (and per backward block): the timed steps' peaks
+        # are the history entries of their forwards after the first (which closes the last warm-up step) plus the
+        # running max of the last timed step
+        timed_peak = max(ac_t.step_peak_history[n_peaks0 + 1:] + [ac_t.step_peak()]) / 2**30
     # caching-allocator retries in the timed steps: each one frees cached blocks after a device-wide synchronize
     retries = (torch.cuda.memory_stats(dev).get("num_alloc_retries", 0) - retries0) if on_gpu else 0
     comm = None
@@ -384,6 +392,10 @@ def main():
             out["extra"]["act_cache"] = ac.stats()
             if ac.peak_seen:  # the cache resets the peak counter every forward: report the max over all steps
                 out["extra"]["peak_mem_gib"] = round(max(mem, ac.peak_seen / 2**30), 1)
+            if timed_peak is not None:
+                out["extra"]["peak_gib_timed_steps"] = round(timed_peak, 1)
+                if ac.budget is not None:
+                    out["extra"]["act_cache_budget_gib"] = round(ac.budget / 2**30, 1)
         zo = engine.optimizer
         sw = getattr(zo, "opt_swapper", None)
         if sw is not None:  # ZeRO-Infinity NVMe tier: how much of the optimizer's swap I/O hid behind CPU Adam

@@ -168,6 +168,7 @@ class HostActivationCache:
         # the step across those resets is what every calibration must read, not the raw counter
         self._step_max = 0
         self.last_step_peak = 0  # full peak of the previous step (set at the next forward)
+        self.step_peak_history = []  # every finished step's full peak, in order (bench.py: the timed steps' max)
         # how far a step's peak rose above its forward/backward turn-around peak (backward transients: recompute,
         # prefetched spills, gradients): the plans keep the turn-around peak under budget - bwd_extra, so the WHOLE
         # step stays under the budget (max over the steps seen: conservative)
@@ -306,6 +307,7 @@ class HostActivationCache:
         if self.device.type == "cuda":
             self.last_step_peak = max(self._step_max, torch.cuda.max_memory_allocated(self.device))
             self.peak_seen = max(self.peak_seen, self.last_step_peak)
+            self.step_peak_history.append(self.last_step_peak)
             if self._turn_peak is not None:
                 # the calibration step (everything spilled, prefetched back in backward) gives a conservative first
                 # value; from the first planned step on, the max over the planned steps replaces it
