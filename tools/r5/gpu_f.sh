@@ -16,4 +16,6 @@ run timeout -k 10 300 $B --offload cpu > $O/mb10_zero_offload.log 2>&1
 for r in 0.2 0.25; do
   run timeout -k 10 300 $B --offload-opt-states --offload-states-ratio $r > $O/mb10_offstates_$r.log 2>&1
 done
+export HDS_BENCH_PROGRESS=1
+run timeout -k 10 420 python -u bench.py --seq 65536 --micro-batch 1 --steps 4 --warmup 6 --host-act-cache --act-cache-policy plan --act-cache-spill-overlap 0.8 > $O/plan_65536_mb1.log 2>&1
 exit 0
