@@ -28,111 +28,15 @@
 #include <utility>
 
 #include "attn_common.h"
+#include "flash_attn_shared.h"
 
 using namespace hds;
 using namespace hds::attn;
 
+// variant 9 lives in its own translation unit (flash_attn_w64.hip: built with the VGPR-form MFMA selection)
+int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, hipStream_t st);
+
 namespace {
-
-constexpr int BN = 64;   // keys per LDS tile (fwd, dq) / query rows per tile (dkdv)
-// query rows per workgroup (fwd, dq) = 32 * NW ; keys per workgroup (dkdv) = 32 * NW
-constexpr float kLog2e = 1.4426950408889634f;
-
-struct AttnParams {
-  const bf16* q;
-  const bf16* k;
-  const bf16* v;
-  bf16* o;
-  float* lse;  // [Hq][total_tokens], natural-log units of (scale * q.k)
-  const bf16* dout;
-  bf16* dq;
-  bf16* dk;
-  bf16* dv;
-  float* delta;  // [Hq][total_tokens]
-  float* lse2;   // [Hq][total_tokens] lse * log2(e), written by the delta pre-kernel (null: not wanted)
-  int64_t sq, sk, sv, so, sdo, sdq, sdk, sdv;  // token strides (elements)
-  const int* cu_seqlens;                       // [B+1] or null
-  const int* seq_lens;                         // [B] valid lengths of a right-padded batch (null: all seq_len)
-  int seq_len;                                 // when cu_seqlens is null
-  int total_tokens;
-  int batch, hq, hkv;
-  float scale;
-  int causal;
-  int window;  // >0: sliding window (keys in (q - window, q])
-  // Evoformer (EVO kernels only): additive biases and their gradients, batch = B * evo_n sequences of seq_len
-  const void* b1;  // [B*N][L]        (bf16 or fp32, bias_f32)
-  const void* b2;  // [B][H][L][L]
-  int bias_f32;
-  float* db1;      // [B*N][L]  fp32, accumulated
-  float* db2;      // [B][H][L][L] fp32, accumulated
-  int evo_n;
-};
-
-__device__ __forceinline__ float ld_bias(const AttnParams& p, const void* base, int64_t i) {
-  return p.bias_f32 ? reinterpret_cast<const float*>(base)[i] : (float)reinterpret_cast<const bf16*>(base)[i];
-}
-
-// Evoformer pair / mask bias of (sequence bn, head h, query q, key) (indices clamped; masked() zeroes padding)
-__device__ __forceinline__ float evo_bias(const AttnParams& p, int bn, int h, int q, int key) {
-  const int L = p.seq_len;
-  q = q < L ? q : L - 1;
-  key = key < L ? key : L - 1;
-  float x = 0.f;
-  if (p.b1) x += ld_bias(p, p.b1, (int64_t)bn * L + key);
-  if (p.b2) x += ld_bias(p, p.b2, ((int64_t)((bn / p.evo_n) * p.hq + h) * L + q) * L + key);
-  return x;
-}
-
-__device__ __forceinline__ void seq_bounds(const AttnParams& p, int b, int& start, int& len) {
-  if (p.cu_seqlens) {
-    start = p.cu_seqlens[b];
-    len = p.cu_seqlens[b + 1] - start;
-  } else {
-    start = b * p.seq_len;
-    len = p.seq_lens ? p.seq_lens[b] : p.seq_len;
-  }
-}
-
-// Launch grids are (blocks-per-sequence, heads, batch); reinterpret the linear workgroup id so the
-// block index within a sequence varies SLOWEST: the dispatcher then starts every (head, batch)'s
-// heaviest causal block before any lighter one (longest-processing-time-first across 256 CUs).
-__device__ __forceinline__ void lpt_ids(int& blk, int& head, int& b) {
-  const int heads = gridDim.y, nb = gridDim.z;
-  const int lid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  blk = lid / (heads * nb);
-  const int rem = lid - blk * heads * nb;
-  head = rem % heads;
-  b = rem / heads;
-}
-
-// The per-element mask as an interval test (two compares, no branches): the keys a query may see, or the queries
-// that may see a key, form [lo, hi] (empty when lo > hi). Same predicate as masked() below.
-__device__ __forceinline__ void key_span(const AttnParams& p, int qi, int len, int& lo, int& hi) {
-  lo = p.window > 0 ? max(0, qi - p.window + 1) : 0;
-  hi = p.causal ? min(qi, len - 1) : len - 1;
-  if (qi >= len) lo = 1, hi = 0;
-}
-__device__ __forceinline__ void query_span(const AttnParams& p, int kj, int len, int& lo, int& hi) {
-  lo = p.causal ? kj : 0;
-  hi = p.window > 0 ? min(len - 1, kj + p.window - 1) : len - 1;
-  if (kj >= len) lo = 1, hi = 0;
-}
-__device__ __forceinline__ bool outside(int i, int lo, int hi) { return i < lo || i > hi; }
-
-__device__ __forceinline__ bool masked(const AttnParams& p, int qi, int kj, int len) {
-  if (kj >= len || qi >= len) return true;
-  if (p.causal && kj > qi) return true;
-  if (p.window > 0 && kj <= qi - p.window) return true;
-  return false;
-}
-
-// =====================================================================================
-// forward
-// =====================================================================================
-// VAR bit 0: static s_setprio(1) for the second-dispatched half of the waves (guide T5 static form);
-// VAR bit 1: deferred running-max update -- the max (and the O / l rescale) only moves when some row of the
-//            wave grew by more than kDeferThr (log2 units), so P stays <= 2^kDeferThr (guide T13).
-constexpr float kDeferThr = 8.f;
 
 template <int D, int NW, int VAR>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
@@ -501,27 +405,6 @@ __global__ __launch_bounds__(512) void attn_fwd_stg_kernel(AttnParams p) {
 // 32-bit offset computed once (clamped per-row addressing only on the last, partial tile). Every wave runs every tile
 // of the workgroup's causal range (a fully masked tile contributes exp(-inf) = 0), so the loop body has no
 // wave-level branches that would split the interleaved blocks.
-template <int IMM>
-__device__ __forceinline__ bf16x8 lds_b128(uint32_t a) {
-  bf16x8 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(IMM) : "memory");
-  return r;
-}
-template <int IMM>
-__device__ __forceinline__ bf16x8 lds_tr8(uint32_t a0, uint32_t a1) {
-  bf16x4 lo, hi;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(a0), "n"(IMM) : "memory");
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a1), "n"(IMM) : "memory");
-  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-template <int... I, typename F>
-__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, I...>, F&& f) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(std::make_integer_sequence<int, N>{}, f);
-}
 
 // SKIPW (variant 7): a wave whose queries all lie below a causal key tile skips that tile's math -- and every later
 // one, which is masked too -- keeping only the workgroup's DMA staging and barrier (waves 0-5 of the last 1-3 tiles).
@@ -784,317 +667,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     if (h == 0 && p.lse) {
       const float lse = (l > 0.f) ? (m + __log2f(l)) / kLog2e : -INFINITY;
       p.lse[(int64_t)hq * p.total_tokens + start + myq] = lse;
-    }
-  }
-}
-
-// =====================================================================================
-// forward variant 9: one wave per SIMD, 64 query rows per wave, hand-owned accumulator file
-// =====================================================================================
-// The guide's 1.25 PF/s structure (cdna_hip_programming.md §B "4-wave, one-wave-per-SIMD"): 4 waves x 64 query rows
-// = 256 rows per workgroup, so every K/V tile read from LDS feeds TWICE the MFMAs of the 8-wave kernel and each SIMD
-// runs one instruction stream (no partner wave contending for the matrix pipe or the VALU issue port). Per tile and
-// wave: 32 S MFMAs (2 key halves x 2 query halves x 8 k-steps) + 32 P.V MFMAs = 64 v_mfma_f32_32x32x16_bf16.
-// Register plan (512 per lane): O^T (4 column blocks x 2 query halves x 16) = 128 and the Q fragments (2 x 8 x 4) = 64
-// live in the ACCUMULATOR file through inline-asm MFMAs ("+a" / "a" operands) -- round 4's builtin version let hipcc
-// put the S accumulators there too, so every score crossed v_accvgpr_read twice; here S, P and the K/V fragments are
-// the arch VGPRs. hipcc neither models nor pads an asm MFMA's hazards (guide §5.7 item 2), so: the last MFMA of every
-// S chain ends with the 12 wait states an 8-pass XDL result needs before a VALU reads it, the first P.V MFMA after the
-// bf16 P is written opens with s_nop 1, and the O read-back (rescale, epilogue) is preceded by a full drain.
-// The software pipeline is the one of attn_fwd_sp_kernel: S_{kt+1} beside exp(S_kt keys 0..31), P_kt.V_kt beside
-// exp(S_kt keys 32..63); deferred running max (T13); LDS-DMA K/V ring with K one tile further ahead than V.
-__device__ __forceinline__ void mfma_sq(f32x16& s, const bf16x8& k, const bf16x8& q) {  // S(v) += K(v) . Q^T(a)
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(s) : "v"(k), "a"(q));
-}
-__device__ __forceinline__ void mfma_sq0(f32x16& s, const bf16x8& k, const bf16x8& q) {  // S(v) = K . Q^T
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(s) : "v"(k), "a"(q));
-}
-__device__ __forceinline__ void mfma_sq_end(f32x16& s, const bf16x8& k, const bf16x8& q) {  // last of a chain + pad
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 3" : "+v"(s) : "v"(k), "a"(q));
-}
-__device__ __forceinline__ void mfma_pv(f32x16& o, const bf16x8& v, const bf16x8& pb) {  // O^T(a) += V^T . P^T
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(pb));
-}
-__device__ __forceinline__ void mfma_pv_fresh(f32x16& o, const bf16x8& v, const bf16x8& pb) {  // P just written
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(pb));
-}
-__device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
-
-template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_fwd_w64_kernel(AttnParams p) {
-  constexpr int NW = 4, BM = 64 * NW, PW = 16 / NW;
-  constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
-  static_assert(D == 128, "one-wave-per-SIMD forward: head_dim 128");
-  __shared__ __attribute__((aligned(1024))) char smem[4 * TL];  // K[2], V[2]
-  int blk, hq, b;
-  lpt_ids(blk, hq, b);
-  int start, len;
-  seq_bounds(p, b, start, len);
-  const int nqb = (len + BM - 1) / BM;
-  const int qb = p.causal ? (gridDim.x - 1 - blk) : blk;
-  if (qb >= nqb || len == 0) return;
-  const int hk = hq / (p.hq / p.hkv);
-  const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int q0 = qb * BM;
-  const int wq_lo = q0 + 64 * w, wq_hi = wq_lo + 63;
-  const float c = p.scale * kLog2e;
-  int myq[2], klo[2], khi[2];
-#pragma unroll
-  for (int qh = 0; qh < 2; ++qh) {
-    myq[qh] = wq_lo + 32 * qh + (lane & 31);
-    key_span(p, myq[qh], len, klo[qh], khi[qh]);
-  }
-  bf16x8 qf[2][KS];  // accumulator file (asm "a" operands)
-#pragma unroll
-  for (int qh = 0; qh < 2; ++qh) {
-    const int qr = myq[qh] < len ? myq[qh] : len - 1;
-    const bf16* qp = p.q + (int64_t)(start + qr) * p.sq + (int64_t)hq * D + 8 * h;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qf[qh][ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-  }
-  int kt_end = (len + BN - 1) / BN;
-  if (p.causal) {
-    const int last = q0 + BM - 1 < len - 1 ? q0 + BM - 1 : len - 1;
-    kt_end = last / BN + 1;
-  }
-  int kt_begin = 0;
-  if (p.window > 0) {
-    const int first = q0 - p.window + 1;
-    kt_begin = first > 0 ? first / BN : 0;
-  }
-  auto rowp = [&](const bf16* base, int64_t stride, int kt) {
-    return [=](int row) {
-      int r = kt * BN + row;
-      r = r < len ? r : len - 1;
-      return base + (int64_t)(start + r) * stride + (int64_t)hk * D;
-    };
-  };
-  int32_t dk[PW], dv[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const int row = 4 * (w * PW + i) + (lane >> 4);
-    const int ch = (lane & 15) ^ swz(row);
-    dk[i] = (int32_t)(((int64_t)row * p.sk + 8 * ch) * 2);
-    dv[i] = (int32_t)(((int64_t)row * p.sv + 8 * ch) * 2);
-  }
-  auto stage = [&](char* dst, const bf16* base, int64_t stride, const int32_t* off, int kt) {
-    if (kt * BN + BN <= len) {
-      const char* tb = (const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D);
-#pragma unroll
-      for (int i = 0; i < PW; ++i)
-        __builtin_amdgcn_global_load_lds((gbl_void*)(tb + off[i]), (lds_void*)(dst + (w * PW + i) * 1024), 16, 0, 0);
-    } else {
-      stage_tile_d<NW, D>(dst, rowp(base, stride, kt));
-    }
-  };
-  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-  uint32_t ak[KS], av0[DT], av1[DT];
-  {
-    const uint32_t P0 = rows_lane_off(0);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) ak[ks] = sbase + (P0 ^ (32u * ks));
-    uint32_t y0, y1;
-    tr_lane_offs(y0, y1);
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      av0[dt] = sbase + (y0 ^ (64u * dt));
-      av1[dt] = sbase + (y1 ^ (64u * dt));
-    }
-  }
-  f32x16 o[DT][2];  // accumulator file (asm "+a")
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o[dt][0] = o[dt][1] = f32x16{};
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-
-  // S of one 64-key tile for both query halves: sc[t][qh], t = key half. 8 ks x (2 t) K fragments streamed in pairs.
-  auto s_tile = [&](auto KOFF, f32x16 (&sc)[2][2]) {
-    constexpr int KO = decltype(KOFF)::value;
-    static_for<2>([&](auto TC) {
-      constexpr int t = decltype(TC)::value;
-      bf16x8 kr[2][4];
-      static_for<4>([&](auto IC) {
-        constexpr int i = decltype(IC)::value;
-        kr[0][i] = lds_b128<KO + 8192 * t>(ak[i]);
-      });
-      static_for<2>([&](auto JC) {
-        constexpr int j = decltype(JC)::value;
-        if constexpr (j == 0) {
-          static_for<4>([&](auto IC) {
-            constexpr int i = decltype(IC)::value;
-            kr[1][i] = lds_b128<KO + 8192 * t>(ak[4 + i]);
-          });
-          lds_wait_tie<4>(kr[0][0], kr[0][1], kr[0][2], kr[0][3]);
-        } else {
-          lds_wait_tie<0>(kr[1][0], kr[1][1], kr[1][2], kr[1][3]);
-        }
-#pragma unroll
-        for (int qh = 0; qh < 2; ++qh) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int ks = 4 * j + i;
-            if (ks == 0)
-              mfma_sq0(sc[t][qh], kr[j][i], qf[qh][ks]);
-            else if (ks == KS - 1)
-              mfma_sq_end(sc[t][qh], kr[j][i], qf[qh][ks]);
-            else
-              mfma_sq(sc[t][qh], kr[j][i], qf[qh][ks]);
-          }
-        }
-      });
-    });
-  };
-
-  stage(smem + 0, p.k, p.sk, dk, kt_begin);
-  stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
-  if (kt_begin + 1 < kt_end) {
-    stage(smem + TL, p.k, p.sk, dk, kt_begin + 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's 4 K_0 pieces landed (V_0, K_1: 8 in flight)
-  } else {
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  }
-  __syncthreads();
-  f32x16 sc[2][2];
-  s_tile(std::integral_constant<int, 0>{}, sc);
-
-  auto tile = [&](auto BUFC, int kt) {
-    constexpr int buf = decltype(BUFC)::value;
-    constexpr int KN = (buf ^ 1) * TL;     // K_{kt+1}
-    constexpr int VT = 2 * TL + buf * TL;  // V_kt
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < kt_end) stage(smem + 2 * TL + (buf ^ 1) * TL, p.v, p.sv, dv, kt + 1);
-    if (kt + 2 < kt_end) stage(smem + buf * TL, p.k, p.sk, dk, kt + 2);
-
-    const int k0 = kt * BN;
-    const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
-                           (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
-    if (need_mask) {
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (outside(k0 + 32 * t + acc_row(r, h), klo[qh], khi[qh])) sc[t][qh][r] = -INFINITY;
-    }
-    float alpha[2], muse[2];
-    bool move_any = false;
-#pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      float tm0 = -INFINITY, tm1 = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        tm0 = max3_raw(tm0, sc[0][qh][r], sc[0][qh][r + 1]);
-        tm1 = max3_raw(tm1, sc[1][qh][r], sc[1][qh][r + 1]);
-      }
-      float tmax = fmaxf(tm0, tm1);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
-      const bool move = !__all(tmax <= m[qh] + kDeferThr);
-      const float mnew = move ? fmaxf(m[qh], tmax) : m[qh];
-      alpha[qh] = move ? ((m[qh] == -INFINITY) ? 0.f : fast_exp2(m[qh] - mnew)) : 1.f;
-      m[qh] = mnew;
-      muse[qh] = (mnew == -INFINITY) ? 0.f : mnew;
-      move_any |= move;
-    }
-    if (move_any) {  // rare: O lives in the accumulator file, drain the last P.V MFMAs before reading it back
-      xdl_drain();
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        o[dt][0] *= alpha[0];
-        o[dt][1] *= alpha[1];
-      }
-    }
-
-    // ---- block A: S_{kt+1} beside exp(S_kt keys 0..31) for both query halves ----
-    f32x16 sn[2][2];
-    float rs[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-    auto exp_keys = [&](int t, int qh, int r0, int r1) {
-#pragma unroll
-      for (int r = r0; r < r1; ++r) {
-        const float e = fast_exp2(__builtin_fmaf(sc[t][qh][r], c, -muse[qh]));
-        sc[t][qh][r] = e;
-        rs[qh][r & 1] += e;
-      }
-    };
-    if (kt + 1 < kt_end) {
-      s_tile(std::integral_constant<int, KN>{}, sn);
-    }
-    exp_keys(0, 0, 0, 16);
-    exp_keys(0, 1, 0, 16);
-    bf16x8 pb[2][4];
-#pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      pb[qh][0] = acc_to_b<0>(sc[0][qh]);
-      pb[qh][1] = acc_to_b<1>(sc[0][qh]);
-    }
-    // ---- block B: O += V_kt^T.P_kt (k-steps 0,1 = keys 0..31 first) beside exp(S_kt keys 32..63) ----
-    bf16x8 vf[2][DT];
-    static_for<DT>([&](auto DC) {
-      constexpr int dt = decltype(DC)::value;
-      vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
-    });
-    static_for<4>([&](auto SC) {
-      constexpr int st = decltype(SC)::value;
-      if constexpr (st + 1 < 4) {
-        static_for<DT>([&](auto DC) {
-          constexpr int dt = decltype(DC)::value;
-          vf[(st + 1) & 1][dt] = lds_tr8<VT + 4096 * (st + 1)>(av0[dt], av1[dt]);
-        });
-        lds_wait_tie<8>(vf[st & 1][0], vf[st & 1][1], vf[st & 1][2], vf[st & 1][3]);
-      } else {
-        lds_wait_tie<0>(vf[st & 1][0], vf[st & 1][1], vf[st & 1][2], vf[st & 1][3]);
-      }
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          if (dt == 0 && (st == 0 || st == 2))
-            mfma_pv_fresh(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
-          else
-            mfma_pv(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
-        }
-      if constexpr (st == 0) {
-        exp_keys(1, 0, 0, 16);
-      } else if constexpr (st == 1) {
-        exp_keys(1, 1, 0, 16);
-#pragma unroll
-        for (int qh = 0; qh < 2; ++qh) {
-          pb[qh][2] = acc_to_b<0>(sc[1][qh]);
-          pb[qh][3] = acc_to_b<1>(sc[1][qh]);
-        }
-      }
-    });
-#pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      float r = rs[qh][0] + rs[qh][1];
-      r += __shfl_xor(r, 32, 64);
-      l[qh] = l[qh] * alpha[qh] + r;
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh) sc[t][qh] = sn[t][qh];
-  };
-  int kt = kt_begin;
-  for (; kt + 1 < kt_end; kt += 2) {
-    tile(std::integral_constant<int, 0>{}, kt);
-    tile(std::integral_constant<int, 1>{}, kt + 1);
-  }
-  if (kt < kt_end) tile(std::integral_constant<int, 0>{}, kt);
-
-  xdl_drain();
-#pragma unroll
-  for (int qh = 0; qh < 2; ++qh) {
-    if (myq[qh] < len) {
-      const float inv = l[qh] > 0.f ? 1.f / l[qh] : 0.f;
-      bf16* op = p.o + (int64_t)(start + myq[qh]) * p.so + (int64_t)hq * D;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) store_row_block<D>(op, o[dt][qh], dt, h, inv);
-      if (h == 0 && p.lse) {
-        const float lse = (l[qh] > 0.f) ? (m[qh] + __log2f(l[qh])) / kLog2e : -INFINITY;
-        p.lse[(int64_t)hq * p.total_tokens + start + myq[qh]] = lse;
-      }
     }
   }
 }
@@ -1890,10 +1462,7 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
             hipLaunchKernelGGL((attn_fwd_sp_kernel<D, true, false, 4>), dim3((max_len + 127) / 128, hq, batch),
                                dim3(256), 0, st, p);
             break;
-          case 9:
-            hipLaunchKernelGGL((attn_fwd_w64_kernel<D>), dim3((max_len + 255) / 256, hq, batch), dim3(256), 0, st,
-                               p);
-            break;
+          case 9: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, st);
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;

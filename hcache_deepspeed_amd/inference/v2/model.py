@@ -670,8 +670,18 @@ class _DecodeGraph:
         if model._graph_pool is None:
             model._graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=model._graph_pool):
-            self.out, _ = model.forward(self.batch, capture_latents=cap, sink=sink)
-            if cap:
-                self.ring.advance()
+        # no Python GC while capturing: a collection that frees another engine's CUDAGraph calls hipGraphDestroy, which
+        # is not permitted while a stream captures (the capture and the process abort)
+        import gc
+        was_enabled = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g, pool=model._graph_pool):
+                self.out, _ = model.forward(self.batch, capture_latents=cap, sink=sink)
+                if cap:
+                    self.ring.advance()
+        finally:
+            if was_enabled:
+                gc.enable()
         self.graph = g

@@ -63,6 +63,8 @@ def main():
                 rec["latent_bytes_per_step"] = int(sum(t.numel() * t.element_size() for t in kept[-1] if t is not None))
             print(json.dumps(rec), flush=True)
             del eng, kept
+            import gc
+            gc.collect()  # the engine's captured graphs are freed here, not by a collection during the next capture
             torch.cuda.empty_cache()
 
 
