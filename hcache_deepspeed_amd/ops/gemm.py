@@ -158,8 +158,13 @@ def _wgrad_run(layout, dy2, x2, out, accumulate, dyt=None, xt=None):
 
 
 def _time_layout(layout, dy2, x2, out, accumulate, dyt=None, xt=None, reps=2):
-    scratch = torch.zeros_like(out)
-    _wgrad_run(layout, dy2, x2, scratch, accumulate, dyt, xt)  # warm (hipBLASLt solution lookup, allocator)
+    """Milliseconds of one layout; inf when its scratch (output copy, transposes) does not fit: a near-full device
+    (large micro-batches, offloaded optimizer states) must not fail in the autotuner."""
+    try:
+        scratch = torch.zeros_like(out)
+        _wgrad_run(layout, dy2, x2, scratch, accumulate, dyt, xt)  # warm (hipBLASLt solution lookup, allocator)
+    except torch.OutOfMemoryError:
+        return float("inf")
     best = float("inf")
     for _ in range(reps):  # min of reps: one timed run mis-picked the down-projection layout in situ
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -217,8 +222,11 @@ def wgrad(dy2, x2, out, accumulate=False, dyt=None, xt=None):
                 layout = min(times, key=times.get)
                 if x2 is not None and layout != "direct" and times[layout] > 0.97 * times["direct"]:
                     layout = "direct"  # within noise: keep the plain form
-                _WGRAD_CHOICE[key] = layout
-                _NT_BY_N[N] = layout.startswith("nt")
+                if times[layout] == float("inf"):  # nothing fit: the plain form now, time again on a later call
+                    layout = "direct" if x2 is not None else "nt"
+                else:
+                    _WGRAD_CHOICE[key] = layout
+                    _NT_BY_N[N] = layout.startswith("nt")
     elif x2 is None and not layout.startswith("nt"):
         layout = "nt"
     _wgrad_run(layout, dy2, x2, out, accumulate, dyt, xt)
@@ -262,13 +270,17 @@ def dgrad(dy2, w, out=None, cache=None):
             if layout is None:
                 times = {}
                 for cand in ("direct", "nt"):
-                    _dgrad_run(cand, dy2, w, None)
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    _dgrad_run(cand, dy2, w, None)
-                    e1.record()
-                    e1.synchronize()
-                    times[cand] = e0.elapsed_time(e1)
+                    try:  # a near-full device: a candidate whose scratch does not fit is out
+                        _dgrad_run(cand, dy2, w, None)
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        _dgrad_run(cand, dy2, w, None)
+                        e1.record()
+                        e1.synchronize()
+                        times[cand] = e0.elapsed_time(e1)
+                    except torch.OutOfMemoryError:
+                        times[cand] = float("inf")
                 layout = "nt" if times["nt"] < 0.97 * times["direct"] else "direct"
-                _DGRAD_CHOICE[key] = layout
+                if min(times.values()) < float("inf"):
+                    _DGRAD_CHOICE[key] = layout
     return _dgrad_run(layout, dy2, w, out, cache)
