@@ -34,7 +34,8 @@ using namespace hds;
 using namespace hds::attn;
 
 // variant 9 lives in its own translation unit (flash_attn_w64.hip: built with the VGPR-form MFMA selection)
-int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, hipStream_t st);
+int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, int rebalanced,
+                            hipStream_t st);
 
 namespace {
 
@@ -1418,9 +1419,10 @@ int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_b
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
 // 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel);
 // 6 = 5 without the full-tile DMA fast path; 7 = 5 + per-wave skip of the causal tiles above its queries;
-// 8 = 5 with 4-wave workgroups (two per CU); 9 = one wave per SIMD, 64 rows per wave (attn_fwd_w64_kernel)
+// 8 = 5 with 4-wave workgroups (two per CU); 9 = one wave per SIMD, 64 rows per wave (attn_fwd_w64_kernel);
+// 10 = 9 with the softmax VALU split over both MFMA blocks
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 9) return hipErrorInvalidValue;
+  if (var < 0 || var > 10) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1462,7 +1464,8 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
             hipLaunchKernelGGL((attn_fwd_sp_kernel<D, true, false, 4>), dim3((max_len + 127) / 128, hq, batch),
                                dim3(256), 0, st, p);
             break;
-          case 9: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, st);
+          case 9: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 0, st);
+          case 10: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 1, st);
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;

@@ -34,9 +34,10 @@ __device__ __forceinline__ void mfma_pv(f32x16& o, const bf16x8& v, const bf16x8
 __device__ __forceinline__ void mfma_pv_fresh(f32x16& o, const bf16x8& v, const bf16x8& pb) {  // P just written
   asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(pb));
 }
+constexpr float kMaskPen = 1048576.f;  // 2^20, times the -1 of a masked score (see mask_tile)
 __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
 
-template <int D>
+template <int D, bool REB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_fwd_w64_kernel(AttnParams p) {
   constexpr int NW = 4, BM = 64 * NW, PW = 16 / NW;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
@@ -79,13 +80,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int first = q0 - p.window + 1;
     kt_begin = first > 0 ? first / BN : 0;
   }
-  auto rowp = [&](const bf16* base, int64_t stride, int kt) {
-    return [=](int row) {
-      int r = kt * BN + row;
-      r = r < len ? r : len - 1;
-      return base + (int64_t)(start + r) * stride + (int64_t)hk * D;
-    };
-  };
   int32_t dk[PW], dv[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
@@ -94,14 +88,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     dk[i] = (int32_t)(((int64_t)row * p.sk + 8 * ch) * 2);
     dv[i] = (int32_t)(((int64_t)row * p.sv + 8 * ch) * 2);
   }
+  // LDS-DMA of tile kt: wave-uniform tile base + this lane's byte offset; the last, partial tile clamps its rows to
+  // the sequence end (the same instruction stream, offsets recomputed)
   auto stage = [&](char* dst, const bf16* base, int64_t stride, const int32_t* off, int kt) {
-    if (kt * BN + BN <= len) {
-      const char* tb = (const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D);
+    const char* tb = (const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D);
+    const bool full = kt * BN + BN <= len;
 #pragma unroll
-      for (int i = 0; i < PW; ++i)
-        __builtin_amdgcn_global_load_lds((gbl_void*)(tb + off[i]), (lds_void*)(dst + (w * PW + i) * 1024), 16, 0, 0);
-    } else {
-      stage_tile_d<NW, D>(dst, rowp(base, stride, kt));
+    for (int i = 0; i < PW; ++i) {
+      int32_t o = off[i];
+      if (!full) {
+        const int row = 4 * (w * PW + i) + (lane >> 4);
+        const int r = min(kt * BN + row, len - 1) - kt * BN;
+        o = (int32_t)(((int64_t)r * stride + 8 * ((lane & 15) ^ swz(row))) * 2);
+      }
+      __builtin_amdgcn_global_load_lds((gbl_void*)(tb + o), (lds_void*)(dst + (w * PW + i) * 1024), 16, 0, 0);
     }
   };
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
@@ -123,8 +123,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int dt = 0; dt < DT; ++dt) o[dt][0] = o[dt][1] = f32x16{};
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
 
-  // S of one 64-key tile for both query halves: sc[t][qh], t = key half. 8 ks x (2 t) K fragments streamed in pairs.
-  auto s_tile = [&](auto KOFF, f32x16 (&sc)[2][2]) {
+  // S of one 64-key tile for both query halves, sn[t][qh] (t = key half), K fragments streamed 4 at a time; beside
+  // its 32 MFMAs, FX(chunk) runs the softmax VALU of the PREVIOUS tile in 4 chunks (the MFMAs are the builtin in its
+  // VGPR form -- this TU is built with -amdgpu-mfma-vgpr-form -- so sched_group_barrier can interleave them).
+  auto s_tile = [&](auto KOFF, f32x16 (&sn)[2][2], auto&& FX) {
+    constexpr bool TRANS_SPLIT = REB;
     constexpr int KO = decltype(KOFF)::value;
     static_for<2>([&](auto TC) {
       constexpr int t = decltype(TC)::value;
@@ -146,21 +149,233 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) {
+          if constexpr (j == 0) sn[t][qh] = f32x16{};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int ks = 4 * j + i;
-            if (ks == 0)
-              mfma_sq0(sc[t][qh], kr[j][i], qf[qh][ks]);
-            else if (ks == KS - 1)
-              mfma_sq_end(sc[t][qh], kr[j][i], qf[qh][ks]);
-            else
-              mfma_sq(sc[t][qh], kr[j][i], qf[qh][ks]);
+          for (int i = 0; i < 4; ++i) sn[t][qh] = mfma(kr[j][i], qf[qh][4 * j + i], sn[t][qh]);
+        }
+        FX(std::integral_constant<int, 2 * t + j>{});
+        if constexpr (TRANS_SPLIT) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x400, 2, 0);  // 2 exp2 (8 issue cycles each)
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 2 row-sum adds + 1 cvt
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // then ~6 VALU (fma, exp, add pairs / cvt)
           }
         }
       });
     });
   };
+  auto no_fx = [](auto) {};
 
+  // arithmetic mask of tile kt on the scores sn: key = base + (r & 3) + 8 (r >> 2) with base = k0 + 32 t + 4 h; the
+  // sign of (key - lo) | (hi - key) says "outside [lo, hi]", and a masked score drops by kMaskPen. No per-element
+  // compare: 64 v_cmp masks of the two query halves live at once would spill the SGPR file. The penalty is ONE
+  // moderate constant, not -inf or a multiple of 1e30: a row whose keys in the first tile are all masked takes its
+  // running max from masked scores, and fma(s, c, -max) must not round above 0 by more than exp2 can take (a 1e30
+  // scale rounds by ~1e22 there: exp2 -> inf, and inf x alpha = 0 -> NaN); 2^20 keeps the rounding < 0.01 and still
+  // sends every masked exp2 to 0 once a real key arrives (alpha = exp2(-2^20 c) = 0 rescales the masked start away)
+  auto mask_tile = [&](f32x16 (&sn)[2][2], int kt) {
+    const int k0 = kt * BN;
+    const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
+                           (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
+    if (need_mask) {
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int base = k0 + 32 * t + 4 * h;
+          const int A = base - klo[qh], B = khi[qh] - base;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ar = (r & 3) + 8 * (r >> 2);
+            const int pen = ((A + ar) | (B - ar)) >> 31;  // -1 outside [lo, hi], 0 inside
+            sn[t][qh][r] = __builtin_fmaf((float)pen, kMaskPen, sn[t][qh][r]);
+          }
+        }
+    }
+  };
+
+  if constexpr (REB) {
+    constexpr bool kAddsInB = false;  // row sums of key half 1 in block B (more balanced, 32 more live VGPRs there)
+    // ---- rebalanced pipeline: the softmax VALU of a tile is split over BOTH MFMA blocks so that no MFMA gap carries
+    // more than ~24 cycles of vector issue (MI355X_MICROARCH.md, one wave per SIMD: 32-cycle gap, 8 held by the MFMA)
+    //   block A (32 S_{kt+1} MFMAs): exp2 of x_kt (64 x 8 cyc), bf16 P_kt (16 cvt), K reads, half of the row sums
+    //   block B (32 P_kt.V_kt MFMAs): the other row sums, the max of S_{kt+1} (32 max3), the running-max update and
+    //            x_{kt+1} = S_{kt+1} c - m (64 fma), V reads
+    // x_kt enters the tile already scaled and shifted: exp2 is the only op between it and P.
+    f32x16 x[2][2], sn[2][2];
+    float tm[2][2], alpha[2] = {1.f, 1.f}, muse[2] = {0.f, 0.f}, rs[2][2];
+    bool move_any = false;
+    // block-B VALU, slot s = 0..31 (one per P.V MFMA): 0..15 the max of sn, 15 the max update, 16..31 sn c - m (in
+    // place: x_kt dies with the row sums of slots 0..15, and the next tile's x is this sn)
+    auto bvx = [&](auto SC) {
+      constexpr int sl = decltype(SC)::value;
+      if constexpr (sl < 16) {
+        constexpr int qh = sl >> 3, t = (sl >> 2) & 1, r = (sl & 3) * 4;
+        if constexpr (r == 0) {
+          tm[qh][t] = max3_raw(sn[t][qh][0], sn[t][qh][1], sn[t][qh][2]);
+          tm[qh][t] = max3_raw(tm[qh][t], sn[t][qh][3], sn[t][qh][3]);
+        } else {
+          tm[qh][t] = max3_raw(tm[qh][t], sn[t][qh][r], sn[t][qh][r + 1]);
+          tm[qh][t] = max3_raw(tm[qh][t], sn[t][qh][r + 2], sn[t][qh][r + 3]);
+        }
+        if constexpr (sl == 15) {
+          move_any = false;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            float tmax = fmaxf(tm[q][0], tm[q][1]);
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
+            const bool move = !__all(tmax <= m[q] + kDeferThr);
+            const float mnew = move ? fmaxf(m[q], tmax) : m[q];
+            alpha[q] = move ? ((m[q] == -INFINITY) ? 0.f : fast_exp2(m[q] - mnew)) : 1.f;
+            m[q] = mnew;
+            muse[q] = (mnew == -INFINITY) ? 0.f : mnew;
+            move_any |= move;
+          }
+        }
+      } else {
+        constexpr int u = sl - 16, qh = u >> 3, t = (u >> 2) & 1, r = (u & 3) * 4;
+        float y0 = __builtin_fmaf(sn[t][qh][r], c, -muse[qh]), y1 = __builtin_fmaf(sn[t][qh][r + 1], c, -muse[qh]);
+        float y2 = __builtin_fmaf(sn[t][qh][r + 2], c, -muse[qh]), y3 = __builtin_fmaf(sn[t][qh][r + 3], c, -muse[qh]);
+        asm volatile("" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));  // stay in this slot (pure: would sink otherwise)
+        sn[t][qh][r] = y0;  // in place
+        sn[t][qh][r + 1] = y1;
+        sn[t][qh][r + 2] = y2;
+        sn[t][qh][r + 3] = y3;
+      }
+    };
+    // row sums of the exponentials of key half 1 (chunks 2, 3 of block A), two per block-B slot 0..15
+    auto badd = [&](auto SC) {
+      constexpr int sl = decltype(SC)::value;
+      if constexpr (kAddsInB && sl < 16) {
+        constexpr int qh = sl >> 3, r = (sl & 7) * 2;
+        rs[qh][0] += x[1][qh][r];
+        rs[qh][1] += x[1][qh][r + 1];
+      }
+    };
+    // block-A VALU of chunk cc = 2 t + j (8 S MFMAs): exp2 of x[t][.][8 j .. 8 j + 7] for both query halves, their
+    // bf16 P fragments, and (key half 0 only) their row sums
+    bf16x8 pb[2][4];
+    auto fa = [&](auto CC) {
+      constexpr int cc = decltype(CC)::value, t = cc >> 1, j = cc & 1;
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int r = 8 * j; r < 8 * j + 8; ++r) {
+          x[t][qh][r] = fast_exp2(x[t][qh][r]);
+          if constexpr (t == 0 || !kAddsInB) rs[qh][r & 1] += x[t][qh][r];
+        }
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) pb[qh][2 * t + j] = j == 0 ? acc_to_b<0>(x[t][qh]) : acc_to_b<1>(x[t][qh]);
+      // pin this chunk's results here: the exponentials are pure, and the optimizer would otherwise sink them past
+      // the mask branch that follows block A, next to their first use in block B -- out of the S MFMAs they fill
+      asm volatile("" : "+v"(pb[0][2 * t + j]), "+v"(pb[1][2 * t + j]), "+v"(rs[0][0]), "+v"(rs[0][1]), "+v"(rs[1][0]),
+                   "+v"(rs[1][1]));
+    };
+
+    stage(smem + 0, p.k, p.sk, dk, kt_begin);
+    stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
+    if (kt_begin + 1 < kt_end) {
+      stage(smem + TL, p.k, p.sk, dk, kt_begin + 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    __syncthreads();
+    s_tile(std::integral_constant<int, 0>{}, sn, no_fx);
+    mask_tile(sn, kt_begin);
+    static_for<32>([&](auto SC) { bvx(SC); });  // O = 0, l = 0: alpha is moot
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) x[t][qh] = sn[t][qh];
+
+    auto tile = [&](auto BUFC, int kt) {
+      constexpr int buf = decltype(BUFC)::value;
+      constexpr int KN = (buf ^ 1) * TL;
+      constexpr int VT = 2 * TL + buf * TL;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < kt_end) stage(smem + 2 * TL + (buf ^ 1) * TL, p.v, p.sv, dv, kt + 1);
+      if (kt + 2 < kt_end) stage(smem + buf * TL, p.k, p.sk, dk, kt + 2);
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) rs[qh][0] = rs[qh][1] = 0.f;
+      const bool more = kt + 1 < kt_end;
+      // block A runs on the last tile too (S of a stale K buffer, discarded below): a branch around it would let the
+      // optimizer hoist the exponentials, which both arms need, out of the MFMA block they are meant to fill
+      const float m_keep[2] = {m[0], m[1]};
+      s_tile(std::integral_constant<int, KN>{}, sn, fa);  // block A
+      mask_tile(sn, kt + 1);
+      // ---- block B: O += V_kt^T.P_kt, 32 asm MFMAs, each followed by its VALU slot (sched_barrier-fenced: hipcc
+      // cannot see an asm MFMA, so the interleave is the source order) ----
+      bf16x8 vf[2][DT];
+      static_for<DT>([&](auto DC) {
+        constexpr int dt = decltype(DC)::value;
+        vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
+      });
+      static_for<4>([&](auto STC) {
+        constexpr int st = decltype(STC)::value;
+        if constexpr (st + 1 < 4) {
+          static_for<DT>([&](auto DC) {
+            constexpr int dt = decltype(DC)::value;
+            vf[(st + 1) & 1][dt] = lds_tr8<VT + 4096 * (st + 1)>(av0[dt], av1[dt]);
+          });
+          lds_wait_tie<8>(vf[st & 1][0], vf[st & 1][1], vf[st & 1][2], vf[st & 1][3]);
+        } else {
+          lds_wait_tie<0>(vf[st & 1][0], vf[st & 1][1], vf[st & 1][2], vf[st & 1][3]);
+        }
+        static_for<2 * DT>([&](auto IC) {
+          constexpr int i = decltype(IC)::value, qh = i / DT, dt = i % DT, sl = 8 * st + i;
+          if constexpr (sl == 0)
+            mfma_pv_fresh(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
+          else
+            mfma_pv(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
+          badd(std::integral_constant<int, sl>{});
+          bvx(std::integral_constant<int, sl>{});
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      });
+      // l and O follow P_kt's reference max, then move to m_{kt+1} (alpha = 1 unless the max moved)
+      if (!more) {  // the max update of the stale tile is void
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          m[qh] = m_keep[qh];
+          alpha[qh] = 1.f;
+        }
+        move_any = false;
+      }
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        float r = rs[qh][0] + rs[qh][1];
+        r += __shfl_xor(r, 32, 64);
+        l[qh] = (l[qh] + r) * alpha[qh];
+      }
+      if (move_any) {  // rare: drain the P.V MFMAs before reading O back from the accumulator file
+        xdl_drain();
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          o[dt][0] *= alpha[0];
+          o[dt][1] *= alpha[1];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) x[t][qh] = sn[t][qh];
+    };
+    int kt = kt_begin;
+    for (; kt + 1 < kt_end; kt += 2) {
+      tile(std::integral_constant<int, 0>{}, kt);
+      tile(std::integral_constant<int, 1>{}, kt + 1);
+    }
+    if (kt < kt_end) tile(std::integral_constant<int, 0>{}, kt);
+  } else {
   stage(smem + 0, p.k, p.sk, dk, kt_begin);
   stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
   if (kt_begin + 1 < kt_end) {
@@ -171,7 +386,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   __syncthreads();
   f32x16 sc[2][2];
-  s_tile(std::integral_constant<int, 0>{}, sc);
+  s_tile(std::integral_constant<int, 0>{}, sc, no_fx);
 
   auto tile = [&](auto BUFC, int kt) {
     constexpr int buf = decltype(BUFC)::value;
@@ -186,13 +401,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const bool need_mask = (k0 + BN > len) || (p.causal && k0 + BN - 1 > wq_lo) ||
                            (p.window > 0 && k0 <= wq_hi - p.window) || (wq_hi >= len);
     if (need_mask) {
+      // arithmetic mask (see mask_tile)
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh)
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t) {
+          const int base = k0 + 32 * t + 4 * h;
+          const int A = base - klo[qh], B = khi[qh] - base;
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (outside(k0 + 32 * t + acc_row(r, h), klo[qh], khi[qh])) sc[t][qh][r] = -INFINITY;
+          for (int r = 0; r < 16; ++r) {
+            const int ar = (r & 3) + 8 * (r >> 2);
+            const int pen = ((A + ar) | (B - ar)) >> 31;
+            sc[t][qh][r] = __builtin_fmaf((float)pen, kMaskPen, sc[t][qh][r]);
+          }
+        }
     }
     float alpha[2], muse[2];
     bool move_any = false;
@@ -222,29 +444,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
 
-    // ---- block A: S_{kt+1} beside exp(S_kt keys 0..31) for both query halves ----
-    f32x16 sn[2][2];
+    // ---- block A: S_{kt+1} (32 MFMAs) beside the whole softmax of tile kt: chunk c = 2 t + j exponentiates
+    // sc[t][qh][8 j .. 8 j + 7] of both query halves (16 scores) and converts the finished bf16 P fragments ----
     float rs[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-    auto exp_keys = [&](int t, int qh, int r0, int r1) {
-#pragma unroll
-      for (int r = r0; r < r1; ++r) {
-        const float e = fast_exp2(__builtin_fmaf(sc[t][qh][r], c, -muse[qh]));
-        sc[t][qh][r] = e;
-        rs[qh][r & 1] += e;
-      }
-    };
-    if (kt + 1 < kt_end) {
-      s_tile(std::integral_constant<int, KN>{}, sn);
-    }
-    exp_keys(0, 0, 0, 16);
-    exp_keys(0, 1, 0, 16);
     bf16x8 pb[2][4];
+    auto fx = [&](auto CC) {
+      constexpr int cc = decltype(CC)::value, t = cc >> 1, j = cc & 1;
 #pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      pb[qh][0] = acc_to_b<0>(sc[0][qh]);
-      pb[qh][1] = acc_to_b<1>(sc[0][qh]);
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int r = 8 * j; r < 8 * j + 8; ++r) {
+          const float e = fast_exp2(__builtin_fmaf(sc[t][qh][r], c, -muse[qh]));
+          sc[t][qh][r] = e;
+          rs[qh][r & 1] += e;
+        }
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) pb[qh][2 * t + j] = j == 0 ? acc_to_b<0>(sc[t][qh]) : acc_to_b<1>(sc[t][qh]);
+    };
+    f32x16 sn[2][2];
+    if (kt + 1 < kt_end) {
+      s_tile(std::integral_constant<int, KN>{}, sn, fx);
+    } else {
+      static_for<4>([&](auto CC) { fx(CC); });
     }
-    // ---- block B: O += V_kt^T.P_kt (k-steps 0,1 = keys 0..31 first) beside exp(S_kt keys 32..63) ----
+
+    // ---- block B: O += V_kt^T.P_kt (32 MFMAs, O in the accumulator file) ----
     bf16x8 vf[2][DT];
     static_for<DT>([&](auto DC) {
       constexpr int dt = decltype(DC)::value;
@@ -265,21 +489,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int qh = 0; qh < 2; ++qh)
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          if (dt == 0 && (st == 0 || st == 2))
+          if (st == 0 && qh == 0 && dt == 0)
             mfma_pv_fresh(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
           else
             mfma_pv(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
         }
-      if constexpr (st == 0) {
-        exp_keys(1, 0, 0, 16);
-      } else if constexpr (st == 1) {
-        exp_keys(1, 1, 0, 16);
-#pragma unroll
-        for (int qh = 0; qh < 2; ++qh) {
-          pb[qh][2] = acc_to_b<0>(sc[1][qh]);
-          pb[qh][3] = acc_to_b<1>(sc[1][qh]);
-        }
-      }
     });
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
@@ -299,6 +513,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   if (kt < kt_end) tile(std::integral_constant<int, 0>{}, kt);
 
+  }
+
   xdl_drain();
 #pragma unroll
   for (int qh = 0; qh < 2; ++qh) {
@@ -317,9 +533,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 }  // namespace
 
-int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, hipStream_t st) {
+int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, int rebalanced,
+                            hipStream_t st) {
   if (params_bytes != sizeof(AttnParams)) return hipErrorInvalidValue;
   const AttnParams& p = *static_cast<const AttnParams*>(params);
-  hipLaunchKernelGGL((attn_fwd_w64_kernel<128>), dim3((max_len + 255) / 256, hq, batch), dim3(256), 0, st, p);
+  const dim3 grid((max_len + 255) / 256, hq, batch);
+  if (rebalanced)
+    hipLaunchKernelGGL((attn_fwd_w64_kernel<128, true>), grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((attn_fwd_w64_kernel<128, false>), grid, dim3(256), 0, st, p);
   return hipGetLastError();
 }

@@ -597,6 +597,7 @@ class HostActivationCache:
                 "throttle_wait_s": round(self.throttle_wait_s, 2),
                 "peak_gib_all_steps": round(self.peak_seen / 2**30, 1),
                 "last_step_peak_gib": round(self.last_step_peak / 2**30, 2),
+                "step_peaks_gib": [round(x / 2**30, 1) for x in self.step_peak_history[-16:]],
                 "bwd_extra_gib": round(self.bwd_extra / 2**30, 2)}
 
 

@@ -36,7 +36,9 @@ HIPCC_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-con
 # adjacent scalar f32 muls / adds of the softmax into v_pk_mul_f32 / v_pk_add_f32, which cost MORE issue cycles than
 # two scalar ops beside the MFMAs (MI355X_MICROARCH "price of one filler"): backward 4.10 -> 3.84 ms, headline
 # 24,121 -> 24,440 tok/s on the same box (profiles/r3/fa_noslp_ab_r3p.txt)
-FILE_FLAGS = {"flash_attn.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"flash_attn.hip": ["-fno-slp-vectorize"],
+              # the one-wave-per-SIMD forward keeps S in VGPRs (builtin MFMAs, schedulable) and O in AGPRs (asm)
+              "flash_attn_w64.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
 HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include",
               "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 

@@ -777,6 +777,8 @@ class ZeroOptimizer:
             if self._last_pre_uid != u.uid:  # a bucket unit's later modules do not re-enter the trace
                 self._last_pre_uid = u.uid
                 self._record_and_prefetch(u)
+                if self.state_offload is not None:  # pace the forward to the post-step state offload's drains
+                    self.state_offload.on_forward_position()
             self._fetch(u, "forward")
 
         return pre
@@ -1633,14 +1635,14 @@ class ZeroOptimizer:
     def _seg_group(self, seg):
         return self.param_groups[seg.group]
 
-    def enable_state_offload(self, include_master=True, ratio=1.0):
+    def enable_state_offload(self, include_master=True, ratio=1.0, chunk_mb=1024):
         """Optimizer states (and the fp32 master) live in pinned host memory between ``step()`` and the late
         backward of the next step (compile ``offload_opt_states``)."""
         if self.kind == "generic":
             raise NotImplementedError("offload_opt_states needs a fused optimizer (Adam/Lion/Adagrad) over the flat store")
         from .state_offload import OptimizerStateOffload
         if self.state_offload is None:
-            self.state_offload = OptimizerStateOffload(self, include_master, ratio)
+            self.state_offload = OptimizerStateOffload(self, include_master, ratio, chunk_mb)
             # off the device from the start: the first forward is the one that needs the HBM when the states and
             # the activations do not fit together
             self.state_offload.offload()

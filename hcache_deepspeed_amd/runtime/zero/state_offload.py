@@ -21,33 +21,53 @@ whole 32 GB states (round 4). r = 1 moves everything (a = 0). Readers that need 
 ``safe_get_full_fp32_param``) call ``wait()``, which materializes them (head ++ tail, one device concatenation) and
 leaves them whole until the next step's ``offload()`` splits them again.
 
-Offload and reload run on SEPARATE copy streams: a reload issued while the post-step offload of other states is still
-draining does not queue behind it -- it waits only for its own state's offload.
+The tail is moved in CHUNKS of ``chunk_mb`` (default 1 GiB; ``cuts()`` includes every chunk boundary, so the step
+still runs per contiguous piece):
+
+* each chunk's HBM returns to the allocator as soon as ITS D2H drains (the allocator polls the copy events at every
+  allocation), so the next forward's activations grow into the memory the offload frees, chunk by chunk, instead of
+  waiting for a whole 10-30 GB state; at every forward unit ``on_forward_position()`` waits for just enough of the
+  oldest chunks to drain to hold that unit's activations (the growth measured on the previous step) -- an allocation
+  that found nothing free would otherwise make the allocator synchronize EVERY outstanding copy at once;
+* the backward reloads chunk by chunk as its freed HBM allows, and a chunk fits into a fragmented pool where a whole
+  tail (a contiguous 10+ GB block) does not.
+
+Offload and reload run on SEPARATE copy streams: a reload issued while the post-step offload of other chunks is still
+draining does not queue behind it -- it waits only for its own chunk's offload.
 """
+import collections
+
 import torch
 
 
 class OptimizerStateOffload:
 
-    def __init__(self, zopt, include_master=True, ratio=1.0):
+    def __init__(self, zopt, include_master=True, ratio=1.0, chunk_mb=1024):
         self.z = zopt
         self.include_master = bool(include_master)
         self.ratio = min(1.0, max(0.0, float(ratio)))
+        self.chunk_bytes = max(256, int(float(chunk_mb) * 2**20))
         dev = zopt.device
         self.cuda = dev.type == "cuda"
         self.stream = torch.cuda.Stream(dev, priority=-1) if self.cuda else None  # offload (D2H)
         self.reload_stream = torch.cuda.Stream(dev, priority=-1) if self.cuda else None  # reload (H2D)
         self.host = {}  # key -> pinned tail [n - a]
-        self.tail = {}  # key -> device tail [n - a] while resident (reloaded), else absent
-        self.events = {}  # key -> last D2H / H2D event of its tail
-        self.split = False  # heads + tails (not whole flat states)
-        self.offloaded = False  # tails off the device (not reloaded yet)
+        self.tail = {}  # key -> [device chunk or None (off the device)] per tail chunk
+        self.events = {}  # (key, chunk) -> last D2H / H2D event of that chunk
+        self.split = False  # heads + tail chunks (not whole flat states)
+        self.offloaded = False  # tail chunks (some) off the device, not all reloaded yet
         self.reloading = False
         self.reload_pos = None  # backward trace position that triggers the reload (None: backward start)
         self.a = None  # split element
+        self.bounds = []  # [(lo, hi)] element ranges of the tail chunks, lo of the first = a
         self.bytes = 0
         self.n_offloads = 0
         self.n_reloads = 0
+        self._draining = collections.deque()  # (event, bytes) of chunks whose D2H may still run, oldest first
+        self._fwd_growth = 0  # largest per-unit growth of allocated HBM in the last forward (bytes)
+        self._fwd_last = None
+        self.fwd_waits = 0  # chunk drains the forward waited for (last step)
+        self.fwd_wait_s = 0.0
 
     # -----------------------------------------------------------------------------------------------------
     def _keys(self):
@@ -72,25 +92,36 @@ class OptimizerStateOffload:
         else:
             s.states[k] = t
 
-    def _split_at(self, n):
+    def _split_at(self, n, es=4):
         if self.a is None:
             a = int(round((1.0 - self.ratio) * n))
             self.a = min(n, (a + 63) // 64 * 64) if a > 0 else 0  # 256-B aligned pieces for the vector kernels
+            c = max(64, self.chunk_bytes // es // 64 * 64)
+            self.bounds = [(lo, min(n, lo + c)) for lo in range(self.a, n, c)]
         return self.a
 
     def cuts(self):
-        """Element offsets at which ``step()`` must split its ranges (the head/tail boundary while split)."""
-        return (self.a, ) if self.split and self.a else ()
+        """Element offsets at which ``step()`` must split its ranges: the head/tail boundary and every chunk
+        boundary while split."""
+        if not self.split:
+            return ()
+        return tuple(lo for lo, _ in self.bounds if lo > 0)
+
+    def _chunk_of(self, lo):
+        c = self.bounds[0][1] - self.bounds[0][0]
+        return (lo - self.a) // c
 
     def view(self, k, lo, hi):
         """[lo, hi) of state ``k`` (``k`` = "master" or a moment key) inside ONE piece (never across a cut)."""
         if not self.split or k not in self.host:  # not split, or a state this executor does not move
             return self._get(k)[lo:hi]
-        a = self.a
-        if hi <= a:
+        if hi <= self.a:
             return self._get(k)[lo:hi]
-        assert lo >= a, "a range across the head/tail cut"
-        return self.tail[k][lo - a:hi - a]
+        assert lo >= self.a, "a range across the head/tail cut"
+        i = self._chunk_of(lo)
+        c0, c1 = self.bounds[i]
+        assert hi <= c1, "a range across a tail chunk boundary"
+        return self.tail[k][i][lo - c0:hi - c0]
 
     def moves(self, k):
         return k in self.host or (not self.split and k in self._keys())
@@ -100,95 +131,152 @@ class OptimizerStateOffload:
         if self.host:
             return sum(h.numel() * h.element_size() for h in self.host.values())
         n = self.z.store.numel
-        return sum((n - self._split_at(n)) * self._get(k).element_size() for k in self._keys())
+        return sum((n - self._split_at(n, self._get(k).element_size())) * self._get(k).element_size()
+                   for k in self._keys())
 
     # -----------------------------------------------------------------------------------------------------
     def offload(self):
-        """After ``step()``: D2H every state's tail on the copy stream, release its HBM once the DMA drains. Whole
-        (materialized) states are split first: the head is a new allocation, the whole buffer is released."""
+        """After ``step()``: D2H every tail chunk on the copy stream; each chunk's HBM returns to the allocator when
+        its own DMA drains. Whole (materialized) states are split first: the head is a new allocation."""
         if self.offloaded:
             return
         self.bytes = 0
         cur = torch.cuda.current_stream() if self.cuda else None
+        if self.cuda:
+            self.stream.wait_stream(cur)
         keys = self._keys() if not self.split else list(self.host)
         for k in keys:
             if self.split:
-                t, head = self.tail.pop(k, None), None
-                if t is None:
+                chunks, head = self.tail.get(k), None
+                if chunks is None:
                     continue
-            else:  # whole flat state -> head (stays) + tail (goes)
+            else:  # whole flat state -> head (stays) + tail chunks (go)
                 full = self._get(k)
                 n = full.numel()
                 if n == 0:
                     continue
-                a = self._split_at(n)
+                a = self._split_at(n, full.element_size())
                 head = full[:a].clone() if a else full.new_empty(0)
-                t = full[a:]
-            n_t = t.numel()
+                chunks = [full[lo:hi] for lo, hi in self.bounds]  # views: the whole buffer goes with the last one
+            a = self.a
             h = self.host.get(k)
-            if h is None or h.numel() != n_t:
-                h = self.host[k] = torch.empty(n_t, dtype=t.dtype, pin_memory=self.cuda)
-            if self.cuda:
-                self.stream.wait_stream(cur)
-                with torch.cuda.stream(self.stream):
-                    h.copy_(t, non_blocking=True)
-                    t.record_stream(self.stream)  # the block recycles only after the DMA drained
-                    ev = torch.cuda.Event()
-                    ev.record(self.stream)
-                self.events[k] = ev
-            else:
-                h.copy_(t)
+            if h is None or h.numel() != self.z.store.numel - a:
+                h = self.host[k] = torch.empty(self.z.store.numel - a, dtype=chunks[0].dtype if chunks else torch.float32,
+                                               pin_memory=self.cuda)
+            for i, t in enumerate(chunks):
+                if t is None:
+                    continue
+                lo, hi = self.bounds[i]
+                nb = t.numel() * t.element_size()
+                if self.cuda:
+                    with torch.cuda.stream(self.stream):
+                        h[lo - a:hi - a].copy_(t, non_blocking=True)
+                        t.record_stream(self.stream)  # the block recycles only after ITS DMA drained
+                        ev = torch.cuda.Event()
+                        ev.record(self.stream)
+                    self.events[(k, i)] = ev
+                    self._draining.append((ev, nb))
+                else:
+                    h[lo - a:hi - a].copy_(t)
+                self.bytes += nb
+            self.tail[k] = [None] * len(self.bounds)
+            del chunks
             if head is not None:
                 self._set(k, head)
-            self.bytes += n_t * t.element_size()
         self.split = True
         self.offloaded = True
         self.reloading = False
         self.n_offloads += 1
+        self._fwd_last = None
+        self.fwd_waits, self.fwd_wait_s = 0, 0.0
+
+    def on_forward_position(self):
+        """Before a forward unit runs: retire the drained chunks and, if the HBM the allocator can hand out does not
+        hold this unit's activation growth (measured on the previous forward), wait for the oldest draining chunks --
+        just enough of them -- instead of letting a failed allocation synchronize every outstanding copy."""
+        if not self.cuda:
+            return
+        dq = self._draining
+        while dq and dq[0][0].query():
+            dq.popleft()
+        alloc = torch.cuda.memory_allocated(self.z.device)
+        if self._fwd_last is not None:
+            self._fwd_growth = max(self._fwd_growth, alloc - self._fwd_last)
+        self._fwd_last = alloc
+        if not dq:
+            return
+        need = 2 * self._fwd_growth + (1 << 30) if self._fwd_growth else 4 << 30
+        free, _ = torch.cuda.mem_get_info(self.z.device)
+        draining = sum(nb for _, nb in dq)
+        usable = free + max(0, torch.cuda.memory_reserved(self.z.device) - alloc - draining)
+        if usable >= need:
+            return
+        import time
+        t0 = time.perf_counter()
+        while dq and usable < need:
+            ev, nb = dq.popleft()
+            ev.synchronize()
+            usable += nb
+            self.fwd_waits += 1
+        self.fwd_wait_s += time.perf_counter() - t0
 
     def _pending(self):
-        """(key, host tail) of the tails still off the device."""
-        return [(k, h) for k, h in self.host.items() if k not in self.tail] if self.offloaded else []
+        """(key, chunk) of the tail chunks still off the device, largest states first."""
+        if not self.offloaded:
+            return []
+        return [(k, i) for k in self.host for i in range(len(self.bounds)) if self.tail[k][i] is None]
 
-    def reload(self, keys=None):
-        """Issue the H2D of the offloaded tails (all, or ``keys``; non-blocking); ``wait_tails()`` orders the compute
-        stream after it."""
+    def _chunk_bytes(self, k, i):
+        lo, hi = self.bounds[i]
+        return (hi - lo) * self.host[k].element_size()
+
+    def reload(self, keys=None, chunks=None):
+        """Issue the H2D of the offloaded tail chunks (all, those of ``keys``, or the (key, chunk) pairs ``chunks``;
+        non-blocking); ``wait_tails()`` orders the compute stream after them."""
         if not self.offloaded or self.reloading:
             return
         cur = torch.cuda.current_stream() if self.cuda else None
-        for k, h in self._pending():
-            if keys is not None and k not in keys:
+        ready = None
+        todo = chunks if chunks is not None else [(k, i) for k, i in self._pending() if keys is None or k in keys]
+        for k, i in todo:
+            if self.tail[k][i] is not None:
                 continue
+            lo, hi = self.bounds[i]
+            h = self.host[k][lo - self.a:hi - self.a]
             buf = torch.empty(h.numel(), dtype=h.dtype, device=self.z.device)  # compute stream's allocator pool
             if self.cuda:
-                ready = torch.cuda.Event()
-                ready.record(cur)
+                if ready is None:
+                    ready = torch.cuda.Event()
+                    ready.record(cur)
                 rs = self.reload_stream
                 with torch.cuda.stream(rs):
                     rs.wait_event(ready)
-                    if k in self.events:
-                        rs.wait_event(self.events[k])  # this tail's offload has drained (and only this one)
+                    e = self.events.get((k, i))
+                    if e is not None:
+                        rs.wait_event(e)  # this chunk's offload has drained (and only this one)
                     buf.copy_(h, non_blocking=True)
                     buf.record_stream(rs)
                     ev = torch.cuda.Event()
                     ev.record(rs)
-                self.events[k] = ev
+                self.events[(k, i)] = ev
             else:
                 buf.copy_(h)
-            self.tail[k] = buf
+            self.tail[k][i] = buf
         if not self._pending():
             self.reloading = True
             self.n_reloads += 1
 
     def wait_tails(self):
-        """Before ``step()``: every tail on the device and ordered before the current stream (states stay split)."""
+        """Before ``step()``: every tail chunk on the device and ordered before the current stream (states stay
+        split)."""
         if not self.offloaded:
             return
         self.reload()
         if self.cuda:
             cur = torch.cuda.current_stream()
             for k in self.tail:
-                cur.wait_event(self.events[k])
+                for i in range(len(self.bounds)):
+                    cur.wait_event(self.events[(k, i)])
         self.offloaded = False
         self.reloading = False
 
@@ -199,8 +287,10 @@ class OptimizerStateOffload:
         if not self.split:
             return
         for k in list(self.tail):
-            head, t = self._get(k), self.tail.pop(k)
-            self._set(k, torch.cat([head, t]) if head.numel() else t)
+            parts = self.tail.pop(k)
+            head = self._get(k)
+            self._set(k, torch.cat(([head] if head.numel() else []) + parts))
+            del parts
         self.split = False
 
     ensure_resident = wait
@@ -215,17 +305,26 @@ class OptimizerStateOffload:
         if not self.cuda:
             self.reload()
             return
-        # no schedule: bring each tail back as soon as the HBM the backward has freed holds it -- at the start of
-        # backward when everything fits, late (tail by tail) when the tails and the activations do not fit
+        # no schedule: bring each chunk back as soon as the HBM the backward has freed holds it -- at the start of
+        # backward when everything fits, late (chunk by chunk) when the tails and the activations do not fit
         # together; step() reloads whatever is left
         limit = int(self.mem_fraction * torch.cuda.get_device_properties(self.z.device).total_memory)
-        for k, h in sorted(self._pending(), key=lambda x: -x[1].numel() * x[1].element_size()):
-            if torch.cuda.memory_allocated(self.z.device) + h.numel() * h.element_size() <= limit:
-                self.reload(keys={k})
+        alloc = torch.cuda.memory_allocated(self.z.device)
+        todo = []
+        for k, i in self._pending():
+            nb = self._chunk_bytes(k, i)
+            if alloc + nb > limit:
+                break
+            alloc += nb
+            todo.append((k, i))
+        if todo:
+            self.reload(chunks=todo)
 
-    mem_fraction = 0.9
+    mem_fraction = 0.92
 
     def stats(self):
         return {"state_bytes": self.bytes, "offloads": self.n_offloads, "reloads": self.n_reloads,
                 "reload_pos": self.reload_pos, "ratio": self.ratio, "split_element": self.a,
+                "chunks": len(self.bounds), "chunk_mb": round(self.chunk_bytes / 2**20, 3),
+                "fwd_waits": self.fwd_waits, "fwd_wait_s": round(self.fwd_wait_s, 3),
                 "states": sorted(self.host) if self.host else sorted(self._keys())}

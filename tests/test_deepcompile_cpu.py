@@ -150,7 +150,7 @@ def test_state_reload_placement():
     assert pos == 4
 
 
-def _state_offload_run(rank, world, stage, out, ratio=1.0):
+def _state_offload_run(rank, world, stage, out, ratio=1.0, chunk_mb=1024):
     import os
     import hcache_deepspeed_amd as ds
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
@@ -163,7 +163,7 @@ def _state_offload_run(rank, world, stage, out, ratio=1.0):
                "compile": {"offload_opt_states": off}}
         eng, _, _, _ = ds.initialize(model=m, config=cfg)
         if off:
-            eng.compile(compile_kwargs={"offload_states_ratio": ratio})
+            eng.compile(compile_kwargs={"offload_states_ratio": ratio, "offload_states_chunk_mb": chunk_mb})
         z = eng.optimizer
         g = torch.Generator().manual_seed(5 + rank)
         losses = []
@@ -180,7 +180,10 @@ def _state_offload_run(rank, world, stage, out, ratio=1.0):
                 a = so.a
                 assert a == (0 if ratio == 1.0 else min(n, (round((1 - ratio) * n) + 63) // 64 * 64)), (a, n)
                 assert z.store.states["exp_avg"].numel() == a and z.store.master.numel() == a
-                assert so.state_bytes() == 3 * 4 * (n - a) and not so.tail
+                assert so.state_bytes() == 3 * 4 * (n - a)
+                assert all(c is None for cs in so.tail.values() for c in cs)  # every tail chunk off the device
+                c = max(64, int(chunk_mb * 2**20) // 4 // 64 * 64)
+                assert len(so.bounds) == -(-(n - a) // c) and (so.cuts() or (0, ))[-1] == so.bounds[-1][0]
                 assert so.n_offloads == step + 2  # offloaded at compile(), then after every step
         if off:
             assert z.state_offload.n_reloads == 3  # the states start off the device: every step reloads them
@@ -192,12 +195,15 @@ def _state_offload_run(rank, world, stage, out, ratio=1.0):
     assert torch.equal(res["wFalse"], res["wTrue"])
 
 
-@pytest.mark.parametrize("stage,world,ratio", [(3, 1, 1.0), (3, 2, 1.0), (1, 2, 1.0), (3, 1, 0.3), (3, 2, 0.55)])
-def test_offload_adam_states_keeps_trajectory(stage, world, ratio):
+@pytest.mark.parametrize("stage,world,ratio,chunk_mb", [(3, 1, 1.0, 1024), (3, 2, 1.0, 1024), (1, 2, 1.0, 1024),
+                                                         (3, 1, 0.3, 1024), (3, 2, 0.55, 1024), (3, 1, 0.55, 0.02),
+                                                         (3, 2, 1.0, 0.05)])
+def test_offload_adam_states_keeps_trajectory(stage, world, ratio, chunk_mb):
     """Optimizer states and the fp32 master offloaded after every step and reloaded in the next backward: the
     training trajectory is bit-identical to keeping them resident (GAS=2: only the boundary step moves them). With
-    ratio < 1 exactly that fraction of every state (its tail) moves and the step runs per piece (byte-granular)."""
-    run_distributed(_state_offload_run, world, stage, None, ratio)
+    ratio < 1 exactly that fraction of every state (its tail) moves and the step runs per piece (byte-granular); small
+    ``chunk_mb``: the tail moves as many chunks, each its own piece of the step."""
+    run_distributed(_state_offload_run, world, stage, None, ratio, chunk_mb)
 
 
 def test_param_offload_plan():
