@@ -34,8 +34,11 @@ using namespace hds;
 using namespace hds::attn;
 
 // variant 9 lives in its own translation unit (flash_attn_w64.hip: built with the VGPR-form MFMA selection)
-int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, int rebalanced,
+int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, int mode,
                             hipStream_t st);
+// one-wave-per-SIMD dQ (flash_attn_bwd_w64.hip)
+int hds_attn_bwd_dq_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq,
+                               hipStream_t st);
 
 namespace {
 
@@ -1414,15 +1417,15 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 }  // namespace
 
-int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_bwd_pipe = 0;
+int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_bwd_pipe = 0, g_dq_var = 0;
 
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
 // 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel);
 // 6 = 5 without the full-tile DMA fast path; 7 = 5 + per-wave skip of the causal tiles above its queries;
 // 8 = 5 with 4-wave workgroups (two per CU); 9 = one wave per SIMD, 64 rows per wave (attn_fwd_w64_kernel);
-// 10 = 9 with the softmax VALU split over both MFMA blocks
+// 10 = 9 with the softmax VALU split over both MFMA blocks; 11 = 10 with block A hand-scheduled (asm S MFMAs, Q in AGPRs)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 10) return hipErrorInvalidValue;
+  if (var < 0 || var > 11) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1430,6 +1433,14 @@ HDS_EXPORT int hds_attn_fwd_variant(int var) {
 // backward: dK/dV kernel with LDS reads pipelined two MFMAs ahead (0 / 1; head_dim 128)
 HDS_EXPORT int hds_attn_bwd_pipe(int on) {
   g_bwd_pipe = on < 0 ? 0 : (on > 2 ? 2 : on);  // 2: + uniform-base LDS-DMA staging of full tiles
+  return 0;
+}
+
+// backward dQ kernel: 0 = 8 waves x 32 query rows (attn_bwd_dq_kernel), 1 = one wave per SIMD x 64 rows
+// (attn_bwd_dq_w64_kernel, head_dim 128)
+HDS_EXPORT int hds_attn_bwd_dq_variant(int var) {
+  if (var < 0 || var > 1) return hipErrorInvalidValue;
+  g_dq_var = var;
   return 0;
 }
 
@@ -1466,6 +1477,7 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
             break;
           case 9: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 0, st);
           case 10: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 1, st);
+          case 11: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 2, st);
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;
@@ -1517,8 +1529,15 @@ int launch_bwd(const AttnParams& p, int batch, int max_len, int total_tokens, in
     }
   }
   done = false;
+  if constexpr (D == 128) {
+    if (g_dq_var == 1) {
+      const int rc = hds_attn_bwd_dq_w64_launch(&p, sizeof(p), batch, max_len, hq, st);
+      if (rc != 0) return rc;
+      done = true;
+    }
+  }
   if constexpr (D <= 128) {
-    if (g_dq_nw == 8) {
+    if (!done && g_dq_nw == 8) {
       const dim3 grid((max_len + 255) / 256, hq, batch);
       if (g_bwd_pipe == 2 && D == 128)
         hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 1, false, 2>), grid, dim3(512), 0, st, p);

@@ -34,14 +34,34 @@ __device__ __forceinline__ void mfma_pv(f32x16& o, const bf16x8& v, const bf16x8
 __device__ __forceinline__ void mfma_pv_fresh(f32x16& o, const bf16x8& v, const bf16x8& pb) {  // P just written
   asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(pb));
 }
+// S MFMAs of the hand-scheduled block A (variant 11): Q from the accumulator file ("a"), K and S in VGPRs. hipcc does
+// not pad asm MFMA hazards: the block ends with 13 wait states before any VALU reads S (s_tile_m).
+__device__ __forceinline__ void mfma_s_first(f32x16& s, const bf16x8& k, const bf16x8& q) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(s) : "v"(k), "a"(q));
+}
+__device__ __forceinline__ void mfma_s(f32x16& s, const bf16x8& k, const bf16x8& q) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(s) : "v"(k), "a"(q));
+}
+// max / sum with the other 32-lane half (lane ^ 32) through v_permlane32_swap: a VALU op, where __shfl_xor may become a
+// ds_bpermute round trip through the LDS pipe (~100+ cycles, exposed at one wave per SIMD)
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 constexpr float kMaskPen = 1048576.f;  // 2^20, times the -1 of a masked score (see mask_tile)
 __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
 
-template <int D, bool REB>
+template <int D, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_fwd_w64_kernel(AttnParams p) {
   constexpr int NW = 4, BM = 64 * NW, PW = 16 / NW;
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
   static_assert(D == 128, "one-wave-per-SIMD forward: head_dim 128");
+  constexpr bool REB = MODE >= 1;     // softmax VALU split over both MFMA blocks (variant 10)
+  constexpr bool MANUAL_A = MODE == 2;  // block A as asm MFMAs reading Q from the accumulator file (variant 11)
   __shared__ __attribute__((aligned(1024))) char smem[4 * TL];  // K[2], V[2]
   int blk, hq, b;
   lpt_ids(blk, hq, b);
@@ -172,6 +192,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     });
   };
   auto no_fx = [](auto) {};
+  // variant 11's block A: the same 32 S MFMAs as inline asm, K fragments through a 3-deep ring of 4-fragment groups
+  // g = 2 t + j (two groups in flight), each MFMA followed by its VALU slot SLOT(m), m = 8 g + 4 qh + i, fenced by
+  // sched_barrier so the source order is the issue order
+  auto s_tile_m = [&](auto KOFF, f32x16 (&sn)[2][2], auto&& SLOT) {
+    constexpr int KO = decltype(KOFF)::value;
+    bf16x8 kr[3][4];
+    auto issue = [&](auto GC) {
+      constexpr int g = decltype(GC)::value, t = g >> 1, j = g & 1, b = g % 3;
+      static_for<4>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        kr[b][i] = lds_b128<KO + 8192 * t>(ak[4 * j + i]);
+      });
+    };
+    issue(std::integral_constant<int, 0>{});
+    issue(std::integral_constant<int, 1>{});
+    static_for<4>([&](auto GC) {
+      constexpr int g = decltype(GC)::value, t = g >> 1, j = g & 1, b = g % 3;
+      if constexpr (g == 0) {
+        issue(std::integral_constant<int, 2>{});
+        lds_wait_tie<8>(kr[b][0], kr[b][1], kr[b][2], kr[b][3]);
+      } else if constexpr (g == 1) {
+        lds_wait_tie<4>(kr[b][0], kr[b][1], kr[b][2], kr[b][3]);  // (group 3 not issued yet: 4 = group 2)
+      } else if constexpr (g == 2) {
+        issue(std::integral_constant<int, 3>{});  // into group 0's buffer: its MFMAs have issued
+        lds_wait_tie<4>(kr[b][0], kr[b][1], kr[b][2], kr[b][3]);
+      } else {
+        lds_wait_tie<0>(kr[b][0], kr[b][1], kr[b][2], kr[b][3]);
+      }
+      static_for<8>([&](auto IC) {
+        constexpr int ii = decltype(IC)::value, qh = ii >> 2, i = ii & 3, m = 8 * g + ii;
+        if constexpr (j == 0 && i == 0)
+          mfma_s_first(sn[t][qh], kr[b][i], qf[qh][4 * j + i]);
+        else
+          mfma_s(sn[t][qh], kr[b][i], qf[qh][4 * j + i]);
+        SLOT(std::integral_constant<int, m>{});
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    SLOT(std::integral_constant<int, 32>{});  // drain of a one-slot software pipeline
+    asm volatile("s_nop 7\n\ts_nop 4" ::: "memory");  // XDL result -> VALU read of S
+  };
 
   // arithmetic mask of tile kt on the scores sn: key = base + (r & 3) + 8 (r >> 2) with base = k0 + 32 t + 4 h; the
   // sign of (key - lo) | (hi - key) says "outside [lo, hi]", and a masked score drops by kMaskPen. No per-element
@@ -229,8 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           move_any = false;
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            float tmax = fmaxf(tm[q][0], tm[q][1]);
-            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
+            const float tmax = xor32_max(fmaxf(tm[q][0], tm[q][1])) * c;
             const bool move = !__all(tmax <= m[q] + kDeferThr);
             const float mnew = move ? fmaxf(m[q], tmax) : m[q];
             alpha[q] = move ? ((m[q] == -INFINITY) ? 0.f : fast_exp2(m[q] - mnew)) : 1.f;
@@ -278,6 +338,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       asm volatile("" : "+v"(pb[0][2 * t + j]), "+v"(pb[1][2 * t + j]), "+v"(rs[0][0]), "+v"(rs[0][1]), "+v"(rs[1][0]),
                    "+v"(rs[1][1]));
     };
+    // variant 11: block A's VALU per S MFMA m = 8 g + 4 qh + i (g = 2 t + j): exp2 of x[t][qh][8 j + 2 i, + 1], their row
+    // sums and ONE v_cvt_pk_bf16_f32 into dword i of P fragment (qh, g) -- "2 exp, 2 add, 1 cvt" in every gap
+    uint32_t pw[2][4][4];
+    // software-pipelined by one slot: slot m issues the exponentials of pair m and consumes (row sums, bf16 pack)
+    // pair m - 1, whose v_exp_f32 results are an MFMA gap old -- at one wave per SIMD no other wave hides the
+    // transcendental latency of a dependent add / cvt right behind it. Slot 32 (after the last MFMA) drains.
+    auto fa_slot = [&](auto MC) {
+      constexpr int m = decltype(MC)::value;
+      if constexpr (m < 32) {
+        constexpr int g = m >> 3, t = g >> 1, j = g & 1, qh = (m >> 2) & 1, i = m & 3, r = 8 * j + 2 * i;
+        float ea = fast_exp2(x[t][qh][r]), eb = fast_exp2(x[t][qh][r + 1]);
+        asm volatile("" : "+v"(ea), "+v"(eb));  // issued in this slot
+        x[t][qh][r] = ea;
+        x[t][qh][r + 1] = eb;
+      }
+      if constexpr (m >= 1) {
+        constexpr int mc = m - 1, g = mc >> 3, t = g >> 1, j = g & 1, qh = (mc >> 2) & 1, i = mc & 3;
+        constexpr int r = 8 * j + 2 * i;
+        const float ea = x[t][qh][r], eb = x[t][qh][r + 1];
+        rs[qh][0] += ea;
+        rs[qh][1] += eb;
+        uint32_t wv;
+        asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(wv) : "v"(ea), "v"(eb));
+        pw[qh][g][i] = wv;
+        float r0 = rs[qh][0], r1 = rs[qh][1];
+        asm volatile("" : "+v"(r0), "+v"(r1));  // stay in this slot (see fa)
+        rs[qh][0] = r0;
+        rs[qh][1] = r1;
+      }
+    };
 
     stage(smem + 0, p.k, p.sk, dk, kt_begin);
     stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
@@ -288,7 +378,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     }
     __syncthreads();
-    s_tile(std::integral_constant<int, 0>{}, sn, no_fx);
+    if constexpr (MANUAL_A)
+      s_tile_m(std::integral_constant<int, 0>{}, sn, no_fx);
+    else
+      s_tile(std::integral_constant<int, 0>{}, sn, no_fx);
     mask_tile(sn, kt_begin);
     static_for<32>([&](auto SC) { bvx(SC); });  // O = 0, l = 0: alpha is moot
 #pragma unroll
@@ -302,15 +395,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       constexpr int VT = 2 * TL + buf * TL;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (kt + 1 < kt_end) stage(smem + 2 * TL + (buf ^ 1) * TL, p.v, p.sv, dv, kt + 1);
-      if (kt + 2 < kt_end) stage(smem + buf * TL, p.k, p.sk, dk, kt + 2);
+      // V_{kt+1} and K_{kt+2} are staged by 8 LDS-DMA pieces per wave issued one per 4 P.V MFMAs in block B (its
+      // vector-issue slack), not in a burst here: a piece costs its wave ~60-185 issue cycles in a burst. Past the
+      // sequence end a piece re-reads the last tile into a buffer nobody reads (no branch in the MFMA block).
+      const int ktv = min(kt + 1, kt_end - 1), ktk = min(kt + 2, kt_end - 1);
+      const char* tbv = (const char*)(p.v + (int64_t)(start + ktv * BN) * p.sv + (int64_t)hk * D);
+      const char* tbk = (const char*)(p.k + (int64_t)(start + ktk * BN) * p.sk + (int64_t)hk * D);
+      int32_t ovv[PW], okk[PW];
+      {
+        const bool fv = ktv * BN + BN <= len, fk = ktk * BN + BN <= len;
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+          const int row = 4 * (w * PW + i) + (lane >> 4), ch = 8 * ((lane & 15) ^ swz(row));
+          const int rv = min(ktv * BN + row, len - 1) - ktv * BN, rk = min(ktk * BN + row, len - 1) - ktk * BN;
+          ovv[i] = fv ? dv[i] : (int32_t)(((int64_t)rv * p.sv + ch) * 2);
+          okk[i] = fk ? dk[i] : (int32_t)(((int64_t)rk * p.sk + ch) * 2);
+        }
+      }
+      char* const dstv = smem + 2 * TL + (buf ^ 1) * TL + w * PW * 1024;
+      char* const dstk = smem + buf * TL + w * PW * 1024;
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) rs[qh][0] = rs[qh][1] = 0.f;
       const bool more = kt + 1 < kt_end;
       // block A runs on the last tile too (S of a stale K buffer, discarded below): a branch around it would let the
       // optimizer hoist the exponentials, which both arms need, out of the MFMA block they are meant to fill
       const float m_keep[2] = {m[0], m[1]};
-      s_tile(std::integral_constant<int, KN>{}, sn, fa);  // block A
+      if constexpr (MANUAL_A) {
+        s_tile_m(std::integral_constant<int, KN>{}, sn, fa_slot);  // block A
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            pb[qh][g] = __builtin_bit_cast(bf16x8, u32x4{pw[qh][g][0], pw[qh][g][1], pw[qh][g][2], pw[qh][g][3]});
+      } else {
+        s_tile(std::integral_constant<int, KN>{}, sn, fa);  // block A
+      }
       mask_tile(sn, kt + 1);
       // ---- block B: O += V_kt^T.P_kt, 32 asm MFMAs, each followed by its VALU slot (sched_barrier-fenced: hipcc
       // cannot see an asm MFMA, so the interleave is the source order) ----
@@ -338,6 +457,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             mfma_pv(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
           badd(std::integral_constant<int, sl>{});
           bvx(std::integral_constant<int, sl>{});
+          if constexpr (sl % 4 == 1) {
+            constexpr int j = sl / 4;
+            if constexpr (j < PW)
+              __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
+            else
+              __builtin_amdgcn_global_load_lds((gbl_void*)(tbk + okk[j - PW]), (lds_void*)(dstk + (j - PW) * 1024), 16,
+                                               0, 0);
+          }
           __builtin_amdgcn_sched_barrier(0);
         });
       });
@@ -351,11 +478,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         move_any = false;
       }
 #pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        float r = rs[qh][0] + rs[qh][1];
-        r += __shfl_xor(r, 32, 64);
-        l[qh] = (l[qh] + r) * alpha[qh];
-      }
+      for (int qh = 0; qh < 2; ++qh) l[qh] = (l[qh] + xor32_sum(rs[qh][0] + rs[qh][1])) * alpha[qh];
       if (move_any) {  // rare: drain the P.V MFMAs before reading O back from the accumulator file
         xdl_drain();
 #pragma unroll
@@ -533,14 +656,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 }  // namespace
 
-int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, int rebalanced,
+int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, int max_len, int hq, int mode,
                             hipStream_t st) {
   if (params_bytes != sizeof(AttnParams)) return hipErrorInvalidValue;
   const AttnParams& p = *static_cast<const AttnParams*>(params);
   const dim3 grid((max_len + 255) / 256, hq, batch);
-  if (rebalanced)
-    hipLaunchKernelGGL((attn_fwd_w64_kernel<128, true>), grid, dim3(256), 0, st, p);
-  else
-    hipLaunchKernelGGL((attn_fwd_w64_kernel<128, false>), grid, dim3(256), 0, st, p);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 0>), grid, dim3(256), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 1>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 2>), grid, dim3(256), 0, st, p); break;
+  }
   return hipGetLastError();
 }

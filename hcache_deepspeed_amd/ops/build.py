@@ -38,7 +38,8 @@ HIPCC_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-con
 # 24,121 -> 24,440 tok/s on the same box (profiles/r3/fa_noslp_ab_r3p.txt)
 FILE_FLAGS = {"flash_attn.hip": ["-fno-slp-vectorize"],
               # the one-wave-per-SIMD forward keeps S in VGPRs (builtin MFMAs, schedulable) and O in AGPRs (asm)
-              "flash_attn_w64.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
+              "flash_attn_w64.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+              "flash_attn_bwd_w64.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
 HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include",
               "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 

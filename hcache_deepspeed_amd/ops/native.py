@@ -44,6 +44,7 @@ _KERNEL_SIGS = {
     "hds_attn_head_dim_supported": "i",
     "hds_attn_config": "iii",
     "hds_attn_fwd_variant": "i",
+    "hds_attn_bwd_dq_variant": "i",
     "hds_attn_bwd_prio": "i",
     "hds_attn_bwd_pipe": "i",
     "hds_bsattn_fwd": "p" * 8 + "i" * 7 + "f" + "i" + "s",
@@ -158,6 +159,8 @@ def load_kernels(build_if_missing=True):
         lib.hds_attn_bwd_pipe(int(os.environ.get("HDS_ATTN_BWD_PIPE", "2")))
         # FlashAttention forward variant (csrc/kernels/flash_attn.hip hds_attn_fwd_variant; 5 = software-pipelined)
         lib.hds_attn_fwd_variant(int(os.environ.get("HDS_ATTN_FWD_VAR", "5")))
+        # FlashAttention backward dQ kernel (hds_attn_bwd_dq_variant; 1 = one wave per SIMD, 64 rows per wave)
+        lib.hds_attn_bwd_dq_variant(int(os.environ.get("HDS_ATTN_DQ_VAR", "0")))
         _klib = lib
         return _klib
 

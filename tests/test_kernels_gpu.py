@@ -665,7 +665,7 @@ def test_decode_attention_matches_reference_gpu(D, H, Hkv, S):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("case", ["causal", "full", "window", "varlen"])
 def test_flash_fwd_staggered_variant_gpu(case, variant):
     """Forward variants 4 (staggered wave groups) and 5 (software-pipelined softmax) against variant 2 and the fp32
@@ -847,3 +847,57 @@ def test_adam_flat_lp_out_dtypes_gpu(lp_kind):
     torch.testing.assert_close(p.cpu(), want, rtol=1e-5, atol=1e-6)
     tol = {"bf16": 1e-2, "fp16": 1e-3}.get(lp_kind, 1e-6)
     torch.testing.assert_close(lp.float().cpu(), want, rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["causal", "full", "window", "varlen", "gqa_odd"])
+def test_flash_bwd_dq_w64_matches_gpu(case):
+    """Backward dQ variant 1 (one wave per SIMD, 64 query rows per wave, flash_attn_bwd_w64.hip) against variant 0 and
+    the fp32 autograd reference; dK / dV come from the same kernel either way and must not move."""
+    from hcache_deepspeed_amd.ops import native
+    from hcache_deepspeed_amd.ops.attention import flash_attn
+    lib = native.kernels()
+    torch.manual_seed(11)
+    B, S, Hq, Hkv, D = (2, 700, 8, 2, 128) if case != "gqa_odd" else (1, 333, 6, 3, 128)
+    q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
+    kw = dict(causal=case != "full", window=100 if case == "window" else 0)
+    grads = {}
+    try:
+        for var in (0, 1):
+            assert lib.hds_attn_bwd_dq_variant(var) == 0
+            qg, kg, vg = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+            if case == "varlen":
+                cu = torch.tensor([0, 333, 2 * S], device="cuda", dtype=torch.int32)
+                o = flash_attn(qg.reshape(-1, Hq, D), kg.reshape(-1, Hkv, D), vg.reshape(-1, Hkv, D),
+                               causal=True, cu_seqlens=cu).reshape(B, S, Hq, D)
+            else:
+                o = flash_attn(qg, kg, vg, **kw)
+            o.backward(do)
+            torch.cuda.synchronize()
+            grads[var] = (qg.grad, kg.grad, vg.grad)
+    finally:
+        lib.hds_attn_bwd_dq_variant(int(os.environ.get("HDS_ATTN_DQ_VAR", "0")))
+    dq0, dq1 = grads[0][0].float(), grads[1][0].float()
+    assert torch.isfinite(dq1).all()
+    rel = ((dq1 - dq0).norm() / dq0.norm()).item()
+    assert rel < 1e-2, rel
+    assert torch.equal(grads[0][1], grads[1][1]) and torch.equal(grads[0][2], grads[1][2])
+    if case in ("causal", "full", "window"):
+        G = Hq // Hkv
+        qf, kf, vf = (t.float().transpose(1, 2).requires_grad_(True) for t in (q, k.repeat_interleave(G, 2),
+                                                                                 v.repeat_interleave(G, 2)))
+        s = qf @ kf.transpose(-1, -2) / D**0.5
+        i = torch.arange(S, device="cuda")
+        mask = torch.zeros(S, S, dtype=torch.bool, device="cuda")
+        if kw["causal"]:
+            mask |= i[None, :] > i[:, None]
+        if kw["window"]:
+            mask |= i[None, :] <= i[:, None] - kw["window"]
+        ref = torch.softmax(s.masked_fill(mask, float("-inf")), -1) @ vf
+        ref.backward(do.float().transpose(1, 2))
+        dq_ref = qf.grad.transpose(1, 2)
+        rel_ref = ((dq1 - dq_ref).norm() / dq_ref.norm()).item()
+        assert rel_ref < 2e-2, rel_ref
