@@ -52,6 +52,16 @@ __device__ __forceinline__ float xor32_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// cycle stamp (cdna_hip_programming.md "In-kernel stamps"): s_memtime with its own lgkmcnt(0), fenced on both sides.
+// Placed only where no LDS read is in flight (block boundaries).
+__device__ __forceinline__ uint64_t memtime_stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ unsigned long long g_w64_stamps[8];  // segment cycles summed over waves, tiles, waves
 constexpr float kMaskPen = 1048576.f;  // 2^20, times the -1 of a masked score (see mask_tile)
 __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
 
@@ -61,7 +71,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int KS = Dim<D>::KS, DT = Dim<D>::DT, TL = Dim<D>::TILE;
   static_assert(D == 128, "one-wave-per-SIMD forward: head_dim 128");
   constexpr bool REB = MODE >= 1;     // softmax VALU split over both MFMA blocks (variant 10)
-  constexpr bool MANUAL_A = MODE == 2;  // block A as asm MFMAs reading Q from the accumulator file (variant 11)
+  constexpr bool MANUAL_A = MODE >= 2;  // block A as asm MFMAs reading Q from the accumulator file (variant 11)
+  constexpr bool STAMPS = MODE == 3;    // variant 12 = 11 + per-segment cycle stamps (hds_attn_w64_stamps)
+  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
+  auto stamp = [&](auto SEG) {
+    if constexpr (STAMPS) {
+      constexpr int sg = decltype(SEG)::value;
+      const uint64_t t = memtime_stamp();
+      if constexpr (sg >= 0) st_acc[sg] += t - st_prev;
+      st_prev = t;
+    }
+  };
   __shared__ __attribute__((aligned(1024))) char smem[4 * TL];  // K[2], V[2]
   int blk, hq, b;
   lpt_ids(blk, hq, b);
@@ -393,8 +413,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       constexpr int buf = decltype(BUFC)::value;
       constexpr int KN = (buf ^ 1) * TL;
       constexpr int VT = 2 * TL + buf * TL;
+      stamp(std::integral_constant<int, 4>{});  // seg 4: the previous tile's tail (l, rescale, x = S)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      stamp(std::integral_constant<int, 0>{});  // seg 0: DMA wait + barrier
       // V_{kt+1} and K_{kt+2} are staged by 8 LDS-DMA pieces per wave issued one per 4 P.V MFMAs in block B (its
       // vector-issue slack), not in a burst here: a piece costs its wave ~60-185 issue cycles in a burst. Past the
       // sequence end a piece re-reads the last tile into a buffer nobody reads (no branch in the MFMA block).
@@ -430,7 +452,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       } else {
         s_tile(std::integral_constant<int, KN>{}, sn, fa);  // block A
       }
+      stamp(std::integral_constant<int, 1>{});  // seg 1: DMA offsets + block A
       mask_tile(sn, kt + 1);
+      stamp(std::integral_constant<int, 2>{});  // seg 2: P pack + mask
       // ---- block B: O += V_kt^T.P_kt, 32 asm MFMAs, each followed by its VALU slot (sched_barrier-fenced: hipcc
       // cannot see an asm MFMA, so the interleave is the source order) ----
       bf16x8 vf[2][DT];
@@ -468,6 +492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           __builtin_amdgcn_sched_barrier(0);
         });
       });
+      stamp(std::integral_constant<int, 3>{});  // seg 3: block B
       // l and O follow P_kt's reference max, then move to m_{kt+1} (alpha = 1 unless the max moved)
       if (!more) {  // the max update of the stale tile is void
 #pragma unroll
@@ -492,12 +517,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) x[t][qh] = sn[t][qh];
     };
+    stamp(std::integral_constant<int, -1>{});
+    const uint64_t st_t0 = st_prev;
     int kt = kt_begin;
     for (; kt + 1 < kt_end; kt += 2) {
       tile(std::integral_constant<int, 0>{}, kt);
       tile(std::integral_constant<int, 1>{}, kt + 1);
     }
     if (kt < kt_end) tile(std::integral_constant<int, 0>{}, kt);
+    stamp(std::integral_constant<int, 4>{});
+    if constexpr (STAMPS) {
+      st_acc[5] = st_prev - st_t0;  // the whole loop
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_w64_stamps[k], (unsigned long long)st_acc[k]);
+        atomicAdd(&g_w64_stamps[6], (unsigned long long)(kt_end - kt_begin));
+        atomicAdd(&g_w64_stamps[7], 1ull);
+      }
+    }
   } else {
   stage(smem + 0, p.k, p.sk, dk, kt_begin);
   stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
@@ -664,7 +701,19 @@ int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, 
   switch (mode) {
     case 0: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 0>), grid, dim3(256), 0, st, p); break;
     case 1: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 1>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 2>), grid, dim3(256), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 2>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 3>), grid, dim3(256), 0, st, p); break;
   }
   return hipGetLastError();
+}
+
+// variant 12's stamps: out[0..4] cycles per segment (DMA wait + barrier, block A, mask, block B, tail), out[5] the whole
+// loop, summed over waves; out[6] tiles summed over waves' workgroups; out[7] waves. reset != 0 zeroes them after.
+HDS_EXPORT int hds_attn_w64_stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w64_stamps), sizeof(g_w64_stamps));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_w64_stamps), z, sizeof(z));
+  }
+  return e;
 }

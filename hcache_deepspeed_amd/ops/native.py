@@ -45,6 +45,7 @@ _KERNEL_SIGS = {
     "hds_attn_config": "iii",
     "hds_attn_fwd_variant": "i",
     "hds_attn_bwd_dq_variant": "i",
+    "hds_attn_w64_stamps": "pi",
     "hds_attn_bwd_prio": "i",
     "hds_attn_bwd_pipe": "i",
     "hds_bsattn_fwd": "p" * 8 + "i" * 7 + "f" + "i" + "s",

@@ -1215,7 +1215,13 @@ class ZeroOptimizer:
 
     def _pre_backward(self, u):
         self._fetch(u, "backward")
-        if self.partitioned and self._fwd_trace and not self._recording:
+        so = self.state_offload
+        traced = self.partitioned and self._fwd_trace and not self._recording
+        if so is not None and self.boundary and not traced:
+            # no trace positions (nothing partitioned, e.g. one rank): reload the offloaded optimizer states as the
+            # HBM the backward frees allows -- before this, a one-rank run reloaded them all inside step()
+            so.on_backward_position(None)
+        if traced:
             t = self._fwd_trace
             try:
                 i = len(t) - 1 - t[::-1].index(u.uid)

@@ -298,8 +298,8 @@ class OptimizerStateOffload:
     def on_backward_position(self, pos):
         if not self.offloaded or self.reloading:
             return
-        if self.reload_pos is not None:  # placed by the compiled schedule (compile/passes.plan_state_reload)
-            if pos is not None and pos <= self.reload_pos:
+        if self.reload_pos is not None and pos is not None:  # placed by the compiled schedule (plan_state_reload)
+            if pos <= self.reload_pos:
                 self.reload()
             return
         if not self.cuda:

@@ -1,0 +1,33 @@
+"""Where a one-wave-per-SIMD forward tile spends its cycles: run forward variant 12 (variant 11 + s_memtime stamps at
+the block boundaries) at the bench shape and print cycles per tile and wave for each segment."""
+import ctypes
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from hcache_deepspeed_amd.ops import native  # noqa: E402
+from hcache_deepspeed_amd.ops.attention import flash_attn  # noqa: E402
+
+lib = native.kernels()
+B, S, Hq, Hkv, D = 7, 4096, 32, 8, 128
+q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
+k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+out = (ctypes.c_ulonglong * 8)()
+lib.hds_attn_fwd_variant(12)
+for _ in range(2):
+    flash_attn(q, k, v, causal=True)
+torch.cuda.synchronize()
+lib.hds_attn_w64_stamps(out, 1)
+for _ in range(3):
+    flash_attn(q, k, v, causal=True)
+torch.cuda.synchronize()
+lib.hds_attn_w64_stamps(out, 1)
+lib.hds_attn_fwd_variant(5)
+waves, tiles = out[7], out[6]  # tiles summed per wave (each wave adds its workgroup's tile count)
+names = ["dma wait + barrier", "block A (S MFMAs + exp)", "P pack + mask", "block B (PV MFMAs + max)", "tail", "loop"]
+print(f"waves {waves}, tiles per wave {tiles / max(1, waves):.1f}")
+for i, n in enumerate(names):
+    print(f"{n:28s} {out[i] / max(1, tiles):9.0f} cycles per tile")
+print(f"{'MFMA floor (64 x 32)':28s} {2048:9d}")
