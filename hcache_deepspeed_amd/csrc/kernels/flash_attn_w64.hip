@@ -409,6 +409,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) x[t][qh] = sn[t][qh];
 
+    // last tile this wave computes: past it every key follows the wave's last row (causal)
+    const int kt_end_w = p.causal ? min(kt_end, wq_hi / BN + 1) : kt_end;
     auto tile = [&](auto BUFC, int kt) {
       constexpr int buf = decltype(BUFC)::value;
       constexpr int KN = (buf ^ 1) * TL;
@@ -436,14 +438,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       char* const dstv = smem + 2 * TL + (buf ^ 1) * TL + w * PW * 1024;
       char* const dstk = smem + buf * TL + w * PW * 1024;
+      if (kt >= kt_end_w) {  // idle tile: its keys all follow this wave's rows (causal); the wave still stages its
+        // share of the tiles the other waves read and keeps the barrier count (stamps: the waves with the most mask
+        // work on the diagonal tiles set the pace at every barrier)
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+          __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((gbl_void*)(tbk + okk[j]), (lds_void*)(dstk + j * 1024), 16, 0, 0);
+        }
+        return;
+      }
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) rs[qh][0] = rs[qh][1] = 0.f;
-      const bool more = kt + 1 < kt_end;
+      const bool more = kt + 1 < kt_end_w;
       // block A runs on the last tile too (S of a stale K buffer, discarded below): a branch around it would let the
       // optimizer hoist the exponentials, which both arms need, out of the MFMA block they are meant to fill
       const float m_keep[2] = {m[0], m[1]};
       if constexpr (MANUAL_A) {
-        s_tile_m(std::integral_constant<int, KN>{}, sn, fa_slot);  // block A
+        // block A; the 8 LDS-DMA pieces of V_{kt+1} and K_{kt+2} go out in its first 16 slots (one per odd slot):
+        // stamps (variant 12): issued in block B, the tile-start wait for them cost ~1,100 cycles per tile, issued
+        // here ~770 (the rest is the barrier: waves with more mask work arrive later)
+        s_tile_m(std::integral_constant<int, KN>{}, sn, [&](auto MC) {
+          constexpr int m = decltype(MC)::value;
+          fa_slot(MC);
+          if constexpr (m < 16 && (m & 1)) {
+            constexpr int j = m >> 1;
+            if constexpr (j < PW)
+              __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
+            else
+              __builtin_amdgcn_global_load_lds((gbl_void*)(tbk + okk[j - PW]), (lds_void*)(dstk + (j - PW) * 1024), 16,
+                                               0, 0);
+          }
+        });
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh)
 #pragma unroll
@@ -481,7 +507,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             mfma_pv(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
           badd(std::integral_constant<int, sl>{});
           bvx(std::integral_constant<int, sl>{});
-          if constexpr (sl % 4 == 1) {
+          if constexpr (!MANUAL_A && sl % 4 == 1) {
             constexpr int j = sl / 4;
             if constexpr (j < PW)
               __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);

@@ -1215,12 +1215,11 @@ class ZeroOptimizer:
 
     def _pre_backward(self, u):
         self._fetch(u, "backward")
-        so = self.state_offload
+        # (no trace positions -- nothing partitioned, e.g. one rank -- : the offloaded optimizer states come back in
+        # step(), in one allocation once the activations are gone. Reloading them in the middle of a near-full
+        # backward measured slower at Llama-3-8B mb10 -- 12.3-13.1k vs 14.4-14.6k tok/s: allocator retries, and
+        # chunk-wise reloads fragmented the pool for the next forward, profiles/r5/mb10_*)
         traced = self.partitioned and self._fwd_trace and not self._recording
-        if so is not None and self.boundary and not traced:
-            # no trace positions (nothing partitioned, e.g. one rank): reload the offloaded optimizer states as the
-            # HBM the backward frees allows -- before this, a one-rank run reloaded them all inside step()
-            so.on_backward_position(None)
         if traced:
             t = self._fwd_trace
             try:

@@ -29,8 +29,8 @@ still runs per contiguous piece):
   waiting for a whole 10-30 GB state; at every forward unit ``on_forward_position()`` waits for just enough of the
   oldest chunks to drain to hold that unit's activations (the growth measured on the previous step) -- an allocation
   that found nothing free would otherwise make the allocator synchronize EVERY outstanding copy at once;
-* the backward reloads chunk by chunk as its freed HBM allows, and a chunk fits into a fragmented pool where a whole
-  tail (a contiguous 10+ GB block) does not.
+* the backward reloads the tails as soon as the HBM it has freed holds them -- in ONE allocation (sliced per chunk):
+  chunk-by-chunk reloads into the holes of a half-freed activation pool fragmented it for the next forward.
 
 Offload and reload run on SEPARATE copy streams: a reload issued while the post-step offload of other chunks is still
 draining does not queue behind it -- it waits only for its own chunk's offload.
@@ -238,12 +238,24 @@ class OptimizerStateOffload:
         cur = torch.cuda.current_stream() if self.cuda else None
         ready = None
         todo = chunks if chunks is not None else [(k, i) for k, i in self._pending() if keys is None or k in keys]
+        todo = [(k, i) for k, i in todo if self.tail[k][i] is None]
+        # ONE allocation for the chunks of this call, sliced per chunk: reloading chunk by chunk into the holes the
+        # backward frees scattered 1 GiB blocks among the activations, and the next forward found 40 GiB free but no
+        # 2 GiB in one piece (this allocator has no expandable segments on ROCm)
+        dts = {self.host[k].dtype for k, _ in todo}
+        arena = None
+        if self.cuda and len(dts) == 1 and len(todo) > 1:
+            arena = torch.empty(sum(self.bounds[i][1] - self.bounds[i][0] for _, i in todo), dtype=dts.pop(),
+                                device=self.z.device)
+        off = 0
         for k, i in todo:
-            if self.tail[k][i] is not None:
-                continue
             lo, hi = self.bounds[i]
             h = self.host[k][lo - self.a:hi - self.a]
-            buf = torch.empty(h.numel(), dtype=h.dtype, device=self.z.device)  # compute stream's allocator pool
+            if arena is not None:
+                buf = arena[off:off + h.numel()]
+                off += h.numel()
+            else:
+                buf = torch.empty(h.numel(), dtype=h.dtype, device=self.z.device)  # compute stream's allocator pool
             if self.cuda:
                 if ready is None:
                     ready = torch.cuda.Event()
@@ -305,20 +317,14 @@ class OptimizerStateOffload:
         if not self.cuda:
             self.reload()
             return
-        # no schedule: bring each chunk back as soon as the HBM the backward has freed holds it -- at the start of
-        # backward when everything fits, late (chunk by chunk) when the tails and the activations do not fit
-        # together; step() reloads whatever is left
+        # no schedule: bring the tails back as soon as the HBM the backward has freed holds all of them -- at the
+        # start of backward when everything fits, later when the tails and the activations do not fit together;
+        # step() reloads them if they never fit
         limit = int(self.mem_fraction * torch.cuda.get_device_properties(self.z.device).total_memory)
         alloc = torch.cuda.memory_allocated(self.z.device)
-        todo = []
-        for k, i in self._pending():
-            nb = self._chunk_bytes(k, i)
-            if alloc + nb > limit:
-                break
-            alloc += nb
-            todo.append((k, i))
-        if todo:
-            self.reload(chunks=todo)
+        pending = self._pending()
+        if pending and alloc + sum(self._chunk_bytes(k, i) for k, i in pending) <= limit:
+            self.reload(chunks=pending)  # all of it at once, in one allocation, as soon as it fits
 
     mem_fraction = 0.92
 
