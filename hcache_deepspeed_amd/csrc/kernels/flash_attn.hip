@@ -1417,7 +1417,7 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 }  // namespace
 
-int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 2, g_bwd_prio = 1, g_bwd_pipe = 0, g_dq_var = 0;
+int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 11, g_bwd_prio = 1, g_bwd_pipe = 0, g_dq_var = 0;
 
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
 // 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel);

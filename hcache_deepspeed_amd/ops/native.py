@@ -158,12 +158,19 @@ def load_kernels(build_if_missing=True):
         # FlashAttention backward with LDS reads pipelined two MFMAs ahead (csrc/kernels/flash_attn.hip PIPE; 2 = + uniform-
         # base LDS-DMA staging of full tiles: 3.80 vs 3.85 ms, profiles/r3/fa_bwd_pipe2_r3q.txt)
         lib.hds_attn_bwd_pipe(int(os.environ.get("HDS_ATTN_BWD_PIPE", "2")))
-        # FlashAttention forward variant (csrc/kernels/flash_attn.hip hds_attn_fwd_variant; 5 = software-pipelined)
-        lib.hds_attn_fwd_variant(int(os.environ.get("HDS_ATTN_FWD_VAR", "5")))
+        # FlashAttention forward variant (csrc/kernels/flash_attn.hip hds_attn_fwd_variant): 11 = one wave per SIMD,
+        # 64 rows per wave, hand-scheduled MFMA blocks (flash_attn_w64.hip; 1.074-1.077 ms vs 1.109-1.116 for the
+        # 8-wave software-pipelined variant 5 at the bench shape, profiles/r5/fa_fwd_variants_idle_tiles_r5w.log)
+        lib.hds_attn_fwd_variant(fwd_variant_default())
         # FlashAttention backward dQ kernel (hds_attn_bwd_dq_variant; 1 = one wave per SIMD, 64 rows per wave)
         lib.hds_attn_bwd_dq_variant(int(os.environ.get("HDS_ATTN_DQ_VAR", "0")))
         _klib = lib
         return _klib
+
+
+def fwd_variant_default():
+    """The FlashAttention forward variant the library is loaded with (``HDS_ATTN_FWD_VAR`` overrides)."""
+    return int(os.environ.get("HDS_ATTN_FWD_VAR", "11"))
 
 
 def kernels():

@@ -24,7 +24,7 @@ for _ in range(3):
     flash_attn(q, k, v, causal=True)
 torch.cuda.synchronize()
 lib.hds_attn_w64_stamps(out, 1)
-lib.hds_attn_fwd_variant(5)
+lib.hds_attn_fwd_variant(native.fwd_variant_default())
 waves, tiles = out[7], out[6]  # tiles summed per wave (each wave adds its workgroup's tile count)
 names = ["dma wait + barrier", "block A (S MFMAs + exp)", "P pack + mask", "block B (PV MFMAs + max)", "tail", "loop"]
 print(f"waves {waves}, tiles per wave {tiles / max(1, waves):.1f}")
