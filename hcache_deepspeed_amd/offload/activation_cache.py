@@ -326,8 +326,14 @@ class HostActivationCache:
         return bool(self._calibrating)
 
     def plan_budget(self):
-        """The budget the forward-side plans aim the turn-around peak at (see ``bwd_extra``)."""
-        return None if self.budget is None else self.budget - self.bwd_extra
+        """The budget the forward-side plans aim the turn-around peak at (see ``bwd_extra``). Until a planned step has
+        measured its own backward excess, the first plan also keeps the D2H copy window free: the calibration step
+        it is sized from ran with nothing in that window at the turn-around, and the first planned 32k x mb2 step
+        peaked 2.9 GiB over the budget without it (profiles/r5/plan_32768_mb2_r5full.json, ``step_peaks_gib``)."""
+        if self.budget is None:
+            return None
+        first = self._bwd_extra_planned is None
+        return self.budget - self.bwd_extra - (self.copy_window if first else 0)
 
     @contextlib.contextmanager
     def forward_context(self):
