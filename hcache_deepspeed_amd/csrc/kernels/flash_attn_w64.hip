@@ -377,16 +377,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         constexpr int mc = m - 1, g = mc >> 3, t = g >> 1, j = g & 1, qh = (mc >> 2) & 1, i = mc & 3;
         constexpr int r = 8 * j + 2 * i;
         const float ea = x[t][qh][r], eb = x[t][qh][r + 1];
-        rs[qh][0] += ea;
-        rs[qh][1] += eb;
         uint32_t wv;
         asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(wv) : "v"(ea), "v"(eb));
         pw[qh][g][i] = wv;
-        float r0 = rs[qh][0], r1 = rs[qh][1];
-        asm volatile("" : "+v"(r0), "+v"(r1));  // stay in this slot (see fa)
-        rs[qh][0] = r0;
-        rs[qh][1] = r1;
       }
+    };
+    // variant 11: the row sums of tile kt's exponentials run in block B (2 adds per P.V slot, its gaps have room:
+    // stamps put block A at ~2,100 issue-bound cycles against block B's ~1,450); x holds them until the tile ends
+    auto badd11 = [&](auto SC) {
+      constexpr int sl = decltype(SC)::value, qh = sl >> 4, t = (sl >> 3) & 1, r = (sl & 7) * 2;
+      float r0 = rs[qh][0] + x[t][qh][r], r1 = rs[qh][1] + x[t][qh][r + 1];
+      asm volatile("" : "+v"(r0), "+v"(r1));  // stay in this slot
+      rs[qh][0] = r0;
+      rs[qh][1] = r1;
     };
 
     stage(smem + 0, p.k, p.sk, dk, kt_begin);
@@ -505,7 +508,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             mfma_pv_fresh(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
           else
             mfma_pv(o[dt][qh], vf[st & 1][dt], pb[qh][st]);
-          badd(std::integral_constant<int, sl>{});
+          if constexpr (MANUAL_A)
+            badd11(std::integral_constant<int, sl>{});
+          else
+            badd(std::integral_constant<int, sl>{});
           bvx(std::integral_constant<int, sl>{});
           if constexpr (!MANUAL_A && sl % 4 == 1) {
             constexpr int j = sl / 4;
