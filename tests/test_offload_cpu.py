@@ -536,3 +536,21 @@ def test_blit_limit_detection_by_import_order(order, env, expect):
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stderr[-2000:]
     assert f"EARLY {expect}" in r.stdout, r.stdout
+
+
+def test_first_plan_keeps_the_copy_window_free():
+    """plan_budget: the budget minus the measured backward excess; until a PLANNED step has measured its own excess,
+    minus the D2H copy window too (the calibration step it is sized from had nothing in flight at the turn-around).
+    step_peaks_gib reports every finished step's peak."""
+    import torch
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache
+    GB = 1 << 30
+    c = HostActivationCache(torch.device("cpu"), gpu_budget_bytes=100 * GB, copy_window_bytes=3 * GB)
+    assert c.copy_window == 3 * GB
+    c.bwd_extra = 2 * GB
+    assert c.plan_budget() == 95 * GB  # first plan: budget - excess - window
+    c._bwd_extra_planned = 2 * GB
+    assert c.plan_budget() == 98 * GB  # a planned step measured its excess: the window margin goes
+    c.step_peak_history = [x * GB for x in (10, 50, 60)]
+    assert c.stats()["step_peaks_gib"] == [10.0, 50.0, 60.0]
+    assert HostActivationCache(torch.device("cpu")).plan_budget() is None
