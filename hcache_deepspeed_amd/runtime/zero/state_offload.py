@@ -142,6 +142,8 @@ class OptimizerStateOffload:
             return
         self.bytes = 0
         cur = torch.cuda.current_stream() if self.cuda else None
+        # retire drained entries (engines without per-unit forward hooks never call on_forward_position)
+        self._draining = collections.deque((e, nb) for e, nb in self._draining if not e.query())
         if self.cuda:
             self.stream.wait_stream(cur)
         keys = self._keys() if not self.split else list(self.host)
