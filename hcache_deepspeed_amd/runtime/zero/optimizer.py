@@ -1220,6 +1220,9 @@ class ZeroOptimizer:
         # backward measured slower at Llama-3-8B mb10 -- 12.3-13.1k vs 14.4-14.6k tok/s: allocator retries, and
         # chunk-wise reloads fragmented the pool for the next forward, profiles/r5/mb10_*)
         traced = self.partitioned and self._fwd_trace and not self._recording
+        so = self.state_offload
+        if so is not None and self.boundary and not traced and so.untraced_backward_reload:
+            so.on_backward_position(None)  # opt-in (HDS_STATE_RELOAD_IN_BWD=1): one bulk reload once it fits
         if traced:
             t = self._fwd_trace
             try:

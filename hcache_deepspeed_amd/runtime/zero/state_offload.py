@@ -36,6 +36,7 @@ Offload and reload run on SEPARATE copy streams: a reload issued while the post-
 draining does not queue behind it -- it waits only for its own chunk's offload.
 """
 import collections
+import os
 
 import torch
 
@@ -328,7 +329,10 @@ class OptimizerStateOffload:
         if pending and alloc + sum(self._chunk_bytes(k, i) for k, i in pending) <= limit:
             self.reload(chunks=pending)  # all of it at once, in one allocation, as soon as it fits
 
-    mem_fraction = 0.92
+    # HBM fraction the memory-driven reload may fill (HDS_STATE_RELOAD_FRACTION) and, without trace positions (one
+    # rank), whether the backward reloads at all before step() (HDS_STATE_RELOAD_IN_BWD)
+    mem_fraction = float(os.environ.get("HDS_STATE_RELOAD_FRACTION", "0.92"))
+    untraced_backward_reload = os.environ.get("HDS_STATE_RELOAD_IN_BWD", "0") == "1"
 
     def stats(self):
         return {"state_bytes": self.bytes, "offloads": self.n_offloads, "reloads": self.n_reloads,

@@ -1,7 +1,8 @@
 """FPDT attention (parallel/fpdt.py: chunked causal attention, every chunk's q / k / v / o / lse parked in pinned host
 memory between forward and backward, prefetched back chunk by chunk) against the plain fused-QKV attention on one
 MI355X at Llama-3-8B attention width (H 4096, 32 / 8 heads, D 128): time of one forward + backward of the layer
-core (qkv projection, RoPE, attention) and the peak HBM it adds on top of its inputs. One JSON line per config.
+core (qkv projection, RoPE, attention), the HBM it holds between forward and backward (what a training step keeps
+per layer) and its transient peak. One JSON line per config.
 
 Usage: python tools/bench_fpdt.py [S,...] [chunks]"""
 import json
@@ -32,11 +33,15 @@ def run(kind, S, chunks):
     cos, sin = rope_tables(S, D, device=dev)
     g = torch.randn(S, NQ * D, device=dev, dtype=torch.bfloat16)
 
+    held = [0]
+
     def step():
+        a0 = torch.cuda.memory_allocated()
         if kind == "plain":
             y = plain(x, w, cos, sin, S)
         else:
             y = fpdt_attention(x, w, None, cos, sin, NQ, NKV, D, None, 1, chunks, offload=True)
+        held[0] = torch.cuda.memory_allocated() - a0 - y.numel() * y.element_size()  # saved for backward
         torch.autograd.grad(y, (x, w), g)
 
     step()
@@ -52,6 +57,7 @@ def run(kind, S, chunks):
     flops = 4 * NQ * S * S * D / 2 * 3.5 + 3 * 2 * S * H * (NQ + 2 * NKV) * D  # causal attn fwd+bwd (2.5x) + proj
     print(json.dumps({"kind": kind, "seq": S, "chunks": chunks if kind == "fpdt" else None,
                       "ms_fwd_bwd": round(dt * 1e3, 1), "TFLOPs": round(flops / dt / 1e12, 1),
+                      "saved_for_backward_gib": round(held[0] / 2**30, 2),
                       "peak_extra_gib": round((torch.cuda.max_memory_allocated() - base) / 2**30, 2)}), flush=True)
 
 
