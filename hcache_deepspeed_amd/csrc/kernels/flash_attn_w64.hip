@@ -48,6 +48,10 @@ __device__ __forceinline__ float xor32_max(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+__device__ __forceinline__ float xor32_max_raw(float x) {  // no NaN canonicalisation (the operands are finite)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return max3_raw(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[1]));
+}
 __device__ __forceinline__ float xor32_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -310,12 +314,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           move_any = false;
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            const float tmax = xor32_max(fmaxf(tm[q][0], tm[q][1])) * c;
+            // branch-free (this runs between two P.V MFMAs): scores are finite after the mask (no -inf), so the
+            // new max is finite, exp2(m - mnew) is 0 for the first tile's m = -inf and exactly 1 when m did not move
+            const float tmax = xor32_max_raw(max3_raw(tm[q][0], tm[q][1], tm[q][1])) * c;
             const bool move = !__all(tmax <= m[q] + kDeferThr);
-            const float mnew = move ? fmaxf(m[q], tmax) : m[q];
-            alpha[q] = move ? ((m[q] == -INFINITY) ? 0.f : fast_exp2(m[q] - mnew)) : 1.f;
+            const float mnew = move ? max3_raw(m[q], tmax, tmax) : m[q];
+            alpha[q] = fast_exp2(m[q] - mnew);
             m[q] = mnew;
-            muse[q] = (mnew == -INFINITY) ? 0.f : mnew;
+            muse[q] = mnew;
             move_any |= move;
           }
         }
