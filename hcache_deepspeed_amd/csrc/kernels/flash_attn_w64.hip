@@ -76,7 +76,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   static_assert(D == 128, "one-wave-per-SIMD forward: head_dim 128");
   constexpr bool REB = MODE >= 1;     // softmax VALU split over both MFMA blocks (variant 10)
   constexpr bool MANUAL_A = MODE >= 2;  // block A as asm MFMAs reading Q from the accumulator file (variant 11)
-  constexpr bool STAMPS = MODE == 3;    // variant 12 = 11 + per-segment cycle stamps (hds_attn_w64_stamps)
+  constexpr bool STAMPS = MODE >= 3;    // variant 12 = 11 + per-segment cycle stamps (hds_attn_w64_stamps)
+  // timing-only diagnostics (wrong results, never a default): 13 = 12 with v_mul in place of v_exp_f32 in block A,
+  // 14 = 12 with the LDS-DMA pieces issued in block B instead of block A
+  constexpr bool DIAG_NOEXP = MODE == 4, DIAG_DMA_B = MODE == 5;
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   auto stamp = [&](auto SEG) {
     if constexpr (STAMPS) {
@@ -374,7 +377,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       constexpr int m = decltype(MC)::value;
       if constexpr (m < 32) {
         constexpr int g = m >> 3, t = g >> 1, j = g & 1, qh = (m >> 2) & 1, i = m & 3, r = 8 * j + 2 * i;
-        float ea = fast_exp2(x[t][qh][r]), eb = fast_exp2(x[t][qh][r + 1]);
+        float ea, eb;
+        if constexpr (DIAG_NOEXP) {
+          ea = x[t][qh][r] * 0.5f;
+          eb = x[t][qh][r + 1] * 0.5f;
+        } else {
+          ea = fast_exp2(x[t][qh][r]);
+          eb = fast_exp2(x[t][qh][r + 1]);
+        }
         asm volatile("" : "+v"(ea), "+v"(eb));  // issued in this slot
         x[t][qh][r] = ea;
         x[t][qh][r + 1] = eb;
@@ -470,7 +480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         s_tile_m(std::integral_constant<int, KN>{}, sn, [&](auto MC) {
           constexpr int m = decltype(MC)::value;
           fa_slot(MC);
-          if constexpr (m < 16 && (m & 1)) {
+          if constexpr (!DIAG_DMA_B && m < 16 && (m & 1)) {
             constexpr int j = m >> 1;
             if constexpr (j < PW)
               __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
@@ -519,7 +529,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           else
             badd(std::integral_constant<int, sl>{});
           bvx(std::integral_constant<int, sl>{});
-          if constexpr (!MANUAL_A && sl % 4 == 1) {
+          if constexpr ((!MANUAL_A || DIAG_DMA_B) && sl % 4 == 1) {
             constexpr int j = sl / 4;
             if constexpr (j < PW)
               __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
@@ -740,7 +750,9 @@ int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, 
     case 0: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 0>), grid, dim3(256), 0, st, p); break;
     case 1: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 1>), grid, dim3(256), 0, st, p); break;
     case 2: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 2>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 3>), grid, dim3(256), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 3>), grid, dim3(256), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 4>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 5>), grid, dim3(256), 0, st, p); break;
   }
   return hipGetLastError();
 }

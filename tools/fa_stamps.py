@@ -15,7 +15,8 @@ q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
 k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
 v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
 out = (ctypes.c_ulonglong * 8)()
-lib.hds_attn_fwd_variant(12)
+VAR = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+lib.hds_attn_fwd_variant(VAR)
 for _ in range(2):
     flash_attn(q, k, v, causal=True)
 torch.cuda.synchronize()
@@ -27,7 +28,7 @@ lib.hds_attn_w64_stamps(out, 1)
 lib.hds_attn_fwd_variant(native.fwd_variant_default())
 waves, tiles = out[7], out[6]  # tiles summed per wave (each wave adds its workgroup's tile count)
 names = ["dma wait + barrier", "block A (S MFMAs + exp)", "P pack + mask", "block B (PV MFMAs + max)", "tail", "loop"]
-print(f"waves {waves}, tiles per wave {tiles / max(1, waves):.1f}")
+print(f"variant {VAR}: waves {waves}, tiles per wave {tiles / max(1, waves):.1f}")
 for i, n in enumerate(names):
     print(f"{n:28s} {out[i] / max(1, tiles):9.0f} cycles per tile")
 print(f"{'MFMA floor (64 x 32)':28s} {2048:9d}")
