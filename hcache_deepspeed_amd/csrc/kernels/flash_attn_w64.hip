@@ -65,7 +65,7 @@ __device__ __forceinline__ uint64_t memtime_stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-__device__ unsigned long long g_w64_stamps[8];  // segment cycles summed over waves, tiles, waves
+__device__ unsigned long long g_w64_stamps[4][8];  // per wave index: segment cycles, tiles, waves (summed)
 constexpr float kMaskPen = 1048576.f;  // 2^20, times the -1 of a masked score (see mask_tile)
 __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
 
@@ -473,6 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // block A runs on the last tile too (S of a stale K buffer, discarded below): a branch around it would let the
       // optimizer hoist the exponentials, which both arms need, out of the MFMA block they are meant to fill
       const float m_keep[2] = {m[0], m[1]};
+      bf16x8 vf[2][DT];  // V^T fragments of block B (variant 11 loads the first group in block A's last slots)
       if constexpr (MANUAL_A) {
         // block A; the 8 LDS-DMA pieces of V_{kt+1} and K_{kt+2} go out in its first 16 slots (one per odd slot):
         // stamps (variant 12): issued in block B, the tile-start wait for them cost ~1,100 cycles per tile, issued
@@ -480,6 +481,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         s_tile_m(std::integral_constant<int, KN>{}, sn, [&](auto MC) {
           constexpr int m = decltype(MC)::value;
           fa_slot(MC);
+          if constexpr (m >= 28 && m < 32) {  // block B's first V^T fragments, after block A's last K wait (slot 24):
+            constexpr int dt = m - 28;          // block B opens with them landed instead of an LDS round trip
+            vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
+          }
           if constexpr (!DIAG_DMA_B && m < 16 && (m & 1)) {
             constexpr int j = m >> 1;
             if constexpr (j < PW)
@@ -502,11 +507,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       stamp(std::integral_constant<int, 2>{});  // seg 2: P pack + mask
       // ---- block B: O += V_kt^T.P_kt, 32 asm MFMAs, each followed by its VALU slot (sched_barrier-fenced: hipcc
       // cannot see an asm MFMA, so the interleave is the source order) ----
-      bf16x8 vf[2][DT];
-      static_for<DT>([&](auto DC) {
-        constexpr int dt = decltype(DC)::value;
-        vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
-      });
+      if constexpr (!MANUAL_A) {
+        static_for<DT>([&](auto DC) {
+          constexpr int dt = decltype(DC)::value;
+          vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
+        });
+      }
       static_for<4>([&](auto STC) {
         constexpr int st = decltype(STC)::value;
         if constexpr (st + 1 < 4) {
@@ -578,9 +584,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       st_acc[5] = st_prev - st_t0;  // the whole loop
       if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) atomicAdd(&g_w64_stamps[k], (unsigned long long)st_acc[k]);
-        atomicAdd(&g_w64_stamps[6], (unsigned long long)(kt_end - kt_begin));
-        atomicAdd(&g_w64_stamps[7], 1ull);
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_w64_stamps[w][k], (unsigned long long)st_acc[k]);
+        atomicAdd(&g_w64_stamps[w][6], (unsigned long long)(kt_end - kt_begin));
+        atomicAdd(&g_w64_stamps[w][7], 1ull);
       }
     }
   } else {
@@ -757,12 +763,12 @@ int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, 
   return hipGetLastError();
 }
 
-// variant 12's stamps: out[0..4] cycles per segment (DMA wait + barrier, block A, mask, block B, tail), out[5] the whole
-// loop, summed over waves; out[6] tiles summed over waves' workgroups; out[7] waves. reset != 0 zeroes them after.
+// variant 12's stamps, out[32] = 4 wave indices x 8: [0..4] cycles per segment (DMA wait + barrier, block A, mask,
+// block B, tail), [5] the whole loop, [6] tiles, [7] waves -- summed over the workgroups. reset != 0 zeroes them after.
 HDS_EXPORT int hds_attn_w64_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w64_stamps), sizeof(g_w64_stamps));
   if (e == hipSuccess && reset) {
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long z[32] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_w64_stamps), z, sizeof(z));
   }
   return e;

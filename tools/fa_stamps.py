@@ -14,7 +14,7 @@ B, S, Hq, Hkv, D = 7, 4096, 32, 8, 128
 q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
 k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
 v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
-out = (ctypes.c_ulonglong * 8)()
+out = (ctypes.c_ulonglong * 32)()
 VAR = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 lib.hds_attn_fwd_variant(VAR)
 for _ in range(2):
@@ -26,9 +26,11 @@ for _ in range(3):
 torch.cuda.synchronize()
 lib.hds_attn_w64_stamps(out, 1)
 lib.hds_attn_fwd_variant(native.fwd_variant_default())
-waves, tiles = out[7], out[6]  # tiles summed per wave (each wave adds its workgroup's tile count)
 names = ["dma wait + barrier", "block A (S MFMAs + exp)", "P pack + mask", "block B (PV MFMAs + max)", "tail", "loop"]
-print(f"variant {VAR}: waves {waves}, tiles per wave {tiles / max(1, waves):.1f}")
+tot = [sum(out[8 * w + i] for w in range(4)) for i in range(8)]
+print(f"variant {VAR}: waves {tot[7]}, tiles per wave {tot[6] / max(1, tot[7]):.1f}; cycles per tile (all waves, then "
+      f"wave 0 / 1 / 2 / 3: waves whose rows precede the last tiles idle there)")
 for i, n in enumerate(names):
-    print(f"{n:28s} {out[i] / max(1, tiles):9.0f} cycles per tile")
-print(f"{'MFMA floor (64 x 32)':28s} {2048:9d}")
+    per = [out[8 * w + i] / max(1, out[8 * w + 6]) for w in range(4)]
+    print(f"{n:28s} {tot[i] / max(1, tot[6]):7.0f}   " + " / ".join(f"{x:5.0f}" for x in per))
+print(f"{'MFMA floor (64 x 32)':28s} {2048:7d}")
