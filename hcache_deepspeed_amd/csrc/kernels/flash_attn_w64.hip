@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // block A runs on the last tile too (S of a stale K buffer, discarded below): a branch around it would let the
       // optimizer hoist the exponentials, which both arms need, out of the MFMA block they are meant to fill
       const float m_keep[2] = {m[0], m[1]};
-      bf16x8 vf[2][DT];  // V^T fragments of block B (variant 11 loads the first group in block A's last slots)
+      bf16x8 vf[2][DT];  // V^T fragments of block B
       if constexpr (MANUAL_A) {
         // block A; the 8 LDS-DMA pieces of V_{kt+1} and K_{kt+2} go out in its first 16 slots (one per odd slot):
         // stamps (variant 12): issued in block B, the tile-start wait for them cost ~1,100 cycles per tile, issued
@@ -481,10 +481,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         s_tile_m(std::integral_constant<int, KN>{}, sn, [&](auto MC) {
           constexpr int m = decltype(MC)::value;
           fa_slot(MC);
-          if constexpr (m >= 28 && m < 32) {  // block B's first V^T fragments, after block A's last K wait (slot 24):
-            constexpr int dt = m - 28;          // block B opens with them landed instead of an LDS round trip
-            vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
-          }
           if constexpr (!DIAG_DMA_B && m < 16 && (m & 1)) {
             constexpr int j = m >> 1;
             if constexpr (j < PW)
@@ -507,12 +503,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       stamp(std::integral_constant<int, 2>{});  // seg 2: P pack + mask
       // ---- block B: O += V_kt^T.P_kt, 32 asm MFMAs, each followed by its VALU slot (sched_barrier-fenced: hipcc
       // cannot see an asm MFMA, so the interleave is the source order) ----
-      if constexpr (!MANUAL_A) {
-        static_for<DT>([&](auto DC) {
-          constexpr int dt = decltype(DC)::value;
-          vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
-        });
-      }
+      // (reading this first group in block A's last slots, or streaming K two tiles ahead through 3-slot rings so
+      // block B could read the next block A's first K groups, both measured slower: 4,524-4,559 cycles per tile
+      // against 4,364, profiles/r5/fa_fwd_stamps_*_r5ad/ae.txt)
+      static_for<DT>([&](auto DC) {
+        constexpr int dt = decltype(DC)::value;
+        vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
+      });
       static_for<4>([&](auto STC) {
         constexpr int st = decltype(STC)::value;
         if constexpr (st + 1 < 4) {
