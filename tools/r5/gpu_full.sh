@@ -2,7 +2,7 @@
 # 32k x mb2 plan under the default budget (timed-step peak)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-D=gpurun_out/${RUN:-r5full}
+D=gpurun_out/${RUN:-r5final}
 mkdir -p $D
 timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > $D/gpu_suite.log 2>&1
 rc=$?; echo "suite rc=$rc" >> $D/status.txt
