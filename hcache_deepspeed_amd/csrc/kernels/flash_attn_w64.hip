@@ -1,33 +1,26 @@
-// FlashAttention forward, variant 9: one wave per SIMD, 64 query rows per wave (see the kernel comment). Its own
-// translation unit so that it can be built with its own code-generation options (ops/build.py FILE_FLAGS).
+// FlashAttention forward, one wave per SIMD, 64 query rows per wave: variants 9-15 of hds_attn_fwd_variant, 11 the
+// library default. Its own translation unit so that it builds with its own code-generation options (ops/build.py
+// FILE_FLAGS: -amdgpu-mfma-vgpr-form, no SLP vectorisation).
 #include "flash_attn_shared.h"
 
 namespace {
 
 // =====================================================================================
-// forward variant 9: one wave per SIMD, 64 query rows per wave, hand-owned accumulator file
+// forward, one wave per SIMD, 64 query rows per wave, hand-owned accumulator file
 // =====================================================================================
-// The guide's 1.25 PF/s structure (cdna_hip_programming.md §B "4-wave, one-wave-per-SIMD"): 4 waves x 64 query rows
-// = 256 rows per workgroup, so every K/V tile read from LDS feeds TWICE the MFMAs of the 8-wave kernel and each SIMD
-// runs one instruction stream (no partner wave contending for the matrix pipe or the VALU issue port). Per tile and
-// wave: 32 S MFMAs (2 key halves x 2 query halves x 8 k-steps) + 32 P.V MFMAs = 64 v_mfma_f32_32x32x16_bf16.
-// Register plan (512 per lane): O^T (4 column blocks x 2 query halves x 16) = 128 and the Q fragments (2 x 8 x 4) = 64
-// live in the ACCUMULATOR file through inline-asm MFMAs ("+a" / "a" operands) -- round 4's builtin version let hipcc
-// put the S accumulators there too, so every score crossed v_accvgpr_read twice; here S, P and the K/V fragments are
-// the arch VGPRs. hipcc neither models nor pads an asm MFMA's hazards (guide §5.7 item 2), so: the last MFMA of every
-// S chain ends with the 12 wait states an 8-pass XDL result needs before a VALU reads it, the first P.V MFMA after the
-// bf16 P is written opens with s_nop 1, and the O read-back (rescale, epilogue) is preceded by a full drain.
-// The software pipeline is the one of attn_fwd_sp_kernel: S_{kt+1} beside exp(S_kt keys 0..31), P_kt.V_kt beside
-// exp(S_kt keys 32..63); deferred running max (T13); LDS-DMA K/V ring with K one tile further ahead than V.
-__device__ __forceinline__ void mfma_sq(f32x16& s, const bf16x8& k, const bf16x8& q) {  // S(v) += K(v) . Q^T(a)
-  s = mfma(k, q, s);
-}
-__device__ __forceinline__ void mfma_sq0(f32x16& s, const bf16x8& k, const bf16x8& q) {  // S(v) = K . Q^T
-  s = mfma(k, q, f32x16{});
-}
-__device__ __forceinline__ void mfma_sq_end(f32x16& s, const bf16x8& k, const bf16x8& q) {  // last of a chain + pad
-  s = mfma(k, q, s);
-}
+// The guide's one-wave-per-SIMD structure (cdna_hip_programming.md "4-wave, one-wave-per-SIMD"): 4 waves x 64 query
+// rows = 256 rows per workgroup, so every K/V fragment read from LDS feeds TWICE the MFMAs of the 8-wave kernel and
+// each SIMD runs one instruction stream. Per tile and wave: 32 S MFMAs (2 key halves x 2 query halves x 8 k-steps) +
+// 32 P.V MFMAs = 64 v_mfma_f32_32x32x16_bf16 (the 2,048-cycle floor of a tile).
+// Register plan (512 per lane): O^T (4 column blocks x 2 query halves x 16) = 128 in the ACCUMULATOR file through
+// inline-asm MFMAs ("+a"); variant 11 also keeps Q (64) there as the S MFMAs' "a" operand; S, P and the K/V fragments
+// are arch VGPRs. hipcc neither models nor pads an asm MFMA's hazards (guide §5.7 item 2), so: block A ends with the
+// wait states an XDL result needs before a VALU reads it, the first P.V MFMA after the bf16 P is written opens with
+// s_nop 1, and the O read-back (rescale, epilogue) is preceded by a full drain.
+//   variant 9  (MODE 0): S_{kt+1} beside the whole softmax of tile kt, P.V alone (hipcc-scheduled builtins for S)
+//   variant 10 (MODE 1): the softmax split over both MFMA blocks (below), builtin S MFMAs
+//   variant 11 (MODE 2): 10 with block A hand-scheduled: asm S MFMAs on Q in AGPRs, each followed by its VALU slot
+//   variants 12-14: 11 + s_memtime stamps per segment (12), timing-only diagnostics (13, 14)
 __device__ __forceinline__ void mfma_pv(f32x16& o, const bf16x8& v, const bf16x8& pb) {  // O^T(a) += V^T . P^T
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(pb));
 }
