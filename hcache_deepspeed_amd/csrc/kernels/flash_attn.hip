@@ -1425,7 +1425,7 @@ int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 11, g_bwd_prio = 1, g_
 // 8 = 5 with 4-wave workgroups (two per CU); 9 = one wave per SIMD, 64 rows per wave (attn_fwd_w64_kernel);
 // 10 = 9 with the softmax VALU split over both MFMA blocks; 11 = 10 with block A hand-scheduled (asm S MFMAs, Q in AGPRs); 12 = 11 + cycle stamps (diagnostic); 13 / 14 = timing-only diagnostics of 12 (no exp / DMA in block B)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 14) return hipErrorInvalidValue;
+  if (var < 0 || var > 17) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1481,6 +1481,9 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
           case 12: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 3, st);
           case 13: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 4, st);
           case 14: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 5, st);
+          case 15: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 6, st);
+          case 16: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 7, st);
+          case 17: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 8, st);
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;

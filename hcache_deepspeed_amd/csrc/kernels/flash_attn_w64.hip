@@ -20,7 +20,7 @@ namespace {
 //   variant 9  (MODE 0): S_{kt+1} beside the whole softmax of tile kt, P.V alone (hipcc-scheduled builtins for S)
 //   variant 10 (MODE 1): the softmax split over both MFMA blocks (below), builtin S MFMAs
 //   variant 11 (MODE 2): 10 with block A hand-scheduled: asm S MFMAs on Q in AGPRs, each followed by its VALU slot
-//   variants 12-14: 11 + s_memtime stamps per segment (12), timing-only diagnostics (13, 14)
+//   variants 12-17: 11 + s_memtime stamps per segment (12), timing-only diagnostics (13-17)
 __device__ __forceinline__ void mfma_pv(f32x16& o, const bf16x8& v, const bf16x8& pb) {  // O^T(a) += V^T . P^T
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(pb));
 }
@@ -72,7 +72,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr bool STAMPS = MODE >= 3;    // variant 12 = 11 + per-segment cycle stamps (hds_attn_w64_stamps)
   // timing-only diagnostics (wrong results, never a default): 13 = 12 with v_mul in place of v_exp_f32 in block A,
   // 14 = 12 with the LDS-DMA pieces issued in block B instead of block A
-  constexpr bool DIAG_NOEXP = MODE == 4, DIAG_DMA_B = MODE == 5;
+  constexpr bool DIAG_NOEXP = MODE == 4, DIAG_NOVALU_A = MODE == 6, DIAG_NOAGPR = MODE == 7;
+  constexpr bool DIAG_SACC = MODE == 8;  // 17: S MFMAs accumulate into the accumulator file (garbage O: timing only)
+  constexpr bool DIAG_DMA_B = MODE == 5 || MODE == 6;  // 15: block A without its VALU slots; 16: S MFMAs on VGPRs only
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   auto stamp = [&](auto SEG) {
     if constexpr (STAMPS) {
@@ -243,9 +245,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       static_for<8>([&](auto IC) {
         constexpr int ii = decltype(IC)::value, qh = ii >> 2, i = ii & 3, m = 8 * g + ii;
         if constexpr (j == 0 && i == 0)
-          mfma_s_first(sn[t][qh], kr[b][i], qf[qh][4 * j + i]);
+          if constexpr (DIAG_SACC)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(o[2 * t + qh][0]) : "v"(kr[b][i]), "a"(qf[qh][4 * j + i]));
+          else if constexpr (DIAG_NOAGPR)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(sn[t][qh]) : "v"(kr[b][i]), "v"(kr[b][i]));
+          else
+            mfma_s_first(sn[t][qh], kr[b][i], qf[qh][4 * j + i]);
         else
-          mfma_s(sn[t][qh], kr[b][i], qf[qh][4 * j + i]);
+          if constexpr (DIAG_SACC)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o[2 * t + qh][0]) : "v"(kr[b][i]), "a"(qf[qh][4 * j + i]));
+          else if constexpr (DIAG_NOAGPR)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sn[t][qh]) : "v"(kr[b][i]), "v"(kr[b][i]));
+          else
+            mfma_s(sn[t][qh], kr[b][i], qf[qh][4 * j + i]);
         SLOT(std::integral_constant<int, m>{});
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -473,7 +485,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // here ~770 (the rest is the barrier: waves with more mask work arrive later)
         s_tile_m(std::integral_constant<int, KN>{}, sn, [&](auto MC) {
           constexpr int m = decltype(MC)::value;
-          fa_slot(MC);
+          if constexpr (!DIAG_NOVALU_A) fa_slot(MC);
           if constexpr (!DIAG_DMA_B && m < 16 && (m & 1)) {
             constexpr int j = m >> 1;
             if constexpr (j < PW)
@@ -748,7 +760,10 @@ int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, 
     case 2: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 2>), grid, dim3(256), 0, st, p); break;
     case 3: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 3>), grid, dim3(256), 0, st, p); break;
     case 4: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 4>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 5>), grid, dim3(256), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 5>), grid, dim3(256), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 6>), grid, dim3(256), 0, st, p); break;
+    case 7: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 7>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 8>), grid, dim3(256), 0, st, p); break;
   }
   return hipGetLastError();
 }
