@@ -243,7 +243,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         lds_wait_tie<0>(kr[b][0], kr[b][1], kr[b][2], kr[b][3]);
       }
       static_for<8>([&](auto IC) {
-        constexpr int ii = decltype(IC)::value, qh = ii >> 2, i = ii & 3, m = 8 * g + ii;
+        // the two query halves alternate (qh 0, 1 on K fragment i, then i + 1): consecutive MFMAs accumulate into
+        // different S tiles; each chain keeps its k order
+        constexpr int ii = decltype(IC)::value, qh = ii & 1, i = ii >> 1, m = 8 * g + ii;
         if constexpr (j == 0 && i == 0)
           if constexpr (DIAG_SACC)
             asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(o[2 * t + qh][0]) : "v"(kr[b][i]), "a"(qf[qh][4 * j + i]));
