@@ -60,6 +60,23 @@ __device__ __forceinline__ uint64_t memtime_stamp() {
 }
 __device__ unsigned long long g_w64_stamps[4][8];  // per wave index: segment cycles, tiles, waves (summed)
 constexpr float kMaskPen = 1048576.f;  // 2^20, times the -1 of a masked score (see mask_tile)
+// one LDS-DMA piece of K or V tile through a buffer descriptor built from plain scalars (the descriptor type does not
+// exist in the host pass, so no lambda may hold one): base = the tile's first row of this kv head, records = the bytes
+// up to the end of the tile's last row inside the sequence -- the range check zero-fills the pieces of rows past it
+struct TileSrc {
+  const char* base;
+  int bytes;
+};
+template <int D>
+__device__ __forceinline__ TileSrc tile_src(const bf16* base, int64_t stride, int start, int kt, int hk, int len) {
+  const int rows = min(BN, len - kt * BN);
+  return {(const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D),
+          (int)(((int64_t)(rows - 1) * stride + D) * 2)};
+}
+__device__ __forceinline__ void dma_piece(const TileSrc& t, void* lds, int32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)t.base, (short)0, t.bytes, 0x00020000),
+                                           (lds_void*)lds, 16, off, 0, 0, 0);
+}
 __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
 
 template <int D, int MODE>
@@ -449,19 +466,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // vector-issue slack), not in a burst here: a piece costs its wave ~60-185 issue cycles in a burst. Past the
       // sequence end a piece re-reads the last tile into a buffer nobody reads (no branch in the MFMA block).
       const int ktv = min(kt + 1, kt_end - 1), ktk = min(kt + 2, kt_end - 1);
-      const char* tbv = (const char*)(p.v + (int64_t)(start + ktv * BN) * p.sv + (int64_t)hk * D);
-      const char* tbk = (const char*)(p.k + (int64_t)(start + ktk * BN) * p.sk + (int64_t)hk * D);
-      int32_t ovv[PW], okk[PW];
-      {
-        const bool fv = ktv * BN + BN <= len, fk = ktk * BN + BN <= len;
-#pragma unroll
-        for (int i = 0; i < PW; ++i) {
-          const int row = 4 * (w * PW + i) + (lane >> 4), ch = 8 * ((lane & 15) ^ swz(row));
-          const int rv = min(ktv * BN + row, len - 1) - ktv * BN, rk = min(ktk * BN + row, len - 1) - ktk * BN;
-          ovv[i] = fv ? dv[i] : (int32_t)(((int64_t)rv * p.sv + ch) * 2);
-          okk[i] = fk ? dk[i] : (int32_t)(((int64_t)rk * p.sk + ch) * 2);
-        }
-      }
+      // the pieces go through buffer descriptors of the two tiles (scalar base + byte count up to the end of the
+      // tile's last row in the sequence): every lane keeps its constant offset dv / dk, and the rows past the end of
+      // a partial last tile fail the descriptor's range check and land as zeros (masked keys, zero V rows) -- no
+      // per-tile clamp of 8 per-lane offsets, each behind its own branch, between the barrier and block A
+      const TileSrc rsv = tile_src<D>(p.v, p.sv, start, ktv, hk, len), rsk = tile_src<D>(p.k, p.sk, start, ktk, hk, len);
       char* const dstv = smem + 2 * TL + (buf ^ 1) * TL + w * PW * 1024;
       char* const dstk = smem + buf * TL + w * PW * 1024;
       if (kt >= kt_end_w) {  // idle tile: its keys all follow this wave's rows (causal); the wave still stages its
@@ -469,8 +478,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // work on the diagonal tiles set the pace at every barrier)
 #pragma unroll
         for (int j = 0; j < PW; ++j) {
-          __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
-          __builtin_amdgcn_global_load_lds((gbl_void*)(tbk + okk[j]), (lds_void*)(dstk + j * 1024), 16, 0, 0);
+          dma_piece(rsv, dstv + j * 1024, dv[j]);
+          dma_piece(rsk, dstk + j * 1024, dk[j]);
         }
         return;
       }
@@ -491,10 +500,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           if constexpr (!DIAG_DMA_B && m < 16 && (m & 1)) {
             constexpr int j = m >> 1;
             if constexpr (j < PW)
-              __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
+              dma_piece(rsv, dstv + j * 1024, dv[j]);
             else
-              __builtin_amdgcn_global_load_lds((gbl_void*)(tbk + okk[j - PW]), (lds_void*)(dstk + (j - PW) * 1024), 16,
-                                               0, 0);
+              dma_piece(rsk, dstk + (j - PW) * 1024, dk[j - PW]);
           }
         });
 #pragma unroll
@@ -542,10 +550,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           if constexpr ((!MANUAL_A || DIAG_DMA_B) && sl % 4 == 1) {
             constexpr int j = sl / 4;
             if constexpr (j < PW)
-              __builtin_amdgcn_global_load_lds((gbl_void*)(tbv + ovv[j]), (lds_void*)(dstv + j * 1024), 16, 0, 0);
+              dma_piece(rsv, dstv + j * 1024, dv[j]);
             else
-              __builtin_amdgcn_global_load_lds((gbl_void*)(tbk + okk[j - PW]), (lds_void*)(dstk + (j - PW) * 1024), 16,
-                                               0, 0);
+              dma_piece(rsk, dstk + (j - PW) * 1024, dk[j - PW]);
           }
           __builtin_amdgcn_sched_barrier(0);
         });

@@ -101,6 +101,13 @@ def build_kernels(force=False, jobs=None, verbose=False, file_flags=None, out=No
     tmp = lib_path + ".tmp"
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
           f"-Wl,-rpath,{ROCM}/lib"])
+    # a kernel the host pass rejects silently (a device-only type held by a host-device lambda) leaves its launch
+    # stub undefined: the shared object still links and only fails at dlopen on the GPU box -- refuse it here
+    nm = subprocess.run(["nm", "-u", tmp], capture_output=True, text=True)
+    missing = [ln.split()[-1] for ln in nm.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        os.remove(tmp)
+        raise RuntimeError(f"kernel library leaves launch stubs undefined: {missing[:4]}")
     os.replace(tmp, lib_path)
     with open(lib_path + ".sha256", "w") as f:
         f.write(digest)
