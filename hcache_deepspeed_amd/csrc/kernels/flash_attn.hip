@@ -1417,7 +1417,7 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 }  // namespace
 
-int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 11, g_bwd_prio = 1, g_bwd_pipe = 0, g_dq_var = 0;
+int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 20, g_bwd_prio = 1, g_bwd_pipe = 0, g_dq_var = 0;
 
 // forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
 // 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel);
@@ -1425,7 +1425,7 @@ int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 11, g_bwd_prio = 1, g_
 // 8 = 5 with 4-wave workgroups (two per CU); 9 = one wave per SIMD, 64 rows per wave (attn_fwd_w64_kernel);
 // 10 = 9 with the softmax VALU split over both MFMA blocks; 11 = 10 with block A hand-scheduled (asm S MFMAs, Q in AGPRs); 12 = 11 + cycle stamps (diagnostic); 13 / 14 = timing-only diagnostics of 12 (no exp / DMA in block B)
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
-  if (var < 0 || var > 17) return hipErrorInvalidValue;
+  if (var < 0 || var > 21) return hipErrorInvalidValue;
   g_fwd_var = var;
   return 0;
 }
@@ -1484,6 +1484,10 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
           case 15: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 6, st);
           case 16: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 7, st);
           case 17: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 8, st);
+          case 18: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 9, st);
+          case 19: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 10, st);
+          case 20: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 11, st);
+          case 21: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 12, st);
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;

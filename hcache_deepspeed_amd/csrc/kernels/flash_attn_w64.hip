@@ -1,4 +1,4 @@
-// FlashAttention forward, one wave per SIMD, 64 query rows per wave: variants 9-15 of hds_attn_fwd_variant, 11 the
+// FlashAttention forward, one wave per SIMD, 64 query rows per wave: variants 9-21 of hds_attn_fwd_variant, 20 the
 // library default. Its own translation unit so that it builds with its own code-generation options (ops/build.py
 // FILE_FLAGS: -amdgpu-mfma-vgpr-form, no SLP vectorisation).
 #include "flash_attn_shared.h"
@@ -21,6 +21,8 @@ namespace {
 //   variant 10 (MODE 1): the softmax split over both MFMA blocks (below), builtin S MFMAs
 //   variant 11 (MODE 2): 10 with block A hand-scheduled: asm S MFMAs on Q in AGPRs, each followed by its VALU slot
 //   variants 12-17: 11 + s_memtime stamps per segment (12), timing-only diagnostics (13-17)
+//   variant 18 (MODE 9): 11 with the LDS-DMA pieces spread over all of block A; 20 (MODE 11, the default): 18 with the
+//   first P.V group's V fragments read in block A's last slots; 19 / 21: their stamps
 __device__ __forceinline__ void mfma_pv(f32x16& o, const bf16x8& v, const bf16x8& pb) {  // O^T(a) += V^T . P^T
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(pb));
 }
@@ -86,7 +88,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   static_assert(D == 128, "one-wave-per-SIMD forward: head_dim 128");
   constexpr bool REB = MODE >= 1;     // softmax VALU split over both MFMA blocks (variant 10)
   constexpr bool MANUAL_A = MODE >= 2;  // block A as asm MFMAs reading Q from the accumulator file (variant 11)
-  constexpr bool STAMPS = MODE >= 3;    // variant 12 = 11 + per-segment cycle stamps (hds_attn_w64_stamps)
+  // variant 18 (MODE 9) = 11 with the 8 LDS-DMA pieces spread over all of block A (one per 4 slots); 20 (MODE 11) = 18
+  // with the first P.V group's V fragments read in block A's last 8 slots (after its last K wait); 19 / 21 = their stamps
+  constexpr bool SPREAD = MODE >= 9, VPRE = MODE >= 11;
+  constexpr bool STAMPS = (MODE >= 3 && MODE <= 8) || MODE == 10 || MODE == 12;  // 12 = 11 + per-segment stamps
   // timing-only diagnostics (wrong results, never a default): 13 = 12 with v_mul in place of v_exp_f32 in block A,
   // 14 = 12 with the LDS-DMA pieces issued in block B instead of block A
   constexpr bool DIAG_NOEXP = MODE == 4, DIAG_NOVALU_A = MODE == 6, DIAG_NOAGPR = MODE == 7;
@@ -497,8 +502,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         s_tile_m(std::integral_constant<int, KN>{}, sn, [&](auto MC) {
           constexpr int m = decltype(MC)::value;
           if constexpr (!DIAG_NOVALU_A) fa_slot(MC);
-          if constexpr (!DIAG_DMA_B && m < 16 && (m & 1)) {
-            constexpr int j = m >> 1;
+          if constexpr (VPRE && m >= 24 && m < 32 && (m & 1) == 0) {  // past block A's last K wait (before m 24)
+            constexpr int dt = (m - 24) >> 1;
+            vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
+          }
+          if constexpr (!DIAG_DMA_B && (SPREAD ? (m < 32 && (m & 3) == 1) : (m < 16 && (m & 1)))) {
+            constexpr int j = SPREAD ? m >> 2 : m >> 1;
             if constexpr (j < PW)
               dma_piece(rsv, dstv + j * 1024, dv[j]);
             else
@@ -521,10 +530,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // (reading this first group in block A's last slots, or streaming K two tiles ahead through 3-slot rings so
       // block B could read the next block A's first K groups, both measured slower: 4,524-4,559 cycles per tile
       // against 4,364, profiles/r5/fa_fwd_stamps_*_r5ad/ae.txt)
-      static_for<DT>([&](auto DC) {
-        constexpr int dt = decltype(DC)::value;
-        vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
-      });
+      if constexpr (!VPRE) {
+        static_for<DT>([&](auto DC) {
+          constexpr int dt = decltype(DC)::value;
+          vf[0][dt] = lds_tr8<VT>(av0[dt], av1[dt]);
+        });
+      }
       static_for<4>([&](auto STC) {
         constexpr int st = decltype(STC)::value;
         if constexpr (st + 1 < 4) {
@@ -772,12 +783,16 @@ int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, 
     case 5: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 5>), grid, dim3(256), 0, st, p); break;
     case 6: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 6>), grid, dim3(256), 0, st, p); break;
     case 7: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 7>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 8>), grid, dim3(256), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 8>), grid, dim3(256), 0, st, p); break;
+    case 9: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 9>), grid, dim3(256), 0, st, p); break;
+    case 10: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 10>), grid, dim3(256), 0, st, p); break;
+    case 11: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 11>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 12>), grid, dim3(256), 0, st, p); break;
   }
   return hipGetLastError();
 }
 
-// variant 12's stamps, out[32] = 4 wave indices x 8: [0..4] cycles per segment (DMA wait + barrier, block A, mask,
+// variant 12's (19's, 21's) stamps, out[32] = 4 wave indices x 8: [0..4] cycles per segment (DMA wait + barrier, block A, mask,
 // block B, tail), [5] the whole loop, [6] tiles, [7] waves -- summed over the workgroups. reset != 0 zeroes them after.
 HDS_EXPORT int hds_attn_w64_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w64_stamps), sizeof(g_w64_stamps));

@@ -170,7 +170,7 @@ def load_kernels(build_if_missing=True):
 
 def fwd_variant_default():
     """The FlashAttention forward variant the library is loaded with (``HDS_ATTN_FWD_VAR`` overrides)."""
-    return int(os.environ.get("HDS_ATTN_FWD_VAR", "11"))
+    return int(os.environ.get("HDS_ATTN_FWD_VAR", "20"))
 
 
 def kernels():

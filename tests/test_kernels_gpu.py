@@ -665,7 +665,7 @@ def test_decode_attention_matches_reference_gpu(D, H, Hkv, S):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10, 11, 18, 20])
 @pytest.mark.parametrize("case", ["causal", "full", "window", "varlen"])
 def test_flash_fwd_staggered_variant_gpu(case, variant):
     """Forward variants 4 (staggered wave groups) and 5 (software-pipelined softmax) against variant 2 and the fp32
