@@ -91,32 +91,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   // LDS layout: K tiles in slots 0..2 at [0, 48 KiB), V tiles at [48, 96 KiB) -- every LDS read is an immediate offset
   // (< 64 KiB) on one of two per-lane base registers
-  // LDS-DMA of tile kt into slot `slot`: per-lane byte offsets of this wave's PW pieces of K and of V (rows past the
-  // sequence end clamp to its last row), computed before the MFMA block that issues them
+  // K / V tile kt through buffer descriptors (flash_attn_shared.h tile_dma): every lane keeps its constant offsets
+  // dk / dv, and the rows of a partial last tile past the sequence end land as zeros (range check) instead of being
+  // clamped per lane and piece on every tile
   struct Dma {
-    const char* tk;
-    const char* tv;
-    int32_t ok[PW], ov[PW];
+    TileSrc k, v;
   };
   auto dma_prep = [&](int kt, Dma& d) {
-    d.tk = (const char*)(p.k + (int64_t)(start + kt * BN) * p.sk + (int64_t)hk * D);
-    d.tv = (const char*)(p.v + (int64_t)(start + kt * BN) * p.sv + (int64_t)hk * D);
-    const bool full = kt * BN + BN <= len;
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int row = 4 * (w * PW + i) + (lane >> 4), ch = 8 * ((lane & 15) ^ swz(row));
-      const int r = min(kt * BN + row, len - 1) - kt * BN;
-      d.ok[i] = full ? dk[i] : (int32_t)(((int64_t)r * p.sk + ch) * 2);
-      d.ov[i] = full ? dv[i] : (int32_t)(((int64_t)r * p.sv + ch) * 2);
-    }
+    d.k = tile_src<D>(p.k, p.sk, start, kt, hk, len);
+    d.v = tile_src<D>(p.v, p.sv, start, kt, hk, len);
   };
   auto dma_piece = [&](const Dma& d, int slot, int j) {  // j < PW: K piece j, else V piece j - PW
     if (j < PW)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(d.tk + d.ok[j]), (lds_void*)(smem + slot * TL + (w * PW + j) * 1024),
-                                       16, 0, 0);
+      tile_dma(d.k, smem + slot * TL + (w * PW + j) * 1024, dk[j]);
     else
-      __builtin_amdgcn_global_load_lds((gbl_void*)(d.tv + d.ov[j - PW]),
-                                       (lds_void*)(smem + (3 + slot) * TL + (w * PW + j - PW) * 1024), 16, 0, 0);
+      tile_dma(d.v, smem + (3 + slot) * TL + (w * PW + j - PW) * 1024, dv[j - PW]);
   };
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
   uint32_t ar[KS], arv[KS], at0[DT], at1[DT];  // row-fragment (K, V) / transposed-fragment (K) lane addresses

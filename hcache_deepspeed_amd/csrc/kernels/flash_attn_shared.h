@@ -133,4 +133,22 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
+// one LDS-DMA piece of K or V tile through a buffer descriptor built from plain scalars (the descriptor type does not
+// exist in the host pass, so no lambda may hold one): base = the tile's first row of this kv head, records = the bytes
+// up to the end of the tile's last row inside the sequence -- the range check zero-fills the pieces of rows past it
+struct TileSrc {
+  const char* base;
+  int bytes;
+};
+template <int D>
+__device__ __forceinline__ TileSrc tile_src(const bf16* base, int64_t stride, int start, int kt, int hk, int len) {
+  const int rows = min(BN, len - kt * BN);
+  return {(const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D),
+          (int)(((int64_t)(rows - 1) * stride + D) * 2)};
+}
+__device__ __forceinline__ void tile_dma(const TileSrc& t, void* lds, int32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)t.base, (short)0, t.bytes, 0x00020000),
+                                           (lds_void*)lds, 16, off, 0, 0, 0);
+}
+
 }  // namespace

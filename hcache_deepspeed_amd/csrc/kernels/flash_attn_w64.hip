@@ -62,23 +62,6 @@ __device__ __forceinline__ uint64_t memtime_stamp() {
 }
 __device__ unsigned long long g_w64_stamps[4][8];  // per wave index: segment cycles, tiles, waves (summed)
 constexpr float kMaskPen = 1048576.f;  // 2^20, times the -1 of a masked score (see mask_tile)
-// one LDS-DMA piece of K or V tile through a buffer descriptor built from plain scalars (the descriptor type does not
-// exist in the host pass, so no lambda may hold one): base = the tile's first row of this kv head, records = the bytes
-// up to the end of the tile's last row inside the sequence -- the range check zero-fills the pieces of rows past it
-struct TileSrc {
-  const char* base;
-  int bytes;
-};
-template <int D>
-__device__ __forceinline__ TileSrc tile_src(const bf16* base, int64_t stride, int start, int kt, int hk, int len) {
-  const int rows = min(BN, len - kt * BN);
-  return {(const char*)(base + (int64_t)(start + kt * BN) * stride + (int64_t)hk * D),
-          (int)(((int64_t)(rows - 1) * stride + D) * 2)};
-}
-__device__ __forceinline__ void dma_piece(const TileSrc& t, void* lds, int32_t off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)t.base, (short)0, t.bytes, 0x00020000),
-                                           (lds_void*)lds, 16, off, 0, 0, 0);
-}
 __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
 
 template <int D, int MODE>
@@ -483,8 +466,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // work on the diagonal tiles set the pace at every barrier)
 #pragma unroll
         for (int j = 0; j < PW; ++j) {
-          dma_piece(rsv, dstv + j * 1024, dv[j]);
-          dma_piece(rsk, dstk + j * 1024, dk[j]);
+          tile_dma(rsv, dstv + j * 1024, dv[j]);
+          tile_dma(rsk, dstk + j * 1024, dk[j]);
         }
         return;
       }
@@ -509,9 +492,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           if constexpr (!DIAG_DMA_B && (SPREAD ? (m < 32 && (m & 3) == 1) : (m < 16 && (m & 1)))) {
             constexpr int j = SPREAD ? m >> 2 : m >> 1;
             if constexpr (j < PW)
-              dma_piece(rsv, dstv + j * 1024, dv[j]);
+              tile_dma(rsv, dstv + j * 1024, dv[j]);
             else
-              dma_piece(rsk, dstk + (j - PW) * 1024, dk[j - PW]);
+              tile_dma(rsk, dstk + (j - PW) * 1024, dk[j - PW]);
           }
         });
 #pragma unroll
@@ -561,9 +544,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           if constexpr ((!MANUAL_A || DIAG_DMA_B) && sl % 4 == 1) {
             constexpr int j = sl / 4;
             if constexpr (j < PW)
-              dma_piece(rsv, dstv + j * 1024, dv[j]);
+              tile_dma(rsv, dstv + j * 1024, dv[j]);
             else
-              dma_piece(rsk, dstk + (j - PW) * 1024, dk[j - PW]);
+              tile_dma(rsk, dstk + (j - PW) * 1024, dk[j - PW]);
           }
           __builtin_amdgcn_sched_barrier(0);
         });
