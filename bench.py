@@ -73,6 +73,9 @@ def main():
     ap.add_argument("--offload", choices=["none", "cpu", "nvme"], default="none",
                     help="ZeRO-Offload/Infinity of optimizer states (+ params with --offload-param)")
     ap.add_argument("--offload-param", action="store_true")
+    ap.add_argument("--offload-ratio", type=float, default=1.0,
+                    help="with --offload cpu/nvme: fraction of the optimizer partition updated on the host (Twin-Flow / "
+                         "ZeRO-Offload++); the rest keeps the on-device fused Adam")
     ap.add_argument("--nvme-path", default="/tmp/hds_nvme", help="swap folder of the NVMe tier (--offload nvme)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
     ap.add_argument("--offload-opt-states", action="store_true",
@@ -172,7 +175,8 @@ def main():
                                 "offload_opt_states": bool(args.offload_opt_states),
                                 "offload_parameters": args.offload_params_compile is not None}
     if args.offload != "none":
-        ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True}
+        ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True,
+                                                               "ratio": float(args.offload_ratio)}
         if args.offload_param:
             ds_config["zero_optimization"]["offload_param"] = {"device": args.offload, "pin_memory": True}
         if args.offload == "nvme":
@@ -366,6 +370,8 @@ def main():
             "config": {"model": "Llama-3-8B" if args.model == "llama3-8b" and not args.layers else
                        f"{args.model}{'-L' + str(args.layers) if args.layers else ''}",
                        "host_act_cache": bool(args.host_act_cache), "offload": args.offload,
+                       **({"offload_ratio": float(args.offload_ratio)} if args.offload != "none" and
+                          args.offload_ratio < 1.0 else {}),
                        "global_batch": world * mb * args.gas, "seq_len": S,
                        "parallelism": f"zero{args.zero}-dp{world}", "micro_batch_per_gpu": mb, "gas": args.gas,
                        "stage3_max_reuse_distance": ds_config["zero_optimization"].get("stage3_max_reuse_distance"),
