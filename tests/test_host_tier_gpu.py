@@ -179,6 +179,41 @@ def test_zero_infinity_nvme_tier_gpu(tmp_path):
 
 
 @pytest.mark.gpu
+def test_twin_flow_compact_gpu():
+    """Twin-Flow on the GPU (offload_optimizer.ratio 0.6): the fp32 master and moments of the device part share ONE
+    HBM buffer of n + 2m elements, the first 60 % of the partition steps with the host Adam while the rest steps
+    with the fused device Adam, and the losses follow the all-device run."""
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    res = {}
+    for mode in ("device", "twin"):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(hidden_size=256, intermediate_size=512, num_hidden_layers=4, num_attention_heads=2,
+                                  num_key_value_heads=1, vocab_size=512))
+        z = {"stage": 3}
+        if mode == "twin":
+            z["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "ratio": 0.6}
+        cfg = {"train_micro_batch_size_per_gpu": 2, "bf16": {"enabled": True},
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "zero_optimization": z}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        losses = []
+        for _ in range(4):
+            x = torch.randint(0, 512, (2, 256), device="cuda", generator=g)
+            loss = eng(x, labels=x)
+            eng.backward(loss)
+            eng.step()
+            losses.append(float(loss))
+        if mode == "twin":
+            o = eng.optimizer
+            n, mm = o.store.numel, o.store.numel - o.n_off
+            assert 0 < o.n_off < n and o.store.master.is_cuda
+            assert o.store.master.untyped_storage().nbytes() == 4 * (n + 2 * mm)
+        res[mode] = losses
+    assert res["device"] == pytest.approx(res["twin"], rel=2e-3, abs=2e-3)
+
+
+@pytest.mark.gpu
 def test_deepcompile_zero_infinity_schedule_gpu():
     """DeepCompile on ZeRO-Infinity (parameters in pinned host memory, 1 GPU): the profiled step yields a
     schedule whose selective-gather pass keeps units resident in HBM from forward to backward, so the compiled
