@@ -82,6 +82,8 @@ def main():
                     help="DeepCompile offload_adam_states: Adam moments + fp32 master on pinned host between steps")
     ap.add_argument("--offload-states-ratio", type=float, default=1.0,
                     help="with --offload-opt-states: fraction of every moved state (its tail) kept on the host between steps")
+    ap.add_argument("--offload-states-host-step", action="store_true",
+                    help="with --offload-opt-states: the host tails stay on the host and step there (host Adam)")
     ap.add_argument("--offload-params-compile", type=float, default=None, metavar="BUDGET_GIB",
                     help="DeepCompile offload_parameters on the GPU-optimizer engine; the pass keeps shards on the "
                          "device within BUDGET_GIB of HBM (0: every shard on the host)")
@@ -194,6 +196,7 @@ def main():
         kw = {} if args.offload_params_compile is None else {"mem_budget_bytes": args.offload_params_compile * 2**30}
         if args.offload_opt_states:
             kw["offload_states_ratio"] = args.offload_states_ratio
+            kw["offload_states_host_step"] = bool(args.offload_states_host_step)
         engine.compile(compile_kwargs=kw)  # schedule compiled after the profiled warmup step (compile/backend.py)
     t_init = time.time() - t_init
     dev = engine.device

@@ -94,7 +94,8 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
         kw = compile_kwargs or {}
         engine.optimizer.enable_state_offload(include_master=bool(kw.get("offload_master", True)),
                                               ratio=float(kw.get("offload_states_ratio", 1.0)),
-                                              chunk_mb=float(kw.get("offload_states_chunk_mb", 1024)))
+                                              chunk_mb=float(kw.get("offload_states_chunk_mb", 1024)),
+                                              host_step=bool(kw.get("offload_states_host_step", False)))
     times["offload_adam_states"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     if cfg.offload_parameters and not engine._config.zero_config.offload_param.enabled:

@@ -1643,14 +1643,14 @@ class ZeroOptimizer:
     def _seg_group(self, seg):
         return self.param_groups[seg.group]
 
-    def enable_state_offload(self, include_master=True, ratio=1.0, chunk_mb=1024):
+    def enable_state_offload(self, include_master=True, ratio=1.0, chunk_mb=1024, host_step=False):
         """Optimizer states (and the fp32 master) live in pinned host memory between ``step()`` and the late
         backward of the next step (compile ``offload_opt_states``)."""
         if self.kind == "generic":
             raise NotImplementedError("offload_opt_states needs a fused optimizer (Adam/Lion/Adagrad) over the flat store")
         from .state_offload import OptimizerStateOffload
         if self.state_offload is None:
-            self.state_offload = OptimizerStateOffload(self, include_master, ratio, chunk_mb)
+            self.state_offload = OptimizerStateOffload(self, include_master, ratio, chunk_mb, host_step)
             # off the device from the start: the first forward is the one that needs the HBM when the states and
             # the activations do not fit together
             self.state_offload.offload()
@@ -1737,11 +1737,15 @@ class ZeroOptimizer:
                     return so.view(k, lo, hi)
                 return (s.master if k == "master" else s.states[k])[lo:hi]
 
+            hosted = []  # host-step tails of the state offload: updated on the host after the device pieces are queued
             for sg in s.segments:
                 g = self._seg_group(sg)
                 lo0, hi0 = sg.store_off, sg.store_off + sg.numel
                 bounds = [lo0] + [c for c in cuts if lo0 < c < hi0] + [hi0]
                 for lo, hi in zip(bounds[:-1], bounds[1:]):
+                    if so is not None and found_inf is None and so.hosted(lo):
+                        hosted.append((lo, hi, g))
+                        continue
                     p32, gr, lp = sv("master", lo, hi), s.grad[lo:hi], lp_flat[lo:hi]
                     if self.kind == "adam":
                         fused.adam_flat(p32, gr, sv("exp_avg", lo, hi), sv("exp_avg_sq", lo, hi),
@@ -1755,6 +1759,8 @@ class ZeroOptimizer:
                     elif self.kind == "adagrad":
                         fused.adagrad_flat(p32, gr, sv("sum", lo, hi), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
                                            g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
+            if hosted:
+                so.step_on_host(hosted, coef, lp_flat)
         tmp = self.__dict__.pop("_step_lp", None)
         if tmp is not None:
             self._publish_lp(tmp)

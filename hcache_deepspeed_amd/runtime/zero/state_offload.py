@@ -32,6 +32,12 @@ still runs per contiguous piece):
 * the backward reloads the tails as soon as the HBM it has freed holds them -- in ONE allocation (sliced per chunk):
   chunk-by-chunk reloads into the holes of a half-freed activation pool fragmented it for the next forward.
 
+``host_step`` (``offload_states_host_step``): the tails never come back. They stay in pinned host memory and ``step()``
+updates them THERE with the host Adam -- per piece, the fp32 gradient goes D2H, the host kernel updates master and
+moments in place and writes the bf16 parameters into pinned staging, which goes H2D -- while the device kernels update
+the heads. Per step r x 4 bytes per element cross PCIe each way instead of r x 12 (the Twin-Flow split of ZeRO-Offload,
+applied to the pass's byte-granular tails); nothing is reloaded before ``step()`` and nothing is offloaded after it.
+
 Offload and reload run on SEPARATE copy streams: a reload issued while the post-step offload of other chunks is still
 draining does not queue behind it -- it waits only for its own chunk's offload.
 """
@@ -43,9 +49,11 @@ import torch
 
 class OptimizerStateOffload:
 
-    def __init__(self, zopt, include_master=True, ratio=1.0, chunk_mb=1024):
+    def __init__(self, zopt, include_master=True, ratio=1.0, chunk_mb=1024, host_step=False):
         self.z = zopt
         self.include_master = bool(include_master)
+        self.host_step = bool(host_step) and self.include_master and zopt.kind == "adam"
+        self._h_grad = self._h_lp = None  # host-step staging (pinned, double-buffered)
         self.ratio = min(1.0, max(0.0, float(ratio)))
         self.chunk_bytes = max(256, int(float(chunk_mb) * 2**20))
         dev = zopt.device
@@ -281,10 +289,75 @@ class OptimizerStateOffload:
             self.reloading = True
             self.n_reloads += 1
 
+    def hosted(self, lo):
+        """Does ``step()`` update the piece starting at ``lo`` on the host (host-step tails)?"""
+        return (self.host_step and self.split and self.offloaded and lo >= self.a and "master" in self.host
+                and all(k in self.host for k, v in self.z.store.states.items() if v is not None))
+
+    def step_on_host(self, pieces, coef, lp_flat):
+        """Host Adam over the tail pieces [(lo, hi, group)]: D2H of piece i + 1's gradient and H2D of piece i - 1's
+        bf16 parameters overlap the host update of piece i; the device kernels of the heads (already queued) run
+        meanwhile. The bf16 parameters land in ``lp_flat`` ordered before the current stream on return."""
+        from ...ops.cpu_optimizers import cpu_adam_flat
+        z, s = self.z, self.z.store
+        cur = torch.cuda.current_stream() if self.cuda else None
+        big = max(hi - lo for lo, hi, _ in pieces)
+        if self._h_grad is None or self._h_grad[0].numel() < big:
+            self._h_grad = [torch.empty(big, dtype=s.grad.dtype, pin_memory=self.cuda) for _ in range(2)]
+            self._h_lp = [torch.empty(big, dtype=lp_flat.dtype, pin_memory=self.cuda) for _ in range(2)]
+        coef = float(coef) if not torch.is_tensor(coef) else float(coef.item())
+        d2h, h2d = [None, None], [None, None]
+
+        def issue_d2h(i):
+            lo, hi, _ = pieces[i]
+            b = i & 1
+            if not self.cuda:
+                self._h_grad[b][:hi - lo].copy_(s.grad[lo:hi])
+                return
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ev)
+                self._h_grad[b][:hi - lo].copy_(s.grad[lo:hi], non_blocking=True)
+                d2h[b] = torch.cuda.Event()
+                d2h[b].record(self.stream)
+
+        issue_d2h(0)
+        for i, (lo, hi, g) in enumerate(pieces):
+            b, n = i & 1, hi - lo
+            if i + 1 < len(pieces):
+                issue_d2h(i + 1)
+            if self.cuda:
+                d2h[b].synchronize()
+                if h2d[b] is not None:
+                    h2d[b].synchronize()  # staging buffer b is free again
+            a = self.a
+            st = {k: self.host[k][lo - a:hi - a] for k in s.states if s.states[k] is not None}
+            out = self._h_lp[b][:n]
+            cpu_adam_flat(self.host["master"][lo - a:hi - a], self._h_grad[b][:n], st["exp_avg"], st["exp_avg_sq"],
+                          g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))),
+                          g.get("eps", 1e-8), g.get("weight_decay", 0.0), z.adamw, g.get("bias_correction", True),
+                          bf16_out=out if out.dtype == torch.bfloat16 else None, grad_scale=coef)
+            if out.dtype != torch.bfloat16:
+                out.copy_(self.host["master"][lo - a:hi - a])
+            if self.cuda:
+                with torch.cuda.stream(self.reload_stream):
+                    lp_flat[lo:hi].copy_(out, non_blocking=True)
+                    h2d[b] = torch.cuda.Event()
+                    h2d[b].record(self.reload_stream)
+            else:
+                lp_flat[lo:hi].copy_(out)
+        if self.cuda:
+            cur.wait_stream(self.reload_stream)
+            cur.wait_stream(self.stream)  # the gradient buffer is zeroed after step()
+        self.host_steps = getattr(self, "host_steps", 0) + 1
+
     def wait_tails(self):
         """Before ``step()``: every tail chunk on the device and ordered before the current stream (states stay
-        split)."""
+        split). Host-step tails stay where they are."""
         if not self.offloaded:
+            return
+        if self.host_step:
             return
         self.reload()
         if self.cuda:
@@ -298,7 +371,15 @@ class OptimizerStateOffload:
     def wait(self):
         """Whole flat states on the device (checkpoint save / load, fp32 fragment access): reload the tails and
         concatenate each state; they stay whole until the next step's ``offload()``."""
-        self.wait_tails()
+        if self.host_step and self.offloaded:
+            self.reload()
+            self.host_step, hs = False, True
+            try:
+                self.wait_tails()
+            finally:
+                self.host_step = hs
+        else:
+            self.wait_tails()
         if not self.split:
             return
         for k in list(self.tail):
@@ -311,7 +392,7 @@ class OptimizerStateOffload:
     ensure_resident = wait
 
     def on_backward_position(self, pos):
-        if not self.offloaded or self.reloading:
+        if not self.offloaded or self.reloading or self.host_step:
             return
         if self.reload_pos is not None and pos is not None:  # placed by the compiled schedule (plan_state_reload)
             if pos <= self.reload_pos:
@@ -338,5 +419,6 @@ class OptimizerStateOffload:
         return {"state_bytes": self.bytes, "offloads": self.n_offloads, "reloads": self.n_reloads,
                 "reload_pos": self.reload_pos, "ratio": self.ratio, "split_element": self.a,
                 "chunks": len(self.bounds), "chunk_mb": round(self.chunk_bytes / 2**20, 3),
+                "host_step": self.host_step, "host_steps": getattr(self, "host_steps", 0),
                 "fwd_waits": self.fwd_waits, "fwd_wait_s": round(self.fwd_wait_s, 3),
                 "states": sorted(self.host) if self.host else sorted(self._keys())}
