@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--offload", choices=["none", "cpu", "nvme"], default="none",
                     help="ZeRO-Offload/Infinity of optimizer states (+ params with --offload-param)")
     ap.add_argument("--offload-param", action="store_true")
+    ap.add_argument("--sub-group-size", type=int, default=None,
+                    help="zero_optimization.sub_group_size (ZeRO-Offload's host-step piece, elements)")
     ap.add_argument("--offload-ratio", type=float, default=1.0,
                     help="with --offload cpu/nvme: fraction of the optimizer partition updated on the host (Twin-Flow / "
                          "ZeRO-Offload++); the rest keeps the on-device fused Adam")
@@ -179,6 +181,8 @@ def main():
     if args.offload != "none":
         ds_config["zero_optimization"]["offload_optimizer"] = {"device": args.offload, "pin_memory": True,
                                                                "ratio": float(args.offload_ratio)}
+        if args.sub_group_size:
+            ds_config["zero_optimization"]["sub_group_size"] = int(args.sub_group_size)
         if args.offload_param:
             ds_config["zero_optimization"]["offload_param"] = {"device": args.offload, "pin_memory": True}
         if args.offload == "nvme":

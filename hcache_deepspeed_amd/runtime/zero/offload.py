@@ -59,7 +59,10 @@ class OffloadZeroOptimizer(ZeroOptimizer):
         self.n_off = int(n * self.ratio) // 64 * 64 if self.ratio < 1.0 else n
         self.lp_on_host = s.lp.device.type == "cpu" and self.device.type == "cuda"
         assert not (self.lp_on_host and self.n_off < n), "offload_param requires offload_optimizer.ratio == 1"
-        self.sub = max(1 << 20, min(int(self.zcfg.sub_group_size), self.n_off or 1))
+        # pipeline piece: sub_group_size, capped at 256M elements -- at the 1e9 default the first gradient D2H and the
+        # last bf16 H2D of a step (4 GB / 2 GB each) sit outside the pipeline; Llama-3-8B mb10 Twin-Flow 0.4 on one
+        # box: 19,772 tok/s at 2.5e8 vs 18,651 at 1e9 and 17,536 at 1e8 (per-piece overhead), profiles/r5/*_r5ay.json
+        self.sub = max(1 << 20, min(int(self.zcfg.sub_group_size), 1 << 28, self.n_off or 1))
         self.nvme = None
         if self.offload_device == "nvme":
             # fp32 master + moments of the offloaded range on NVMe, streamed by the step in chunks of at most
