@@ -33,10 +33,11 @@ still runs per contiguous piece):
   chunk-by-chunk reloads into the holes of a half-freed activation pool fragmented it for the next forward.
 
 ``host_step`` (``offload_states_host_step``): the tails never come back. They stay in pinned host memory and ``step()``
-updates them THERE with the host Adam -- per piece, the fp32 gradient goes D2H, the host kernel updates master and
-moments in place and writes the bf16 parameters into pinned staging, which goes H2D -- while the device kernels update
-the heads. Per step r x 4 bytes per element cross PCIe each way instead of r x 12 (the Twin-Flow split of ZeRO-Offload,
-applied to the pass's byte-granular tails); nothing is reloaded before ``step()`` and nothing is offloaded after it.
+updates them THERE with the host Adam -- per piece, the gradient goes D2H, the host kernel updates master and moments
+in place and writes the bf16 parameters into pinned staging, which goes H2D -- while the device kernels update the
+heads. Per step r x 2 bytes per element cross PCIe each way with bf16 gradients (r x 4 down with fp32 ones) instead of
+r x 12 (the Twin-Flow split of ZeRO-Offload, applied to the pass's byte-granular tails); nothing is reloaded before
+``step()`` and nothing is offloaded after it.
 
 Offload and reload run on SEPARATE copy streams: a reload issued while the post-step offload of other chunks is still
 draining does not queue behind it -- it waits only for its own chunk's offload.
