@@ -298,6 +298,9 @@ def main():
     flops = (cfg_model.flops_per_token(S) if hasattr(cfg_model, "flops_per_token") else
              6 * cfg_model.active_params() + 12 * cfg_model.num_hidden_layers * S * cfg_model.hidden_size) * tokens
     mfu = flops / dt / (2.5e15 * world)
+    # the same with causal attention FLOPs (what the causal kernels execute; matters at long context)
+    flops_c = cfg_model.flops_per_token_causal(S) * tokens if hasattr(cfg_model, "flops_per_token_causal") else flops
+    mfu_c = flops_c / dt / (2.5e15 * world)
     mem = torch.cuda.max_memory_allocated(dev) / 2**30 if on_gpu else 0.0
     timed_peak = None
     if ac_t is not None and on_gpu:
@@ -320,7 +323,8 @@ def main():
             train_step(args.warmup + args.steps)
             sync()
             zopt.comm_stats = None
-        mine = {"rank": rank, "peak_mem_gib": round(mem, 1), "timed_steps_instrumented": timed_events is not None}
+        mine = {"rank": rank, "peak_mem_gib": round(mem, 1), "timed_steps_instrumented": timed_events is not None,
+                "host_threads": getattr(engine, "host_threads", None)}
         ue = getattr(zopt, "unit_events", None)
         if ue is not None:  # ZeRO-3 fetch / wait / prefetch events of the last micro-step (counts, numel, host ms)
             mine["unit_events"] = ue.summary()
@@ -352,6 +356,7 @@ def main():
                 "timed_steps_instrumented": any(r["timed_steps_instrumented"] for r in per_rank),
                 "exposed_comm_ms_per_step_max": max(r.get("exposed_comm_ms_per_step", 0.0) for r in per_rank),
                 "peak_mem_gib_per_rank": [r["peak_mem_gib"] for r in per_rank],
+                "host_threads_per_rank": [(r.get("host_threads") or {}).get("threads") for r in per_rank],
                 "rank0": per_rank[0],
                 "unit_events_rank0": per_rank[0].get("unit_events"),
                 "transport_selection": per_rank[0].get("transport_selection")}
@@ -384,6 +389,8 @@ def main():
                        "stage3_max_reuse_distance": ds_config["zero_optimization"].get("stage3_max_reuse_distance"),
                        "activation_checkpointing": bool(args.ckpt), "deepcompile": bool(args.deepcompile)},
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
+                      "mfu_causal": round(mfu_c, 4), "tflops_causal_per_gpu": round(flops_c / dt / world / 1e12, 1),
+                      "host_threads": getattr(engine, "host_threads", None),
                       "final_loss": round(float(loss.item()), 4), "peak_mem_gib": round(mem, 1),
                       "init_s": round(t_init, 1), "valid": on_gpu and not bool(args.layers),
                       "tuned_gemm_table": tuned, "device": "mi355x" if on_gpu else "cpu-dry-run",

@@ -64,6 +64,9 @@ class Work:
         return self._comm._lib.hds_rccl_query(self._comm._h, self._slot) == 1
 
 
+_fail_setup_ranks = set()  # fault injection (tests): these ranks' local setup raises
+
+
 class RcclCommunicator:
 
     def __init__(self, group=None):
@@ -73,21 +76,36 @@ class RcclCommunicator:
         self.group = group
         self.rank = tdist.get_rank(group) if tdist.is_initialized() else 0
         self.world = tdist.get_world_size(group) if tdist.is_initialized() else 1
-        uid = ctypes.create_string_buffer(128)
-        if self.rank == 0:
-            self._check(self._lib.hds_rccl_unique_id(uid), "unique_id")
-        if self.world > 1:
-            obj = [bytes(uid.raw) if self.rank == 0 else None]
-            src = tdist.get_global_rank(group, 0) if group is not None else 0
-            tdist.broadcast_object_list(obj, src=src, group=group)
-            uid = ctypes.create_string_buffer(obj[0], 128)
-        err = ctypes.c_int(0)
+        from .setup import collective_setup
         # torch's pooled streams are never destroyed, so record_stream() events on it outlive this object
         self.stream = torch.cuda.Stream(priority=-1)
-        self._h = self._lib.hds_rccl_init(uid, self.world, self.rank, ctypes.c_void_p(self.stream.cuda_stream),
-                                          ctypes.byref(err))
-        if not self._h:
-            raise RuntimeError(f"native RCCL init failed: {self._err(err.value)}")
+        self._h = None
+
+        # failure-symmetric (comm/setup.py): rank 0's unique id travels in the same all_gather_object that agrees on
+        # every rank's local readiness; the init result is agreed again, so a rank that failed never leaves the
+        # others in a different collective
+        def local():
+            if _fail_setup_ranks and self.rank in _fail_setup_ranks:
+                raise RuntimeError("injected native RCCL setup failure")
+            uid = ctypes.create_string_buffer(128)
+            if self.rank == 0:
+                self._check(self._lib.hds_rccl_unique_id(uid), "unique_id")
+            return None, (bytes(uid.raw) if self.rank == 0 else None)
+
+        def finish(_, payloads):
+            uid = ctypes.create_string_buffer(payloads[0], 128)
+            err = ctypes.c_int(0)
+            h = self._lib.hds_rccl_init(uid, self.world, self.rank, ctypes.c_void_p(self.stream.cuda_stream),
+                                        ctypes.byref(err))
+            if not h:
+                raise RuntimeError(f"native RCCL init failed: {self._err(err.value)}")
+            return h
+
+        def cleanup(_, h):
+            if h:
+                self._lib.hds_rccl_destroy(h)
+
+        _, self._h = collective_setup(group, local, finish, cleanup, what="native RCCL communicator")
 
     def _err(self, rc):
         s = self._lib.hds_rccl_error_string(rc)

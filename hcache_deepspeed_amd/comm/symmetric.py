@@ -45,6 +45,7 @@ class SymmetricMemoryError(RuntimeError):
 
 
 _same_node = {}  # id(group) -> every rank of the group runs on this host
+_fail_setup_ranks = set()  # fault injection (tests): these ranks' local setup raises
 
 
 def _host_id():
@@ -84,26 +85,55 @@ class SymmetricMemory:
         self.rank = dist.get_rank(group)
         if not 1 <= self.world <= MAX_RANKS:
             raise ValueError(f"symmetric memory supports 1..{MAX_RANKS} ranks, got {self.world}")
-        self.lib = native.kernels()
         self.cap = (int(cap_bytes) + 15) // 16 * 16
-        ptr, handle = ctypes.c_void_p(), ctypes.create_string_buffer(64)
-        native.check(self.lib.hds_symm_alloc(self.cap, ctypes.byref(ptr), handle), "symm_alloc")
-        self._own = ptr.value
-        handles = [None] * self.world
-        dist.all_gather_object(handles, handle.raw, group=group)
-        bases, self._opened = [], []
-        for r, h in enumerate(handles):
-            if r == self.rank:
-                bases.append(self._own)
-                continue
-            p = ctypes.c_void_p()
-            native.check(self.lib.hds_symm_open(h, ctypes.byref(p)), "symm_open")
-            bases.append(p.value)
-            self._opened.append(p.value)
+        self._own, self._opened, self._status = None, [], None
+        from .setup import collective_setup
+
+        # three failure-symmetric phases (comm/setup.py): local allocation, ONE all_gather_object that both agrees
+        # and exchanges the IPC handles, then opening the peers' buffers with a second agreement -- a rank whose
+        # allocation fails (OOM) can no longer leave its peers waiting in a different collective
+        def local():
+            if _fail_setup_ranks and self.rank in _fail_setup_ranks:
+                raise RuntimeError("injected symmetric-memory setup failure")
+            lib = native.kernels()
+            ptr, handle = ctypes.c_void_p(), ctypes.create_string_buffer(64)
+            native.check(lib.hds_symm_alloc(self.cap, ctypes.byref(ptr), handle), "symm_alloc")
+            st = ctypes.c_void_p()
+            if lib.hds_symm_status_alloc(ctypes.byref(st)) != 0:
+                lib.hds_symm_free(ptr)
+                raise RuntimeError("symm_status_alloc failed")
+            return (lib, ptr.value, st.value), handle.raw
+
+        def finish(state, handles):
+            lib, own, _ = state
+            bases, opened = [], []
+            try:
+                for r, h in enumerate(handles):
+                    if r == self.rank:
+                        bases.append(own)
+                        continue
+                    p = ctypes.c_void_p()
+                    native.check(lib.hds_symm_open(h, ctypes.byref(p)), "symm_open")
+                    bases.append(p.value)
+                    opened.append(p.value)
+            except Exception:
+                for q in opened:
+                    lib.hds_symm_close(ctypes.c_void_p(q))
+                raise
+            return bases, opened
+
+        def cleanup(state, fin):
+            if state is None:
+                return
+            lib, own, st = state
+            for q in (fin[1] if fin else []):
+                lib.hds_symm_close(ctypes.c_void_p(q))
+            lib.hds_symm_free(ctypes.c_void_p(own))
+            lib.hds_symm_status_free(ctypes.c_void_p(st))
+
+        (self.lib, self._own, self._status), (bases, self._opened) = collective_setup(
+            group, local, finish, cleanup, what=f"symmetric memory ({self.cap >> 20} MiB)")
         self._bases = (ctypes.c_int64 * MAX_RANKS)(*(bases + [0] * (MAX_RANKS - len(bases))))
-        st = ctypes.c_void_p()
-        native.check(self.lib.hds_symm_status_alloc(ctypes.byref(st)), "symm_status_alloc")
-        self._status = st.value
         self._status_word = ctypes.c_uint32.from_address(self._status)
         self.epoch = 0
         self.calls = {"all_reduce": 0, "all_gather": 0, "reduce_scatter": 0}

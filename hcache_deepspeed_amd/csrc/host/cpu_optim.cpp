@@ -35,6 +35,12 @@ inline uint16_t f_to_bf16(float f) {
 
 constexpr int64_t kTile = 1 << 20;
 
+// Process-wide thread count of the host kernels (0: OpenMP's default). omp_set_num_threads() only sets the CALLING
+// thread's ICV, and the kernels are called from the training thread and from copy-pipeline worker threads alike, so
+// every parallel region names its count explicitly.
+int g_threads = 0;
+inline int nthreads() { return g_threads > 0 ? g_threads : omp_get_max_threads(); }
+
 }  // namespace
 
 // gdtype: 0 fp32, 1 bf16. out_bf16 may be null.
@@ -43,7 +49,7 @@ HDS_CLONES HDS_EXPORT int hds_cpu_adam(float* p, const void* g, int gdtype, floa
                                        float bc2, int adamw, float gscale) {
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = 1.0f / std::sqrt(bc2);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(nthreads())
   for (int64_t t0 = 0; t0 < n; t0 += kTile) {
     const int64_t t1 = t0 + kTile < n ? t0 + kTile : n;
     if (gdtype == 0) {
@@ -88,7 +94,7 @@ HDS_CLONES HDS_EXPORT int hds_cpu_adam(float* p, const void* g, int gdtype, floa
 
 HDS_CLONES HDS_EXPORT int hds_cpu_lion(float* p, const void* g, int gdtype, float* m, uint16_t* out_bf16, int64_t n,
                                        float lr, float b1, float b2, float wd, float gscale) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(nthreads())
   for (int64_t t0 = 0; t0 < n; t0 += kTile) {
     const int64_t t1 = t0 + kTile < n ? t0 + kTile : n;
     for (int64_t i = t0; i < t1; ++i) {
@@ -106,7 +112,7 @@ HDS_CLONES HDS_EXPORT int hds_cpu_lion(float* p, const void* g, int gdtype, floa
 
 HDS_CLONES HDS_EXPORT int hds_cpu_adagrad(float* p, const void* g, int gdtype, float* s, uint16_t* out_bf16,
                                           int64_t n, float lr, float eps, float wd, float gscale) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(nthreads())
   for (int64_t t0 = 0; t0 < n; t0 += kTile) {
     const int64_t t1 = t0 + kTile < n ? t0 + kTile : n;
     for (int64_t i = t0; i < t1; ++i) {
@@ -125,7 +131,7 @@ HDS_CLONES HDS_EXPORT int hds_cpu_adagrad(float* p, const void* g, int gdtype, f
 HDS_CLONES HDS_EXPORT double hds_cpu_sumsq(const void* g, int gdtype, int64_t n, int* found_inf) {
   double acc = 0.0;
   int bad = 0;
-#pragma omp parallel for reduction(+ : acc) reduction(| : bad) schedule(static)
+#pragma omp parallel for reduction(+ : acc) reduction(| : bad) schedule(static) num_threads(nthreads())
   for (int64_t i = 0; i < n; ++i) {
     const float x = gdtype == 0 ? ((const float*)g)[i] : bf16_to_f(((const uint16_t*)g)[i]);
     acc += (double)x * x;
@@ -135,9 +141,10 @@ HDS_CLONES HDS_EXPORT double hds_cpu_sumsq(const void* g, int gdtype, int64_t n,
   return acc;
 }
 
-HDS_EXPORT int hds_cpu_num_threads() { return omp_get_max_threads(); }
+HDS_EXPORT int hds_cpu_num_threads() { return nthreads(); }
 
 HDS_EXPORT int hds_cpu_set_num_threads(int n) {
-  omp_set_num_threads(n);
+  g_threads = n > 0 ? n : 0;
+  if (n > 0) omp_set_num_threads(n);
   return 0;
 }

@@ -121,9 +121,10 @@ class InferenceEngineV2:
         """One ragged forward. Returns logits [n_seqs, V] and, per sequence, its latents [L, n_tokens, W] (host).
         ``sync_latents=False``: the host does not wait for the latent copies (no per-forward synchronize, reference
         engine_v2.py:131-189 keeps its host free the same way); call ``wait_latents()`` (or check
-        ``latents_ready()``) before reading them -- ``restore_kv`` / ``evict`` wait on their own. The default
-        (None) waits after a prefill and defers in HIP-graph decode steps, whose latents go to a device ring drained
-        in bulk (inference/v2/model.py ``_LatentRing``): a decode loop does not synchronize per token."""
+        ``latents_ready()``) before reading them -- ``restore_kv`` / ``evict`` wait on their own; HIP-graph decode
+        steps then leave their latents in a device ring drained in bulk (inference/v2/model.py ``_LatentRing``), so a
+        decode loop does not synchronize per token. The default (None) is synchronous: the returned latents are on
+        the host when ``put`` returns (a graph-decode step flushes its ring first)."""
         batch_uids = list(batch_uids)
         batch_tokens = [t if isinstance(t, torch.Tensor) else torch.tensor(t) for t in batch_tokens]
         if do_checks:
@@ -141,7 +142,7 @@ class InferenceEngineV2:
         if self._model.decode_graph_eligible(batch, capture_latents):
             # HIP-graph decode step (latents, if captured, land in the graph's device ring)
             logits, latents = self._model.forward_decode_graph(batch, capture_latents=capture_latents)
-            if latents is not None and sync_latents:
+            if latents is not None and sync_latents is not False:
                 self.wait_latents()
         else:
             logits, latents = self._model.forward(batch, capture_latents=capture_latents,

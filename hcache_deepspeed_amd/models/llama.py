@@ -74,6 +74,12 @@ class LlamaConfig:
         return 6 * self.num_params(include_embedding=False) + 6 * self.vocab_size * self.hidden_size + \
             12 * self.num_hidden_layers * self.hidden_size * seq_len
 
+    def flops_per_token_causal(self, seq_len):
+        """The same with the attention FLOPs a causal kernel actually performs: each query attends to ~half the keys
+        ((S + 1) / 2 on average), so the score and P.V terms are 6*L*H*(S+1) instead of 12*L*H*S."""
+        return 6 * self.num_params(include_embedding=False) + 6 * self.vocab_size * self.hidden_size + \
+            6 * self.num_hidden_layers * self.hidden_size * (seq_len + 1)
+
 
 def llama3_8b(**kw):
     return LlamaConfig(**kw)

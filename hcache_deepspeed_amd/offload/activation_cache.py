@@ -658,14 +658,17 @@ class BlitLimitError(RuntimeError):
 
 
 def check_blit_limit(cfg, device_type, limit_in_effect=None):
-    """Refuse a spilling host activation cache when DEBUG_CLR_LIMIT_BLIT_WG did not reach the HIP runtime.
+    """Warn -- or, in strict mode, refuse -- a spilling host activation cache when DEBUG_CLR_LIMIT_BLIT_WG did not
+    reach the HIP runtime.
 
     Spills are device->host copies, which this ROCm stack runs as blit kernels spread over as many workgroups as the
     copy has chunks: they take CUs from the forward they overlap (32k tokens, 25 GiB spilled: 10,309 instead of
     13,949 tok/s, profiles/r4/copy_engine_ab_r4f.txt). The runtime reads the workgroup limit once, when it loads --
     i.e. at ``import torch`` -- so a script that imported torch before this package, without the variable exported,
-    would silently lose ~25 %. Rather than that, fail loudly with the fix. Policy "recompute" spills nothing and is
-    allowed; ``host_act_cache.allow_unlimited_blit`` (or HDS_ALLOW_UNLIMITED_BLIT=1) accepts the slower spills."""
+    loses ~25 % of the overlapped forward. By default that is a loud warning with the fix (the run still trains
+    correctly, only slower); ``host_act_cache.strict_blit_limit`` (or HDS_STRICT_BLIT=1) makes it a
+    ``BlitLimitError`` at engine init. Policy "recompute" spills nothing; ``allow_unlimited_blit`` (or
+    HDS_ALLOW_UNLIMITED_BLIT=1) silences both."""
     if device_type != "cuda":
         return
     if limit_in_effect is None:
@@ -673,14 +676,16 @@ def check_blit_limit(cfg, device_type, limit_in_effect=None):
     if limit_in_effect or getattr(cfg, "policy", "budget") == "recompute":
         return
     if getattr(cfg, "allow_unlimited_blit", False) or os.environ.get("HDS_ALLOW_UNLIMITED_BLIT") == "1":
-        logger.warning("host activation cache: spills run as unlimited blit kernels (DEBUG_CLR_LIMIT_BLIT_WG was not "
-                       "in the environment when torch loaded the HIP runtime); accepted by allow_unlimited_blit")
+        logger.info("host activation cache: spills run as unlimited blit kernels (DEBUG_CLR_LIMIT_BLIT_WG was not "
+                    "in the environment when torch loaded the HIP runtime); accepted by allow_unlimited_blit")
         return
-    raise BlitLimitError(
-        "host activation cache: DEBUG_CLR_LIMIT_BLIT_WG was not in the environment when torch loaded the HIP runtime, "
-        "so activation spills would run as unlimited blit kernels and slow the overlapped forward by ~25 %. Export "
-        "DEBUG_CLR_LIMIT_BLIT_WG=16 before starting Python (the hcache_deepspeed_amd launcher does), or import "
-        "hcache_deepspeed_amd before torch, or set mi355x.host_act_cache.allow_unlimited_blit=true to accept it.")
+    msg = ("host activation cache: DEBUG_CLR_LIMIT_BLIT_WG was not in the environment when torch loaded the HIP "
+           "runtime, so activation spills run as unlimited blit kernels and slow the overlapped forward by ~25 %. Export "
+           "DEBUG_CLR_LIMIT_BLIT_WG=16 before starting Python (the hcache_deepspeed_amd launcher and bench.py do), or "
+           "import hcache_deepspeed_amd before torch; mi355x.host_act_cache.allow_unlimited_blit=true accepts it.")
+    if getattr(cfg, "strict_blit_limit", False) or os.environ.get("HDS_STRICT_BLIT") == "1":
+        raise BlitLimitError(msg)
+    logger.warning(msg)
 
 
 def build_activation_cache(cfg, device):

@@ -186,6 +186,8 @@ class HostActCacheConfig:
     forced_actions: Optional[dict] = None
     # accept spills through unlimited runtime blit kernels (DEBUG_CLR_LIMIT_BLIT_WG missing when HIP loaded)
     allow_unlimited_blit: bool = False
+    # refuse (BlitLimitError) instead of warning when spills would run as unlimited blit kernels
+    strict_blit_limit: bool = False
 
 
 AUTO = -1
@@ -214,6 +216,11 @@ class MI355XConfig:
     zero_comm_transport: str = "auto"
     # the ZeRO-3 fetch / wait / prefetch events also start / stop the engine timers (reference ENABLE_PROFILER)
     zero3_event_timers: bool = False
+    # host threads per rank of the C++ kernels (CPU Adam / Lion / Adagrad, host-step tails, NVMe tier) and of torch's
+    # CPU ops: "auto" = the rank's share of the node's CPUs (its NUMA node's when sysfs says where its GPU sits) when
+    # several ranks share the host and the count was not set explicitly (torchrun forces OMP_NUM_THREADS=1), else
+    # left alone; an int forces it
+    cpu_threads_per_rank: object = "auto"
     host_act_cache: HostActCacheConfig = field(default_factory=HostActCacheConfig)
 
 
@@ -338,6 +345,7 @@ class DeepSpeedConfig:
             comm_stats=bool(m.get("comm_stats", False)),
             zero_comm_transport=str(m.get("zero_comm_transport", "auto")),
             zero3_event_timers=bool(m.get("zero3_event_timers", False)),
+            cpu_threads_per_rank=m.get("cpu_threads_per_rank", "auto"),
             direct_wgrad=bool(m.get("direct_wgrad", True)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
             comm_high_priority=bool(m.get("comm_high_priority", True)),

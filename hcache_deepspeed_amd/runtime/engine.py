@@ -120,6 +120,8 @@ class DeepSpeedEngine(nn.Module):
         from ..monitor.monitor import MonitorMaster
         self.monitor = MonitorMaster(cfg.monitor_config)
         dist.configure(cfg)
+        from ..utils.numa import configure_rank_threads
+        self.host_threads = configure_rank_threads(getattr(cfg.mi355x, "cpu_threads_per_rank", "auto"))
         from ..utils.fault_injection import FaultInjector
         self.fault_injector = FaultInjector(cfg.raw.get("fault_injection"))
 

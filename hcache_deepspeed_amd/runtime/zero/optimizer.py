@@ -906,9 +906,33 @@ class ZeroOptimizer:
         if self.device.type != "cuda":
             log_dist("native_comm: CPU run, keeping torch.distributed", ranks=[0])
             return False
+        self.release_transports()  # what the startup selection set up goes first (collectively)
         self._native = {}
         self._route = None  # forced: every unit collective of every group on the native communicator
         return True
+
+    def release_transports(self):
+        """Undo the startup transport selection (or an earlier forced switch): destroy the native communicators and
+        close the symmetric buffers (both collective -- every rank calls this from the same compile switch), and clear
+        the measured route. Called before a forced ``compile.native_comm`` / ``compile.symmetric_memory`` switch so
+        the auto state neither leaks nor keeps routing collectives the switch should own."""
+        torch_sync = self.device.type == "cuda"
+        if torch_sync:
+            torch.cuda.synchronize(self.device)
+        for comm in (getattr(self, "_native", None) or {}).values():
+            try:
+                comm.destroy()
+            except Exception:  # noqa: BLE001 -- a communicator that failed already holds nothing
+                pass
+        for sm in (getattr(self, "_symm", None) or {}).values():
+            sm.close()
+        released = bool(getattr(self, "_native", None) or getattr(self, "_symm", None))
+        self._native = None
+        self._symm = {}
+        self._route = None
+        if released:
+            log_dist("zero comm transport: startup selection released for a forced compile switch", ranks=[0])
+        return released
 
     def _ncomm(self, group):
         cache = getattr(self, "_native", None)
@@ -1043,6 +1067,7 @@ class ZeroOptimizer:
         if not need or not all(symmetric.supported(g) for g, _ in need.values()):
             log_dist("symmetric_memory: no intra-node group of <= 8 ranks, keeping RCCL", ranks=[0])
             return False
+        self.release_transports()
         self._install_symm({key: symmetric.SymmetricMemory(g, nb) for key, (g, nb) in need.items()})
         self._route = None  # forced: symmetric wherever a buffer fits
         return True
@@ -1743,7 +1768,7 @@ class ZeroOptimizer:
                 lo0, hi0 = sg.store_off, sg.store_off + sg.numel
                 bounds = [lo0] + [c for c in cuts if lo0 < c < hi0] + [hi0]
                 for lo, hi in zip(bounds[:-1], bounds[1:]):
-                    if so is not None and found_inf is None and so.hosted(lo):
+                    if so is not None and so.hosted(lo):  # host-step tails never come back: step them there
                         hosted.append((lo, hi, g))
                         continue
                     p32, gr, lp = sv("master", lo, hi), s.grad[lo:hi], lp_flat[lo:hi]
@@ -1760,7 +1785,7 @@ class ZeroOptimizer:
                         fused.adagrad_flat(p32, gr, sv("sum", lo, hi), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
                                            g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
             if hosted:
-                so.step_on_host(hosted, coef, lp_flat)
+                so.step_on_host(hosted, coef, lp_flat, found_inf=found_inf, lp_cur=s.lp)
         tmp = self.__dict__.pop("_step_lp", None)
         if tmp is not None:
             self._publish_lp(tmp)

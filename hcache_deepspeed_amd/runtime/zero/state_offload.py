@@ -157,6 +157,8 @@ class OptimizerStateOffload:
         if self.cuda:
             self.stream.wait_stream(cur)
         keys = self._keys() if not self.split else list(self.host)
+        issued = []  # (event, bytes, storage) in D2H order: chunks that are views of ONE allocation (a reload arena,
+        # or a whole state split for the first time) free their HBM only when the LAST of them drains
         for k in keys:
             if self.split:
                 chunks, head = self.tail.get(k), None
@@ -187,7 +189,7 @@ class OptimizerStateOffload:
                         ev = torch.cuda.Event()
                         ev.record(self.stream)
                     self.events[(k, i)] = ev
-                    self._draining.append((ev, nb))
+                    issued.append((ev, nb, t.untyped_storage().data_ptr()))
                 else:
                     h[lo - a:hi - a].copy_(t)
                 self.bytes += nb
@@ -195,12 +197,24 @@ class OptimizerStateOffload:
             del chunks
             if head is not None:
                 self._set(k, head)
+        self._draining.extend(self._merge_shared(issued))
         self.split = True
         self.offloaded = True
         self.reloading = False
         self.n_offloads += 1
         self._fwd_last = None
         self.fwd_waits, self.fwd_wait_s = 0, 0.0
+
+    @staticmethod
+    def _merge_shared(issued):
+        """[(event, bytes, storage)] in issue order -> [(event, bytes)] with every group of chunks that share one
+        allocation merged into ONE entry at its last chunk's position: its bytes become usable only when that last
+        D2H drains (``record_stream`` on each view pins the whole block until then)."""
+        last, total = {}, collections.Counter()
+        for j, (_, nb, st) in enumerate(issued):
+            last[st] = j
+            total[st] += nb
+        return [(ev, total[st]) for j, (ev, _, st) in enumerate(issued) if last[st] == j]
 
     def on_forward_position(self):
         """Before a forward unit runs: retire the drained chunks and, if the HBM the allocator can hand out does not
@@ -295,13 +309,23 @@ class OptimizerStateOffload:
         return (self.host_step and self.split and self.offloaded and lo >= self.a and "master" in self.host
                 and all(k in self.host for k, v in self.z.store.states.items() if v is not None))
 
-    def step_on_host(self, pieces, coef, lp_flat):
+    def step_on_host(self, pieces, coef, lp_flat, found_inf=None, lp_cur=None):
         """Host Adam over the tail pieces [(lo, hi, group)]: D2H of piece i + 1's gradient and H2D of piece i - 1's
         bf16 parameters overlap the host update of piece i; the device kernels of the heads (already queued) run
-        meanwhile. The bf16 parameters land in ``lp_flat`` ordered before the current stream on return."""
+        meanwhile. The bf16 parameters land in ``lp_flat`` ordered before the current stream on return.
+
+        ``found_inf`` (device flag: fp16 dynamic loss scaling, or a symmetric-memory skip) is the same skip the device
+        kernels fold: when it is set the host tails are left untouched (and ``lp_flat``, if it is not the live
+        parameter buffer ``lp_cur``, receives the current parameters of the pieces)."""
         from ...ops.cpu_optimizers import cpu_adam_flat
         z, s = self.z, self.z.store
         cur = torch.cuda.current_stream() if self.cuda else None
+        if found_inf is not None and float(found_inf.reshape(-1)[0].item()) != 0.0:  # one sync, only when a flag exists
+            if lp_cur is not None and lp_flat.data_ptr() != lp_cur.data_ptr():
+                for lo, hi, _ in pieces:
+                    lp_flat[lo:hi].copy_(lp_cur[lo:hi])
+            self.host_skips = getattr(self, "host_skips", 0) + 1
+            return
         big = max(hi - lo for lo, hi, _ in pieces)
         if self._h_grad is None or self._h_grad[0].numel() < big:
             self._h_grad = [torch.empty(big, dtype=s.grad.dtype, pin_memory=self.cuda) for _ in range(2)]

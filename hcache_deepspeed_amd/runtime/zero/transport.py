@@ -73,28 +73,63 @@ def _shared_device(group, device):
 
 
 class _Timer:
+    """Median milliseconds of a collective. On the GPU every timed call runs BESIDE a stream of bf16 GEMMs on a
+    second stream (``contend``, default on): in training the unit collectives overlap the compute stream's GEMMs, and
+    a transport that takes CUs (the symmetric-memory kernels) or HBM bandwidth pays for it only under that load --
+    isolated timing never sees it. ``alone`` keeps the uncontended median of the last call for the table."""
 
-    def __init__(self, cuda):
+    def __init__(self, cuda, contend=True):
         self.cuda = cuda
+        self.contend = bool(contend) and cuda
+        self.alone = None
+        self._gemm = None
+
+    def _load(self, ms):
+        """Queue GEMMs on the side stream covering ~2x ``ms`` of work (the collective then runs under load)."""
+        if self._gemm is None:
+            a = torch.randn(4096, 4096, device="cuda").to(torch.bfloat16)
+            st = torch.cuda.Stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(st):
+                torch.mm(a, a)
+                e0.record(st)
+                for _ in range(4):
+                    torch.mm(a, a)
+                e1.record(st)
+            e1.synchronize()
+            self._gemm = (a, st, max(1e-3, e0.elapsed_time(e1) / 4))
+        a, st, per = self._gemm
+        n = max(2, min(256, int(2 * ms / per) + 2))
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            for _ in range(n):
+                torch.mm(a, a)
+        return st
+
+    def _one(self, fn, load_ms=None):
+        if not self.cuda:
+            t0 = time.perf_counter()
+            fn()
+            return (time.perf_counter() - t0) * 1e3
+        torch.cuda.synchronize()
+        st = self._load(load_ms) if load_ms is not None else None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        if st is not None:
+            st.synchronize()
+        return e0.elapsed_time(e1)
 
     def run(self, fn, iters, transport=None):
         """Median milliseconds of ``fn`` (issue + wait), after one untimed call (``transport``: for stub timers)."""
         fn()
-        ts = []
-        for _ in range(iters):
-            if self.cuda:
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                fn()
-                e1.record()
-                e1.synchronize()
-                ts.append(e0.elapsed_time(e1))
-            else:
-                t0 = time.perf_counter()
-                fn()
-                ts.append((time.perf_counter() - t0) * 1e3)
-        ts.sort()
+        alone = sorted(self._one(fn) for _ in range(iters))
+        self.alone = alone[len(alone) // 2]
+        if not self.contend:
+            return self.alone
+        ts = sorted(self._one(fn, load_ms=self.alone) for _ in range(iters))
         return ts[len(ts) // 2]
 
 
@@ -115,21 +150,34 @@ def _issue(kind, transport, out, inp, group, comm):
             comm.reduce_scatter_tensor(out, inp)
 
 
+def _native_factory(kind, group, max_bytes, device):
+    if device.type != "cuda":
+        raise RuntimeError("needs a GPU")
+    if _shared_device(group, device):  # collective, same answer on every rank
+        raise RuntimeError("two ranks of the group on one GPU (RCCL refuses a communicator over them)")
+    from ...comm.native_rccl import RcclCommunicator
+    return RcclCommunicator(group)  # failure-symmetric setup (comm/setup.py)
+
+
+def _symmetric_factory(kind, group, max_bytes, device):
+    if device.type != "cuda":
+        raise RuntimeError("needs a GPU")
+    from ...comm import symmetric
+    if not symmetric.supported(group):  # collective: same-node check
+        raise RuntimeError("group is not one node of <= 8 ranks")
+    return symmetric.SymmetricMemory(group, max_bytes)  # failure-symmetric setup (comm/setup.py)
+
+
+# transport -> factory(kind, group, max_bytes, device) -> communicator. A factory may only raise BEFORE its first
+# collective if the condition is the same on every rank; after that its collectives must be failure-symmetric.
+FACTORIES = {"native": _native_factory, "symmetric": _symmetric_factory}
+
+
 def _setup(transport, kind, group, max_bytes, device):
     """The communicator object of ``transport`` for ``group`` (None for rccl), or raise."""
     if transport == "rccl":
         return None
-    if device.type != "cuda":
-        raise RuntimeError("needs a GPU")
-    if transport == "native":
-        if _shared_device(group, device):
-            raise RuntimeError("two ranks of the group on one GPU (RCCL refuses a communicator over them)")
-        from ...comm.native_rccl import RcclCommunicator
-        return RcclCommunicator(group)
-    from ...comm import symmetric
-    if not symmetric.supported(group):  # collective: same-node check
-        raise RuntimeError("group is not one node of <= 8 ranks")
-    return symmetric.SymmetricMemory(group, max_bytes)
+    return FACTORIES[transport](kind, group, max_bytes, device)
 
 
 def select_unit_transports(units, device, lp_dtype, rs_dtype, transports=TRANSPORTS, iters=5, max_symm_bytes=1 << 30,
@@ -155,8 +203,6 @@ def select_unit_transports(units, device, lp_dtype, rs_dtype, transports=TRANSPO
             need = sizes[0]  # a symmetric buffer holds one rank's all-gather shard / one full reduce-scatter input
             if tr == "symmetric" and need > max_symm_bytes:
                 ok, why = False, "larger than the symmetric buffer limit"
-            if ok and tr != "rccl" and device.type != "cuda":
-                ok, why = False, "needs a GPU"
             if ok:
                 try:
                     ck = (tr, gid) if tr == "native" else (tr, kind, gid)
@@ -166,8 +212,7 @@ def select_unit_transports(units, device, lp_dtype, rs_dtype, transports=TRANSPO
                         shared[ck] = comm
                 except Exception as e:  # noqa: BLE001 -- an unavailable transport drops out of the table
                     ok, why = False, f"{type(e).__name__}: {e}"[:160]
-            if device.type == "cuda" or tr == "rccl":
-                ok = _agree_min(ok, group, device)  # usable only if it set up on EVERY rank
+            ok = _agree_min(ok, group, device)  # usable only if it set up on EVERY rank
             if ok:
                 avail[tr] = comm
             else:
@@ -207,6 +252,8 @@ def select_unit_transports(units, device, lp_dtype, rs_dtype, transports=TRANSPO
                 ms = timer.run(lambda tr=tr, comm=comm: _issue(kind, tr, out, inp, group, comm), iters, transport=tr)
                 ms = _agree_max(ms, group, device)  # the slowest rank paces a collective
                 row["ms"][tr] = round(ms, 4)
+                if getattr(timer, "alone", None) is not None and getattr(timer, "contend", False):
+                    row.setdefault("ms_alone", {})[tr] = round(_agree_max(timer.alone, group, device), 4)
                 # nccl-tests bus-bandwidth factor (W-1)/W of the full message
                 row["busbw_GBps"][tr] = round(nb * world * (world - 1) / world / (ms * 1e-3) / 1e9, 1) if ms else None
             timed = {k: v for k, v in row["ms"].items() if v is not None}

@@ -253,6 +253,47 @@ def test_offload_adam_states_host_step(world, ratio):
     run_distributed(_state_host_step_run, world, ratio)
 
 
+def _state_host_step_fp16_run(rank, world):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(tiny(**TINY))
+    # dynamic loss scaling starting far too high: the first steps overflow (skipped), later ones step -- every
+    # non-skipped step reaches the host tails with a (zero) found_inf flag
+    cfg = {"train_micro_batch_size_per_gpu": 2, "fp16": {"enabled": True, "loss_scale": 0, "initial_scale_power": 32,
+                    "hysteresis": 1},
+           "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}, "zero_optimization": {"stage": 3},
+           "compile": {"offload_opt_states": True}}
+    eng, _, _, _ = ds.initialize(model=m, config=cfg)
+    eng.compile(compile_kwargs={"offload_states_ratio": 0.5, "offload_states_chunk_mb": 0.05,
+                                "offload_states_host_step": True})
+    z = eng.optimizer
+    g = torch.Generator().manual_seed(5 + rank)
+    applied = 0
+    for _ in range(24):
+        x = torch.randint(0, TINY["vocab_size"], (2, 12), generator=g)
+        loss = eng(x, labels=x)
+        eng.backward(loss)
+        eng.step()
+        applied += int(not z.overflow)
+        assert torch.isfinite(loss.float())
+    so = z.state_offload
+    assert applied >= 1 and so.host_step and so.host_steps >= applied - 1, (applied, so.host_step, getattr(so, "host_steps", 0), so.stats())
+    # a set skip flag (symmetric-memory failure, or an overflow folded on the device) leaves the host tails alone
+    before = so.host["master"].clone()
+    lp = z.store.lp.clone()
+    pieces = [(so.a, z.store.numel, z.param_groups[0])]
+    so.step_on_host(pieces, 1.0, lp, found_inf=torch.ones(1), lp_cur=z.store.lp)
+    assert torch.equal(before, so.host["master"]) and so.host_skips == 1
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_offload_adam_states_host_step_fp16_dynamic(world):
+    """Host-step tails under fp16 dynamic loss scaling: found_inf is a device flag on every step (it used to send
+    the step down the device path, which indexed the host tails' missing device chunks)."""
+    run_distributed(_state_host_step_fp16_run, world)
+
+
 def test_param_offload_plan():
     """offload_parameters pass: units fetched in both phases are kept on the device first, then the smallest, within
     the budget; units with no fetch are ignored."""

@@ -195,7 +195,7 @@ def test_graph_decode_captures_latents_for_restore_gpu(latent_mode):
         assert torch.equal(tr, te), j  # the capturing graph computes exactly what the plain graph computes
         fed.append(te.clone())
         lr, _ = ref.put([1], [tr], capture_latents=False)
-        le, lat = eng.put([1], [te])  # graph decode, latents deferred to the ring
+        le, lat = eng.put([1], [te], sync_latents=False)  # graph decode, latents deferred to the ring
         steps.append(lat[0])
         tr, te = lr.argmax(-1).cpu(), le.argmax(-1).cpu()
     assert (1, True) in eng._model._decode_graphs and (1, False) in ref._model._decode_graphs

@@ -552,20 +552,29 @@ def test_step_peak_survives_per_block_resets(monkeypatch):
     assert c.stash_keep_from == 10 - 6
 
 
-def test_blit_limit_check_branches(monkeypatch):
-    """A spilling host activation cache refuses to start when DEBUG_CLR_LIMIT_BLIT_WG did not reach the HIP runtime
-    (a script that imported torch first); recompute-only, the explicit opt-out and the in-effect case pass."""
+def test_blit_limit_check_branches(monkeypatch, caplog):
+    """A spilling host activation cache warns (strict mode: refuses to start) when DEBUG_CLR_LIMIT_BLIT_WG did not
+    reach the HIP runtime (a script that imported torch first); recompute-only, the explicit opt-out and the
+    in-effect case pass silently."""
+    import logging
     import types
     from hcache_deepspeed_amd.offload.activation_cache import BlitLimitError, check_blit_limit
     monkeypatch.delenv("HDS_ALLOW_UNLIMITED_BLIT", raising=False)
+    monkeypatch.delenv("HDS_STRICT_BLIT", raising=False)
     cfg = types.SimpleNamespace(policy="ckpt_offload", allow_unlimited_blit=False)
     check_blit_limit(cfg, "cuda", limit_in_effect=True)
     check_blit_limit(cfg, "cpu", limit_in_effect=False)  # CPU tensors: no blit kernels
-    with pytest.raises(BlitLimitError, match="DEBUG_CLR_LIMIT_BLIT_WG"):
+    from hcache_deepspeed_amd.utils.logging import logger
+    logger.propagate = True
+    with caplog.at_level(logging.WARNING):
+        check_blit_limit(cfg, "cuda", limit_in_effect=False)  # default: loud warning, run continues
+    assert "DEBUG_CLR_LIMIT_BLIT_WG" in caplog.text
+    for pol in ("budget", "plan", "auto", "all", "ckpt_offload"):
+        with pytest.raises(BlitLimitError, match="DEBUG_CLR_LIMIT_BLIT_WG"):
+            check_blit_limit(types.SimpleNamespace(policy=pol, strict_blit_limit=True), "cuda", limit_in_effect=False)
+    monkeypatch.setenv("HDS_STRICT_BLIT", "1")
+    with pytest.raises(BlitLimitError):
         check_blit_limit(cfg, "cuda", limit_in_effect=False)
-    for pol in ("budget", "plan", "auto", "all"):
-        with pytest.raises(BlitLimitError):
-            check_blit_limit(types.SimpleNamespace(policy=pol), "cuda", limit_in_effect=False)
     check_blit_limit(types.SimpleNamespace(policy="recompute"), "cuda", limit_in_effect=False)
     check_blit_limit(types.SimpleNamespace(policy="plan", allow_unlimited_blit=True), "cuda", limit_in_effect=False)
     monkeypatch.setenv("HDS_ALLOW_UNLIMITED_BLIT", "1")
@@ -607,3 +616,13 @@ def test_first_plan_keeps_the_copy_window_free():
     c.step_peak_history = [x * GB for x in (10, 50, 60)]
     assert c.stats()["step_peaks_gib"] == [10.0, 50.0, 60.0]
     assert HostActivationCache(torch.device("cpu")).plan_budget() is None
+
+
+def test_state_offload_shared_allocation_drains_as_one():
+    """Tail chunks that are views of ONE allocation (the reload arena, or a whole state split the first time) free
+    their HBM only when the last of them drains: the draining queue holds one entry for them, at the last chunk's
+    event, with all their bytes; separately allocated chunks keep one entry each."""
+    from hcache_deepspeed_amd.runtime.zero.state_offload import OptimizerStateOffload
+    issued = [("e0", 10, "arena"), ("e1", 20, "own1"), ("e2", 30, "arena"), ("e3", 5, "own2"), ("e4", 7, "arena")]
+    assert OptimizerStateOffload._merge_shared(issued) == [("e1", 20), ("e3", 5), ("e4", 47)]
+    assert OptimizerStateOffload._merge_shared([("a", 1, 1), ("b", 2, 2)]) == [("a", 1), ("b", 2)]

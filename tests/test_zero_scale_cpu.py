@@ -203,6 +203,13 @@ def test_bench_torchrun_cpu_dry_run():
     assert iso["all_gather_busbw_GBps"] >= 0 and iso["reduce_scatter"]["samples"]
     # bucket sizes default to "auto" at N > 1: the alpha-beta fit of the data-parallel all-gather is reported
     assert comm["rank0"]["auto_bucket_fit"]["samples"] and comm["rank0"]["xgmi_bucket_mb"] >= 16
+    # torchrun forced OMP_NUM_THREADS=1: every rank took its share of the host's CPUs for the host kernels instead
+    from hcache_deepspeed_amd.utils.numa import _cgroup_cpu_budget, rank_core_slice
+    want = len(rank_core_slice(0, W, budget=_cgroup_cpu_budget()))
+    assert comm["host_threads_per_rank"][0] == want and all(t >= 1 for t in comm["host_threads_per_rank"])
+    ht = out["extra"]["host_threads"]
+    assert ht["source"] == "auto" and ht["local_world"] == W and ht.get("host_kernel_threads", want) == want
+    assert out["extra"]["mfu_causal"] <= out["extra"]["mfu_bf16_dense_2.5PF"]
 
 
 def test_memory_plan_bench_configs():

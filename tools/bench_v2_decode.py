@@ -41,14 +41,14 @@ def main():
             logits, _ = eng.put(uids, prompts, capture_latents=cap)
             nxt = logits.argmax(-1).cpu()
             for _ in range(2):  # graph capture of this batch size outside the timed loop
-                logits, _ = eng.put(uids, [nxt[i:i + 1] for i in range(B)], capture_latents=cap)
+                logits, _ = eng.put(uids, [nxt[i:i + 1] for i in range(B)], capture_latents=cap, sync_latents=False)
                 nxt = logits.argmax(-1).cpu()
             eng.wait_latents()
             torch.cuda.synchronize()
             kept = []
             t0 = time.perf_counter()
             for _ in range(steps):
-                logits, lats = eng.put(uids, [nxt[i:i + 1] for i in range(B)], capture_latents=cap)
+                logits, lats = eng.put(uids, [nxt[i:i + 1] for i in range(B)], capture_latents=cap, sync_latents=False)
                 kept.append(lats)
                 nxt = logits.argmax(-1).cpu()
             eng.wait_latents()
