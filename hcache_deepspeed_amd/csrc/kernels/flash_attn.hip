@@ -1419,16 +1419,25 @@ AttnParams make_params(const void* q, const void* k, const void* v, void* o, flo
 
 int g_fwd_nw = 8, g_dkdv_nw = 8, g_dq_nw = 8, g_fwd_var = 20, g_bwd_prio = 1, g_bwd_pipe = 0, g_dq_var = 0;
 
-// forward variant bits (see attn_fwd_kernel): 0 = baseline, 1 = static priority, 2 = deferred max, 3 = both;
-// 4 = staggered wave groups (attn_fwd_stg_kernel, deferred max); 5 = software-pipelined softmax (attn_fwd_sp_kernel);
-// 6 = 5 without the full-tile DMA fast path; 7 = 5 + per-wave skip of the causal tiles above its queries;
-// 8 = 5 with 4-wave workgroups (two per CU); 9 = one wave per SIMD, 64 rows per wave (attn_fwd_w64_kernel);
-// 10 = 9 with the softmax VALU split over both MFMA blocks; 11 = 10 with block A hand-scheduled (asm S MFMAs, Q in AGPRs); 12 = 11 + cycle stamps (diagnostic); 13 / 14 = timing-only diagnostics of 12 (no exp / DMA in block B)
+// forward variants (hds_attn_fwd_variant). Shipped library: 20 = one wave per SIMD, 64 rows per wave, hand-scheduled
+// MFMA blocks (flash_attn_w64.hip, the default); 5 = 8 waves, software-pipelined softmax (attn_fwd_sp_kernel, the
+// fallback); 2 = 8 waves, deferred max (attn_fwd_kernel; the head dims other than 128 always run it).
+// The A/B build (ops/build.py build_kernels_diag: -DHDS_FA_DIAG=1, its own .so) adds the experiment variants:
+// 0/1/3 = attn_fwd_kernel priority / deferred-max bits, 4 = staggered wave groups, 6-8 = variant-5 ablations,
+// 9-11/18 = earlier one-wave-per-SIMD schedules, 12/19/21 = cycle stamps, 13-17 = timing-only diagnostics (WRONG
+// results). The shipped library rejects every one of them, so no setting can select a wrong-result kernel.
 HDS_EXPORT int hds_attn_fwd_variant(int var) {
+#if HDS_FA_DIAG
   if (var < 0 || var > 21) return hipErrorInvalidValue;
+#else
+  if (var != 2 && var != 5 && var != 20) return hipErrorInvalidValue;
+#endif
   g_fwd_var = var;
   return 0;
 }
+
+// 1 when this library carries the A/B experiment / diagnostic variants (never the shipped one)
+HDS_EXPORT int hds_attn_diag_build() { return HDS_FA_DIAG ? 1 : 0; }
 
 // backward: dK/dV kernel with LDS reads pipelined two MFMAs ahead (0 / 1; head_dim 128)
 HDS_EXPORT int hds_attn_bwd_pipe(int on) {
@@ -1467,8 +1476,10 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
       const dim3 grid((max_len + 255) / 256, hq, batch);
       if constexpr (D == 128) {  // the A/B variants exist for the training head dim only
         switch (g_fwd_var) {
-          case 4: hipLaunchKernelGGL((attn_fwd_stg_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 5: hipLaunchKernelGGL((attn_fwd_sp_kernel<D>), grid, dim3(512), 0, st, p); break;
+          case 20: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 11, st);
+#if HDS_FA_DIAG
+          case 4: hipLaunchKernelGGL((attn_fwd_stg_kernel<D>), grid, dim3(512), 0, st, p); break;
           case 6: hipLaunchKernelGGL((attn_fwd_sp_kernel<D, false>), grid, dim3(512), 0, st, p); break;
           case 7: hipLaunchKernelGGL((attn_fwd_sp_kernel<D, true, true>), grid, dim3(512), 0, st, p); break;
           case 8:
@@ -1486,11 +1497,11 @@ int launch_fwd(const AttnParams& p, int batch, int max_len, int hq, hipStream_t 
           case 17: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 8, st);
           case 18: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 9, st);
           case 19: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 10, st);
-          case 20: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 11, st);
           case 21: return hds_attn_fwd_w64_launch(&p, sizeof(p), batch, max_len, hq, 12, st);
           case 0: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 0>), grid, dim3(512), 0, st, p); break;
           case 1: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 1>), grid, dim3(512), 0, st, p); break;
           case 3: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 3>), grid, dim3(512), 0, st, p); break;
+#endif
           default: hipLaunchKernelGGL((attn_fwd_kernel<D, 8, 2>), grid, dim3(512), 0, st, p); break;
         }
       } else {

@@ -2,6 +2,12 @@
 // sequence / mask helpers and the LDS read wrappers. Anonymous namespace: every TU has its own copy; the
 // parameter block crosses TUs only as bytes of this one definition (hds_attn_fwd_w64_launch).
 #pragma once
+// A/B experiment build of the FlashAttention units (ops/build.py build_kernels_diag): 1 adds the earlier forward
+// schedules, the cycle-stamp builds and the timing-only (wrong-result) diagnostics to a separate library. The shipped
+// library is built without it and carries none of them.
+#ifndef HDS_FA_DIAG
+#define HDS_FA_DIAG 0
+#endif
 #include <type_traits>
 #include <utility>
 

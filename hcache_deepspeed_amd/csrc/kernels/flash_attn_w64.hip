@@ -60,7 +60,9 @@ __device__ __forceinline__ uint64_t memtime_stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
+#if HDS_FA_DIAG
 __device__ unsigned long long g_w64_stamps[4][8];  // per wave index: segment cycles, tiles, waves (summed)
+#endif
 constexpr float kMaskPen = 1048576.f;  // 2^20, times the -1 of a masked score (see mask_tile)
 __device__ __forceinline__ void xdl_drain() { asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 3" ::: "memory"); }
 
@@ -585,6 +587,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     if (kt < kt_end) tile(std::integral_constant<int, 0>{}, kt);
     stamp(std::integral_constant<int, 4>{});
+#if HDS_FA_DIAG
     if constexpr (STAMPS) {
       st_acc[5] = st_prev - st_t0;  // the whole loop
       if (lane == 0) {
@@ -594,6 +597,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         atomicAdd(&g_w64_stamps[w][7], 1ull);
       }
     }
+#endif
   } else {
   stage(smem + 0, p.k, p.sk, dk, kt_begin);
   stage(smem + 2 * TL, p.v, p.sv, dv, kt_begin);
@@ -758,6 +762,8 @@ int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, 
   const AttnParams& p = *static_cast<const AttnParams*>(params);
   const dim3 grid((max_len + 255) / 256, hq, batch);
   switch (mode) {
+    case 11: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 11>), grid, dim3(256), 0, st, p); break;
+#if HDS_FA_DIAG
     case 0: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 0>), grid, dim3(256), 0, st, p); break;
     case 1: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 1>), grid, dim3(256), 0, st, p); break;
     case 2: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 2>), grid, dim3(256), 0, st, p); break;
@@ -769,12 +775,14 @@ int hds_attn_fwd_w64_launch(const void* params, size_t params_bytes, int batch, 
     case 8: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 8>), grid, dim3(256), 0, st, p); break;
     case 9: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 9>), grid, dim3(256), 0, st, p); break;
     case 10: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 10>), grid, dim3(256), 0, st, p); break;
-    case 11: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 11>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 12>), grid, dim3(256), 0, st, p); break;
+    case 12: hipLaunchKernelGGL((attn_fwd_w64_kernel<128, 12>), grid, dim3(256), 0, st, p); break;
+#endif
+    default: return hipErrorInvalidValue;  // the shipped library holds only the default schedule (MODE 11)
   }
   return hipGetLastError();
 }
 
+#if HDS_FA_DIAG
 // variant 12's (19's, 21's) stamps, out[32] = 4 wave indices x 8: [0..4] cycles per segment (DMA wait + barrier, block A, mask,
 // block B, tail), [5] the whole loop, [6] tiles, [7] waves -- summed over the workgroups. reset != 0 zeroes them after.
 HDS_EXPORT int hds_attn_w64_stamps(unsigned long long* out, int reset) {
@@ -785,3 +793,4 @@ HDS_EXPORT int hds_attn_w64_stamps(unsigned long long* out, int reset) {
   }
   return e;
 }
+#endif

@@ -116,6 +116,19 @@ def build_kernels(force=False, jobs=None, verbose=False, file_flags=None, out=No
     return lib_path
 
 
+DIAG_LIB = os.path.join(os.path.dirname(KERNEL_LIB), "libhds_kernels_diag.so")
+
+
+def build_kernels_diag(force=False, jobs=None, verbose=False):
+    """The A/B experiment library: the FlashAttention units built with -DHDS_FA_DIAG=1 (earlier forward schedules,
+    cycle-stamp builds, timing-only diagnostics with WRONG results) into ``_lib/libhds_kernels_diag.so``. Never the
+    library the package loads by default; tools load it with HDS_KERNEL_LIB=<path> (tools/fa_stamps.py)."""
+    flags = {k: list(v) for k, v in FILE_FLAGS.items()}
+    for f in ("flash_attn.hip", "flash_attn_w64.hip", "flash_attn_bwd_w64.hip"):
+        flags[f] = flags.get(f, []) + ["-DHDS_FA_DIAG=1"]
+    return build_kernels(force=force, jobs=jobs, verbose=verbose, file_flags=flags, out=DIAG_LIB)
+
+
 def build_host(force=False, verbose=False):
     srcs = _sources("host", (".cpp",))
     hdrs = _sources("host", (".h",))

@@ -45,7 +45,8 @@ _KERNEL_SIGS = {
     "hds_attn_config": "iii",
     "hds_attn_fwd_variant": "i",
     "hds_attn_bwd_dq_variant": "i",
-    "hds_attn_w64_stamps": "pi",
+    "hds_attn_w64_stamps": "pi",  # A/B library only (build_kernels_diag)
+    "hds_attn_diag_build": "",
     "hds_attn_bwd_prio": "i",
     "hds_attn_bwd_pipe": "i",
     "hds_bsattn_fwd": "p" * 8 + "i" * 7 + "f" + "i" + "s",
@@ -161,16 +162,29 @@ def load_kernels(build_if_missing=True):
         # FlashAttention forward variant (csrc/kernels/flash_attn.hip hds_attn_fwd_variant): 11 = one wave per SIMD,
         # 64 rows per wave, hand-scheduled MFMA blocks (flash_attn_w64.hip; 1.074-1.077 ms vs 1.109-1.116 for the
         # 8-wave software-pipelined variant 5 at the bench shape, profiles/r5/fa_fwd_variants_idle_tiles_r5w.log)
-        lib.hds_attn_fwd_variant(fwd_variant_default())
+        check(lib.hds_attn_fwd_variant(fwd_variant_default()), "hds_attn_fwd_variant")
         # FlashAttention backward dQ kernel (hds_attn_bwd_dq_variant; 1 = one wave per SIMD, 64 rows per wave)
         lib.hds_attn_bwd_dq_variant(int(os.environ.get("HDS_ATTN_DQ_VAR", "0")))
         _klib = lib
         return _klib
 
 
+# FlashAttention forward variants of the shipped library (flash_attn.hip hds_attn_fwd_variant): 20 the default, 5 the
+# 8-wave fallback, 2 the generic 8-wave kernel. The experiment / diagnostic variants exist only in the A/B library
+# (ops/build.py build_kernels_diag, loaded through HDS_KERNEL_LIB), where HDS_ATTN_FWD_VAR may name them.
+SHIPPED_FWD_VARIANTS = (2, 5, 20)
+
+
 def fwd_variant_default():
-    """The FlashAttention forward variant the library is loaded with (``HDS_ATTN_FWD_VAR`` overrides)."""
-    return int(os.environ.get("HDS_ATTN_FWD_VAR", "20"))
+    """The FlashAttention forward variant the library is loaded with (``HDS_ATTN_FWD_VAR`` overrides; a variant the
+    shipped library does not carry raises instead of silently running something else)."""
+    var = int(os.environ.get("HDS_ATTN_FWD_VAR", "20"))
+    diag = os.path.basename(os.environ.get("HDS_KERNEL_LIB", "")) == os.path.basename(_build.DIAG_LIB)
+    if var not in SHIPPED_FWD_VARIANTS and not diag:
+        raise ValueError(f"HDS_ATTN_FWD_VAR={var}: the shipped FlashAttention library has forward variants "
+                         f"{SHIPPED_FWD_VARIANTS}; experiment / diagnostic variants need the A/B library "
+                         f"(ops/build.py build_kernels_diag, HDS_KERNEL_LIB={_build.DIAG_LIB})")
+    return var
 
 
 def kernels():

@@ -66,3 +66,26 @@ def test_host_signatures_match_exports():
            if n in ex and len(a) != len(ex[n])]
     missing = [n for n in host_sigs.SIGS if n not in ex]
     assert not bad and not missing, (bad, missing)
+
+
+def test_shipped_fa_variants_only(monkeypatch):
+    """HDS_ATTN_FWD_VAR may name only a forward variant the shipped library carries (2, 5, 20): a diagnostic or
+    experiment variant raises instead of selecting a wrong-result kernel; the A/B library accepts it."""
+    import pytest
+    from hcache_deepspeed_amd.ops import build
+    monkeypatch.delenv("HDS_KERNEL_LIB", raising=False)
+    for v in ("2", "5", "20"):
+        monkeypatch.setenv("HDS_ATTN_FWD_VAR", v)
+        assert native.fwd_variant_default() == int(v)
+    for v in ("13", "12", "11", "4"):
+        monkeypatch.setenv("HDS_ATTN_FWD_VAR", v)
+        with pytest.raises(ValueError, match="shipped FlashAttention library"):
+            native.fwd_variant_default()
+    monkeypatch.setenv("HDS_KERNEL_LIB", build.DIAG_LIB)
+    monkeypatch.setenv("HDS_ATTN_FWD_VAR", "13")
+    assert native.fwd_variant_default() == 13
+    src = open(os.path.join(os.path.dirname(native.__file__), "..", "csrc", "kernels", "flash_attn_w64.hip")).read()
+    # the shipped launcher instantiates only the default schedule outside the HDS_FA_DIAG block
+    launch = src[src.index("int hds_attn_fwd_w64_launch"):]
+    shipped = launch[:launch.index("#if HDS_FA_DIAG")]
+    assert "attn_fwd_w64_kernel<128, 11>" in shipped and shipped.count("attn_fwd_w64_kernel<") == 1

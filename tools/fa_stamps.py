@@ -1,11 +1,20 @@
 """Where a one-wave-per-SIMD forward tile spends its cycles: run forward variant 12 (variant 11 + s_memtime stamps at
-the block boundaries) at the bench shape and print cycles per tile and wave for each segment."""
+the block boundaries) at the bench shape and print cycles per tile and wave for each segment.
+
+Stamps live only in the A/B experiment library: build it with
+``python -c "from hcache_deepspeed_amd.ops import build; build.build_kernels_diag()"`` (this script does it) and run
+with ``HDS_KERNEL_LIB=hcache_deepspeed_amd/_lib/libhds_kernels_diag.so``."""
 import ctypes
+import os
 import sys
 
 import torch
 
 sys.path.insert(0, ".")
+from hcache_deepspeed_amd.ops import build as _build  # noqa: E402
+
+if not os.environ.get("HDS_KERNEL_LIB"):
+    os.environ["HDS_KERNEL_LIB"] = _build.build_kernels_diag()
 from hcache_deepspeed_amd.ops import native  # noqa: E402
 from hcache_deepspeed_amd.ops.attention import flash_attn  # noqa: E402
 
