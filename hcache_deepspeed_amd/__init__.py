@@ -58,6 +58,33 @@ from .inference.engine import InferenceEngine  # noqa: F401
 from .inference.config import DeepSpeedInferenceConfig  # noqa: F401
 from .ops.transformer import DeepSpeedTransformerConfig, DeepSpeedTransformerLayer  # noqa: F401
 from .module_inject import replace_transformer_layer, revert_transformer_layer, set_autotp_mode  # noqa: F401
+from . import comm as dist  # noqa: F401  (reference: ``deepspeed.dist``)
+from typing import Callable as _Callable, Dict as _Dict, Iterable as _Iterable, Union as _Union
+
+import torch as _torch
+
+TORCH_DISTRIBUTED_DEFAULT_PORT = 29500
+ADAM_OPTIMIZER, LAMB_OPTIMIZER = "adam", "lamb"  # reference runtime/config.py optimizer-name constants
+# reference __init__.py:30-31: what ``initialize(optimizer=..., lr_scheduler=...)`` accepts besides instances
+DeepSpeedOptimizerCallable = _Callable[[_Union[_Iterable[_torch.nn.Parameter], _Dict[str, _Iterable]]],
+                                       _torch.optim.Optimizer]
+DeepSpeedSchedulerCallable = _Callable[[_torch.optim.Optimizer], _torch.optim.lr_scheduler.LRScheduler]
+
+
+def _git_info():
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        h = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=root, capture_output=True, text=True,
+                           timeout=5).stdout.strip()
+        b = subprocess.run(["git", "rev-parse", "--abbrev-ref", "HEAD"], cwd=root, capture_output=True, text=True,
+                           timeout=5).stdout.strip()
+        return h or "unknown", b or "unknown"
+    except Exception:  # noqa: BLE001 -- no git in the environment
+        return "unknown", "unknown"
+
+
+git_hash, git_branch = _git_info()
 from .runtime import domino  # noqa: F401
 
 version = __version__

@@ -160,6 +160,7 @@ class HostActivationCache:
         self._steps_seen = 0
         self._capped_this_step = 0
         self._attached = []
+        self._wrapped = []  # blocks whose forward attach() wrapped (restored by detach)
         self._cal_bytes = {}  # per-layer eligible bytes measured by the calibration step
         self._turn_peak = None  # max allocation at the forward/backward turn-around of the last step
         self.plan_adjustments = 0
@@ -215,9 +216,24 @@ class HostActivationCache:
             self._attached.append(b.register_forward_pre_hook(lambda mod, args, i=i: self._enter(i)))
             if self.policy_recompute:
                 b.forward = self._recompute_wrapper(b.forward, i)
+                self._wrapped.append(b)
             elif self.ckpt_offload:
                 b.forward = self._ckpt_offload_wrapper(b.forward)
+                self._wrapped.append(b)
         return self
+
+    def detach(self):
+        """Undo ``attach`` (engine.destroy()): remove the block hooks, restore the blocks' own forwards, drop the
+        pinned pool's buffers."""
+        for h in self._attached:
+            h.remove()
+        self._attached = []
+        for b in self._wrapped:
+            b.__dict__.pop("forward", None)
+        self._wrapped = []
+        pool = getattr(self, "pool", None)
+        if pool is not None and hasattr(pool, "clear"):
+            pool.clear()
 
     def _ckpt_offload_wrapper(self, fwd):
         from ..runtime.activation_checkpointing import checkpointing as ck

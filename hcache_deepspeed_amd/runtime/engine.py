@@ -20,6 +20,7 @@ from ..utils.timer import NoopTimer, SynchronizedWallClockTimer, ThroughputTimer
 from . import lr_schedules
 from .config import DeepSpeedConfig
 from .dataloader import DeepSpeedDataLoader
+from .engine_api import EngineApiMixin
 from .zero.optimizer import ZeroOptimizer
 
 FORWARD_MICRO_TIMER = "fwd_microstep"
@@ -67,7 +68,7 @@ def _truncate_seqlen(inputs, kwargs, d):
     return tuple(cut(t) for t in inputs), {k: cut(v) for k, v in kwargs.items()}
 
 
-class DeepSpeedEngine(nn.Module):
+class DeepSpeedEngine(EngineApiMixin, nn.Module):
 
     def __init__(self, args=None, model=None, optimizer=None, model_parameters=None, training_data=None,
                  lr_scheduler=None, mpu=None, dist_init_required=None, collate_fn=None, config=None,
@@ -414,9 +415,14 @@ class DeepSpeedEngine(nn.Module):
         if scale_wrt_gas and self.gradient_accumulation_steps() > 1:
             loss = loss / self.gradient_accumulation_steps()
         boundary = self.is_gradient_accumulation_boundary() and not self._is_in_no_sync
-        self.optimizer.prepare_backward(boundary)
-        self.optimizer.backward(loss, retain_graph=retain_graph)
-        self.optimizer.finish_backward()
+        z = self.optimizer
+        hold = not allreduce_gradients and self.zero_optimization_stage() < 3 and hasattr(z, "hold_reduction")
+        if hold:  # reduced by a later engine.allreduce_gradients() (reference engine.py:2245)
+            self._pipe_hold = bool(z.hold_reduction)
+            z.hold_reduction = True
+        z.prepare_backward(boundary)
+        z.backward(loss, retain_graph=retain_graph)
+        z.finish_backward()
         self.timers(BACKWARD_MICRO_TIMER).stop()
         if self.monitor.enabled and dist.get_rank() == 0 and boundary:
             self.summary_events = [("Train/Samples/train_loss", float(loss.detach().item()), self.global_samples)]
@@ -437,7 +443,10 @@ class DeepSpeedEngine(nn.Module):
         self.timers(STEP_MICRO_TIMER).start()
         boundary = self.is_gradient_accumulation_boundary()
         if boundary:
+            if getattr(self.optimizer, "_held", None):  # backward(allreduce_gradients=False) without the call
+                self.allreduce_gradients()
             ok = self.optimizer.step()
+            self._step_applied = ok is not False
             if ok is False:
                 self.skipped_steps += 1
             elif self.lr_scheduler is not None:
@@ -525,7 +534,14 @@ class DeepSpeedEngine(nn.Module):
                                load_lr_scheduler_states, load_module_only)
 
     def save_16bit_model(self, save_dir, save_filename="pytorch_model.bin", exclude_frozen_parameters=False):
+        """Consolidated 16-bit weights. Under ZeRO-3 this needs ``stage3_gather_16bit_weights_on_model_save``, as in
+        the reference (engine.py:3835): without it nothing is gathered and False is returned."""
         from .checkpointing import save_16bit_model
+        if self.zero_optimization_partition_weights() and getattr(self.optimizer, "partitioned", False) and \
+                not self.zero_gather_16bit_weights_on_model_save():
+            logger.warning("Did not save the model: zero_optimization.stage3_gather_16bit_weights_on_model_save is "
+                           "false under ZeRO-3 (use zero_to_fp32 on a checkpoint instead)")
+            return False
         return save_16bit_model(self, save_dir, save_filename)
 
     def module_state_dict(self, destination=None, prefix="", keep_vars=False, exclude_frozen_parameters=False):

@@ -39,6 +39,7 @@ class PipelineEngine(DeepSpeedEngine):
         self.next_rank = self.grid.stage_to_global(self.stage_id + 1) if self.stage_id < self.num_stages - 1 \
             else None
         self.has_bool_tensors = has_bool_tensors
+        self.has_attention_mask = False
         self.data_iterator = None
         self.batch_fn = None
         self.pipe_buffers = {}
@@ -47,6 +48,8 @@ class PipelineEngine(DeepSpeedEngine):
         self.total_loss = None
         self.agg_train_loss = None
         self.agg_eval_loss = None
+        self.agg_additional_losses = None
+        self._additional_acc = {}
         self._eval_outputs = None
         self._compute_loss = True
         # tensor parallelism inside a stage: every model-parallel rank holds the same activation, so each sends only
@@ -78,6 +81,75 @@ class PipelineEngine(DeepSpeedEngine):
     def set_batch_fn(self, fn):
         self.batch_fn = fn
 
+    # ---- reference PipelineEngine surface (runtime/pipe/engine.py) -----------------------------------------------
+    def set_has_attention_mask(self, value):
+        """The first stage's micro-batch inputs carry an attention mask as their last tensor (sent to the next stage
+        with the activations: the p2p meta describes every tensor of the tuple, bool ones included)."""
+        assert isinstance(value, bool)
+        self.has_attention_mask = value
+
+    def reset_activation_shape(self):
+        """Forget the cached activation / gradient shapes so the next batch re-sends its meta (variable sequence
+        length between batches). Every stage must call it before the same batch."""
+        self._send_meta_done = False
+        self._recv_meta = None
+        self.pipe_buffers = {}
+
+    def set_train_batch_size(self, train_batch_size):
+        super().set_train_batch_size(train_batch_size)
+        self.micro_batches = self.gradient_accumulation_steps()
+
+    def set_dataloader(self, loader):
+        """Data for the stages that read it (first: inputs, last: labels)."""
+        if self.is_first_stage() or self.is_last_stage():
+            self.training_dataloader = loader
+            self.data_iterator = iter(loader)
+
+    def log_for_device(self, *msg):
+        """Print on the rank given by ``LOG_STAGE`` / ``DATA_PARALLEL_ID`` (env, default: stage 0, dp rank 0)."""
+        import os
+        stage = int(os.environ.get("LOG_STAGE", "0"))
+        dp_id = int(os.environ.get("DATA_PARALLEL_ID", "0"))
+        if self.stage_id == stage and self.grid.get_data_parallel_rank() == dp_id:
+            print(f"RANK={dist.get_rank()} PIPE-ID={self.stage_id} DATA-ID={self.grid.get_data_parallel_rank()} "
+                  f"MBATCH-ID={self._mb_index} STEP-ID={self.global_steps}", *msg, flush=True)
+
+    def tput_log(self, *msg):
+        if dist.get_rank() == 0 and self.global_steps % self.steps_per_print() == 0:
+            print(*msg, flush=True)
+
+    def mem_status(self, msg, print_rank=-1, reset_max=False):
+        """Allocated / cached / peak device memory on this rank (``print_rank``: only that global rank)."""
+        if print_rank >= 0 and dist.get_rank() != print_rank:
+            return None
+        if not torch.cuda.is_available():
+            return None
+        if reset_max:
+            torch.cuda.reset_peak_memory_stats()
+        g = 2**30
+        rec = {"allocated_gib": torch.cuda.memory_allocated() / g, "reserved_gib": torch.cuda.memory_reserved() / g,
+               "max_allocated_gib": torch.cuda.max_memory_allocated() / g}
+        print(f"RANK={dist.get_rank()} STAGE={self.stage_id} STEP={self.global_steps} MEMSTATS {msg} "
+              + " ".join(f"{k}={v:.2f}" for k, v in rec.items()), flush=True)
+        return rec
+
+    def load_module_state_dict(self, checkpoint, strict=True, custom_load_fn=None, fetch_z3_params=False):
+        """A state dict (or ``{"module": ...}``) loads through the engine; a directory of layer files (the
+        reference's layer-wise pipeline checkpoint, PipelineModule.save_state_dict) loads per stage."""
+        import os
+        if isinstance(checkpoint, str) and os.path.isdir(checkpoint):
+            self.module.load_state_dir(checkpoint, strict=strict)
+            if self.optimizer is not None:
+                self.optimizer.refresh_fp32_from_lp()
+            return
+        super().load_module_state_dict(checkpoint, strict=strict, custom_load_fn=custom_load_fn,
+                                       fetch_z3_params=fetch_z3_params)
+
+    def get_additional_losses(self):
+        """Extra named losses the last stage's loss function reported (a dict returned next to the loss), averaged
+        over the micro-batches of the last batch; None if it reported none."""
+        return getattr(self, "agg_additional_losses", None)
+
     def is_gradient_accumulation_boundary(self):
         return self._mb_index == self.micro_batches - 1
 
@@ -98,6 +170,7 @@ class PipelineEngine(DeepSpeedEngine):
             self.set_dataiterator(data_iter)
         self.module.train()
         self.total_loss = None
+        self._additional_acc = {}
         self._compute_loss = True
         if getattr(self, "_ac_reset", False):
             from ..activation_checkpointing import checkpointing as _ac
@@ -105,6 +178,8 @@ class PipelineEngine(DeepSpeedEngine):
         sched = S.TrainSchedule(self.micro_batches, self.num_stages, self.stage_id)
         self._exec_schedule(sched)
         self.agg_train_loss = self._aggregate_loss(self.total_loss)
+        self.agg_additional_losses = ({k: v / self.micro_batches for k, v in self._additional_acc.items()}
+                                      if self._additional_acc else None)
         return self.agg_train_loss
 
     def eval_batch(self, data_iter, return_logits=False, compute_loss=True, reduce_output="avg", bcast_loss=True,
@@ -200,6 +275,12 @@ class PipelineEngine(DeepSpeedEngine):
             labels = self.pipe_buffers["labels"].pop(mb, None)
             if self._compute_loss and self.module.loss_fn is not None:
                 loss = self.module.loss_fn(out, labels)
+                if isinstance(loss, (tuple, list)) and len(loss) == 2 and isinstance(loss[1], dict):
+                    loss, extra = loss  # (loss, {name: additional loss}) -> get_additional_losses()
+                    acc = self._additional_acc
+                    for k, v in extra.items():
+                        v = v.detach().float() if torch.is_tensor(v) else torch.tensor(float(v))
+                        acc[k] = v if k not in acc else acc[k] + v
             else:
                 loss = out
             if self._eval_outputs is not None:

@@ -284,6 +284,46 @@ class PipelineModule(nn.Module):
     def mpu(self):
         return self._grid
 
+    def _local_layers(self):
+        """[(local index, module)] of this stage's parameterised layers (tied modules under their first index)."""
+        out, seen = [], set()
+        for idx in range(self._local_start, self._local_stop):
+            spec = self._layer_specs[idx]
+            mod = None
+            if isinstance(spec, TiedLayerSpec):
+                mod = self.tied_modules[spec.key] if spec.key not in seen else None
+                seen.add(spec.key)
+            elif str(idx) in self._modules:
+                mod = self._modules[str(idx)]
+            if mod is not None and any(True for _ in mod.parameters()):
+                out.append((idx - self._local_start, mod))
+        return out
+
+    def save_state_dict(self, save_dir, checkpoint_engine=None, exclude_frozen_params=False):
+        """One ``layer_XX[-model_YY]-model_states.pt`` per parameterised layer of this stage (the reference's
+        layer-wise pipeline checkpoint, pipe/module.py save_state_dict): written by data-parallel rank 0 of each
+        stage / model-parallel slice."""
+        import os
+        if self._grid.get_data_parallel_rank() != 0:
+            return
+        os.makedirs(save_dir, exist_ok=True)
+        for li, mod in self._local_layers():
+            sd = {k: v.detach().clone().cpu() for k, v in mod.state_dict().items()}
+            if exclude_frozen_params:
+                frozen = {n for n, p in mod.named_parameters() if not p.requires_grad}
+                sd = {k: v for k, v in sd.items() if k not in frozen}
+            path = self.ckpt_layer_path(save_dir, li)
+            (checkpoint_engine.save(sd, path) if checkpoint_engine is not None else torch.save(sd, path))
+
+    def load_state_dir(self, load_dir, checkpoint_engine=None, strict=True):
+        """Load the layer files ``save_state_dict`` wrote into this stage's layers."""
+        for li, mod in self._local_layers():
+            path = self.ckpt_layer_path(load_dir, li)
+            sd = (checkpoint_engine.load(path, map_location="cpu") if checkpoint_engine is not None else
+                  torch.load(path, map_location="cpu", weights_only=True))
+            mod.load_state_dict(sd, strict=strict)
+        self.sync_tied_weights() if self.num_stages > 1 else None
+
     def ckpt_layer_path(self, ckpt_dir, local_layer_idx):
         import os
         idx = local_layer_idx + self._local_start

@@ -163,7 +163,7 @@ def discover_stage3_units(module, leaf_modules=(), persistence_threshold=0, buck
     for name, m in module.named_modules():
         if any(name == c or name.startswith(c + ".") for c in claimed):
             continue
-        if leaf_modules and isinstance(m, leaf_modules) and m is not module:
+        if m is not module and ((leaf_modules and isinstance(m, leaf_modules)) or getattr(m, "_z3_leaf", False)):
             units.append((name, m))
             claimed.add(name)
             continue

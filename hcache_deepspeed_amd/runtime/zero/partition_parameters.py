@@ -338,12 +338,51 @@ def unregister_external_parameter(module, parameter):
         module._external_params.pop(id(parameter), None)
 
 
+def _mark_leaf(m, flag):
+    m._z3_leaf = bool(flag)
+    for p in m.parameters():
+        if flag:
+            p.ds_z3_leaf_module = m
+        else:
+            p.__dict__.pop("ds_z3_leaf_module", None)
+
+
 def set_z3_leaf_modules(model, leaf_module_classes):
-    """Treat every instance of the given classes as ONE ZeRO-3 fetch unit (reference utils/z3_leaf_module.py)."""
+    """Treat every instance of the given classes as ONE ZeRO-3 fetch unit (reference utils/z3_leaf_module.py). Must
+    run before ``deepspeed.initialize`` builds the units. Returns the marked instances."""
     cur = tuple(getattr(model, "_z3_leaf_modules", ()))
-    model._z3_leaf_modules = cur + tuple(leaf_module_classes)
-    return [m for m in model.modules() if isinstance(m, tuple(leaf_module_classes))]
+    model._z3_leaf_modules = cur + tuple(c for c in leaf_module_classes if c not in cur)
+    hit = [m for m in model.modules() if isinstance(m, tuple(leaf_module_classes))]
+    for m in hit:
+        _mark_leaf(m, True)
+    return hit
+
+
+def unset_z3_leaf_modules(model, leaf_module_classes):
+    """Undo ``set_z3_leaf_modules`` for these classes. Returns the unmarked instances."""
+    drop = tuple(leaf_module_classes)
+    model._z3_leaf_modules = tuple(c for c in getattr(model, "_z3_leaf_modules", ()) if c not in drop)
+    hit = [m for m in model.modules() if isinstance(m, drop)]
+    for m in hit:
+        _mark_leaf(m, False)
+    return hit
+
+
+def set_z3_leaf_module(model, flag):
+    """Mark / unmark ONE module instance as a ZeRO-3 leaf (fetched as one unit)."""
+    _mark_leaf(model, flag)
+
+
+def z3_leaf_module(model):
+    """Is this module a ZeRO-3 leaf (by instance mark or by one of its root's leaf classes)?"""
+    return bool(getattr(model, "_z3_leaf", False))
+
+
+def z3_leaf_parameter(param):
+    """Does this parameter belong to a ZeRO-3 leaf module?"""
+    return getattr(param, "ds_z3_leaf_module", None) is not None
 
 
 def get_z3_leaf_modules(model):
-    return [m for m in model.modules() if isinstance(m, tuple(getattr(model, "_z3_leaf_modules", ())))]
+    classes = tuple(getattr(model, "_z3_leaf_modules", ()))
+    return [m for m in model.modules() if (classes and isinstance(m, classes)) or getattr(m, "_z3_leaf", False)]

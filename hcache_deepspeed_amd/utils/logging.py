@@ -56,3 +56,9 @@ def warning_once(msg):
 
 def should_log_le(max_level):
     return logger.getEffectiveLevel() <= logging.getLevelName(max_level.upper())
+
+
+def get_caller_func(frame=3):
+    """Name of the function ``frame`` levels up the stack (reference utils/logging.py get_caller_func)."""
+    import sys
+    return sys._getframe(frame).f_code.co_name

@@ -183,3 +183,81 @@ def safe_get_local_optimizer_state(param, optim_state_key):
 
 def safe_set_local_optimizer_state(param, value, optim_state_key):
     _set_local(param, value, optim_state_key)
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# hp-param helpers under the reference's names (utils/tensor_fragment.py get_full_hp_param / set_full_hp_param /
+# get_full_hp_grad / set_full_hp_grad / get_hp_fragment_mapping / map_to_flat_opt_states, mixed_precision_linkage.py
+# link_hp_params / lazy_init_hp_params_optimizer_state). The reference links every low-precision parameter to its
+# fragment of a flat fp32 partition and binds these as methods; here the parameter already knows its unit and offset
+# in the flat store, so the functions take the parameter and ``link_hp_params`` binds them the same way.
+# ---------------------------------------------------------------------------------------------------------------------
+def get_full_hp_param(param, optim_state_key=None):
+    """The full fp32 value of ``param`` (or of its optimizer state ``optim_state_key``). Collective."""
+    return _get_full(param, _FP32 if optim_state_key is None else optim_state_key)
+
+
+def set_full_hp_param(param, value, optim_state_key=None):
+    """Write the full fp32 value (or optimizer state) of ``param``; each rank keeps its fragment. Collective."""
+    _set_full(param, value, _FP32 if optim_state_key is None else optim_state_key)
+
+
+def get_full_hp_grad(param):
+    return _get_full(param, _GRAD)
+
+
+def set_full_hp_grad(param, value):
+    _set_full(param, value, _GRAD)
+
+
+def get_hp_fragment_mapping(param):
+    """{"lp_fragment_address", "hp_fragment_address"}: where this rank's fragment of ``param`` sits inside the
+    parameter (lp) and inside this rank's flat fp32 partition (hp); None when this rank holds none of it."""
+    z = _zopt(param)
+    if z is None:
+        return None
+    u, i = z.param_to_unit[id(param)]
+    r = _local_range(z, u, i)
+    if r is None:
+        return None
+    (a, b), (lo, hi) = r
+    return {"lp_fragment_address": fragment_address(numel=b - a, start=a),
+            "hp_fragment_address": fragment_address(numel=hi - lo, start=lo)}
+
+
+def map_to_flat_opt_states(flat_hp_tensor, lp_tensors, optim_state, opt_keys):
+    """Concatenate the per-parameter optimizer states of ``lp_tensors`` into flat states keyed by
+    ``flat_hp_tensor`` (a torch optimizer's per-parameter state -> the flat layout the ZeRO store uses)."""
+    merged = optim_state.setdefault(flat_hp_tensor, {})
+    for key in opt_keys:
+        parts = [optim_state[lp][key].reshape(-1) for lp in lp_tensors if lp in optim_state and key in optim_state[lp]]
+        if parts:
+            merged[key] = torch.cat(parts)
+    return merged
+
+
+def link_hp_params(lp_param_list, *args, **kwargs):
+    """Bind ``get_full_hp_param`` / ``set_full_hp_param`` / ``get_full_hp_grad`` / ``set_full_hp_grad`` /
+    ``get_hp_fragment_mapping`` as methods of every parameter (the reference's linkage; the extra arguments of its
+    signature -- flat partition, gradient dicts, partition bounds -- are implied by the flat store here)."""
+    import functools
+    for p in lp_param_list:
+        p.get_full_hp_param = functools.partial(get_full_hp_param, p)
+        p.set_full_hp_param = functools.partial(set_full_hp_param, p)
+        p.get_full_hp_grad = functools.partial(get_full_hp_grad, p)
+        p.set_full_hp_grad = functools.partial(set_full_hp_grad, p)
+        p.get_hp_fragment_mapping = functools.partial(get_hp_fragment_mapping, p)
+    return lp_param_list
+
+
+def lazy_init_hp_params_optimizer_state(lp_param_list, *args, **kwargs):
+    """The reference creates the optimizer-state fragments of linked parameters after the first step; the flat store
+    creates its states with the optimizer, so this only makes sure they are resident (state offload) for readers."""
+    seen = set()
+    for p in lp_param_list:
+        z = _zopt(p)
+        if z is not None and id(z) not in seen:
+            seen.add(id(z))
+            so = getattr(z, "state_offload", None)
+            if so is not None:
+                so.wait()
