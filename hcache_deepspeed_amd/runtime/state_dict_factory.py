@@ -22,6 +22,7 @@ import torch
 
 from ..utils.logging import logger
 from .checkpoint_engine import TorchCheckpointEngine
+from .weight_quantizer import WeightQuantization
 
 AUTO_MODULE_KEY = "auto"
 
@@ -83,15 +84,20 @@ class SDLoaderBase:
         if is_pipe_parallel and module_key is not None and mp_world_size != n:
             mp_world_size, idx = n, 0
         path = self.ckpt_list[idx]
-        if quantize:
-            raise NotImplementedError("quantized Megatron resharding: load, then use ops.quantizer on the result")
+        q = (quantize_bits, quantize_groups, mlp_extra_grouping) if quantize else None
         if n == mp_world_size:
             assert os.path.exists(path), path
-            return path, self._load(path), (None, 1)
+            sd = self._load(path)
+            scales = None
+            if q is not None:  # int8 weights + per-group scales (reference state_dict_factory.py:62-64)
+                wq = WeightQuantization(mlp_extra_grouping=mlp_extra_grouping, mp_size=mp_world_size)
+                module, scales = wq.sd_quantize_megatron(self.get_module(sd), quantize_bits, quantize_groups)
+                self.set_module(sd, module)
+            return path, sd, (scales, 1)
         if n > mp_world_size:
-            sd, scales, count = self.merge_state_dict(mp_world_size, mp_rank)
+            sd, scales, count = self.merge_state_dict(mp_world_size, mp_rank, q)
             return path, sd, (scales, count)
-        sd, scales = self.split_state_dict(mp_world_size, mp_rank)
+        sd, scales = self.split_state_dict(mp_world_size, mp_rank, q)
         return path, sd, (scales, 1)
 
     def get_merge_state_dicts(self, mp_world_size, mp_rank):
@@ -164,16 +170,22 @@ class MegatronSDLoader(SDLoaderBase):
             return torch.chunk(param, num_to_split, 0)[offset]
         raise AssertionError(f"checkpoint version: {ckpt_ver} is not supported")
 
-    def merge_state_dict(self, mp_world_size, mp_rank, *args, **kwargs):
+    def merge_state_dict(self, mp_world_size, mp_rank, quantize=None, *args, **kwargs):
+        """``quantize`` = (bits, groups, mlp_extra_grouping) or None: each shard of the four projection weights is
+        quantized with its own group scales BEFORE the int8 shards are merged (reference :100)."""
         self.sanity_check(self.ckpt_list[0])
         sd_list = self.get_merge_state_dicts(mp_world_size, mp_rank)
         ds_sd = copy.deepcopy(sd_list[0])
         modules = [self.get_module(sd) for sd in sd_list]
         ver = self.get_checkpoint_version(ds_sd)
+        wq = WeightQuantization(mlp_extra_grouping=quantize[2], mp_size=mp_world_size) if quantize else None
         out = collections.OrderedDict()
         for key in modules[0].keys():
             vals = [m[key] for m in modules]
             rule = _rule(key)
+            if wq is not None and key.endswith(".weight") and rule in ("dim0", "dim1", "qkv") and \
+                    any(k in key for k in ("attention.dense", "mlp.dense_4h_to_h", "mlp.dense_h_to_4h", _QKV)):
+                vals = wq.Quantize(vals, quantize[0], quantize[1], key=key, merge_dim=1 if rule == "dim1" else 0)
             if rule == "dim1":
                 out[key] = torch.cat(vals, 1)
             elif rule == "qkv":
@@ -182,15 +194,21 @@ class MegatronSDLoader(SDLoaderBase):
                 out[key] = torch.cat(vals, 0)
             else:
                 out[key] = vals[0]
-        return self.set_module(ds_sd, out), None, len(modules)
+        return self.set_module(ds_sd, out), (wq.merge_scales() if wq is not None else None), len(modules)
 
-    def split_state_dict(self, mp_world_size, mp_rank, *args, **kwargs):
+    def split_state_dict(self, mp_world_size, mp_rank, quantize=None, *args, **kwargs):
+        """``quantize``: the whole tensor is quantized first, then split; each target gets its slice of the group
+        scales (reference merge_scales_split)."""
         sd, per, off = self.get_split_state_dict(mp_world_size, mp_rank)
         ds_sd = copy.deepcopy(sd)
         ver = self.get_checkpoint_version(ds_sd)
+        wq = WeightQuantization(mlp_extra_grouping=quantize[2], mp_size=mp_world_size) if quantize else None
         out = collections.OrderedDict()
         for key, val in self.get_module(sd).items():
             rule = _rule(key)
+            if wq is not None and key.endswith(".weight") and rule in ("dim0", "dim1", "qkv") and \
+                    any(k in key for k in ("attention.dense", "mlp.dense_4h_to_h", "mlp.dense_h_to_4h", _QKV)):
+                val = wq.Quantize([val], quantize[0], quantize[1], key=key)[0]
             if rule == "dim1":
                 assert val.shape[1] % per == 0
                 out[key] = torch.chunk(val, per, 1)[off]
@@ -201,7 +219,8 @@ class MegatronSDLoader(SDLoaderBase):
                 out[key] = torch.chunk(val, per, 0)[off]
             else:
                 out[key] = val
-        return self.set_module(ds_sd, out), None
+        scales = wq.merge_scales_split(per)[off] if wq is not None and wq.qkv_scales else None
+        return self.set_module(ds_sd, out), scales
 
     def sanity_check(self, ckpt_file_name):
         need = ("attention.dense.weight", "mlp.dense_4h_to_h.weight", _QKV, "mlp.dense_h_to_4h.weight",
