@@ -80,6 +80,14 @@ def main():
                          "ZeRO-Offload++); the rest keeps the on-device fused Adam")
     ap.add_argument("--nvme-path", default="/tmp/hds_nvme", help="swap folder of the NVMe tier (--offload nvme)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
+    ap.add_argument("--sp", type=int, default=1,
+                    help="Ulysses sequence-parallel size: each rank holds seq/sp tokens of every sequence (ZeRO shards "
+                         "over the dp x sp ranks; tokens/s counts each sequence once)")
+    ap.add_argument("--fpdt-chunk", type=int, default=0,
+                    help="FPDT (Ulysses-Offload) attention with this global segment length (mi355x.fpdt): chunked "
+                         "attention, segments in pinned host memory between forward and backward")
+    ap.add_argument("--fpdt-no-offload", action="store_true", help="FPDT: keep the segments on the device")
+    ap.add_argument("--fpdt-ffn-chunks", type=int, default=0, help="FPDT: also run the MLPs in this many chunks")
     ap.add_argument("--offload-opt-states", action="store_true",
                     help="DeepCompile offload_adam_states: Adam moments + fp32 master on pinned host between steps")
     ap.add_argument("--offload-states-ratio", type=float, default=1.0,
@@ -165,6 +173,12 @@ def main():
                                                                         "spill_cost_ms_per_gb": args.act_cache_spill_cost}},
         "steps_per_print": 1000000,
     }
+    if args.sp > 1:
+        assert world % args.sp == 0 and args.seq % args.sp == 0, "--sp must divide the world size and --seq"
+        ds_config["sequence_parallel_size"] = args.sp
+    if args.fpdt_chunk:
+        ds_config["mi355x"]["fpdt"] = {"enabled": True, "chunk_size": args.fpdt_chunk,
+                                       "offload": not args.fpdt_no_offload, "ffn_chunks": args.fpdt_ffn_chunks}
     if args.zero == 3:
         rd = args.reuse_distance
         if rd == "auto":
@@ -206,14 +220,28 @@ def main():
     dev = engine.device
     S, mb = args.seq, args.micro_batch
     gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
+    sp = args.sp
+    if sp > 1:
+        # the ranks of one sequence-parallel group draw the SAME sequences and each feeds its own token positions
+        from hcache_deepspeed_amd.utils import groups as _groups
+        sp_ranks = tdist.get_process_group_ranks(_groups._get_sequence_parallel_group())
+        gen.manual_seed(1234 + min(sp_ranks))
+        shard = engine.sequence_shard_indices(S).to(dev)
+    else:
+        gen.manual_seed(1234 + rank)
+        shard = None
 
     def train_step(i):
         loss = None
         for g in range(args.gas):
             # a fresh synthetic batch every micro-step (no fixed batches to memorise)
-            x = torch.randint(0, cfg_model.vocab_size, (mb, S), device=dev, generator=gen)
-            loss = engine(x, labels=x)
+            if shard is None:
+                x = torch.randint(0, cfg_model.vocab_size, (mb, S), device=dev, generator=gen)
+                loss = engine(x, labels=x)
+            else:
+                full = torch.randint(0, cfg_model.vocab_size, (mb, S + 1), device=dev, generator=gen)
+                x, t = full[:, :-1][:, shard].contiguous(), full[:, 1:][:, shard].contiguous()
+                loss = engine(x, targets=t)
             engine.backward(loss)
             engine.step()
         return loss
@@ -292,7 +320,7 @@ def main():
     dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
     tdist.all_reduce(dt_t, op=tdist.ReduceOp.MAX)
     dt = float(dt_t.item())
-    tokens = world * mb * args.gas * S * args.steps
+    tokens = world // sp * mb * args.gas * S * args.steps  # every sequence once (its sp ranks share it)
     value = tokens / dt
     ms_per_step = dt / args.steps * 1e3
     flops = (cfg_model.flops_per_token(S) if hasattr(cfg_model, "flops_per_token") else
@@ -384,8 +412,11 @@ def main():
                        "host_act_cache": bool(args.host_act_cache), "offload": args.offload,
                        **({"offload_ratio": float(args.offload_ratio)} if args.offload != "none" and
                           args.offload_ratio < 1.0 else {}),
-                       "global_batch": world * mb * args.gas, "seq_len": S,
-                       "parallelism": f"zero{args.zero}-dp{world}", "micro_batch_per_gpu": mb, "gas": args.gas,
+                       "global_batch": world // sp * mb * args.gas, "seq_len": S,
+                       "parallelism": f"zero{args.zero}-dp{world // sp}" + (f"-sp{sp}" if sp > 1 else ""),
+                       "micro_batch_per_gpu": mb, "gas": args.gas,
+                       **({"sequence_parallel_size": sp} if sp > 1 else {}),
+                       **({"fpdt": engine.fpdt_config} if getattr(engine, "fpdt_config", None) else {}),
                        "stage3_max_reuse_distance": ds_config["zero_optimization"].get("stage3_max_reuse_distance"),
                        "activation_checkpointing": bool(args.ckpt), "deepcompile": bool(args.deepcompile)},
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),

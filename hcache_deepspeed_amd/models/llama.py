@@ -114,8 +114,17 @@ def tiny(**kw):
     return LlamaConfig(**d)
 
 
+def tiny_sp(**kw):
+    """Tiny model whose 16 q / 8 kv heads split evenly over up to 8 Ulysses ranks (CPU dry runs of the
+    sequence-parallel bench)."""
+    d = dict(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=16,
+             num_key_value_heads=8, head_dim=16, max_position_embeddings=4096)
+    d.update(kw)
+    return LlamaConfig(**d)
+
+
 PRESETS = {"llama3-8b": llama3_8b, "llama3-70b": llama3_70b, "llama2-7b": llama2_7b, "mistral-7b": mistral_7b,
-           "tiny": tiny}
+           "tiny": tiny, "tiny-sp": tiny_sp}
 
 
 class _Linear(nn.Linear):

@@ -190,7 +190,8 @@ class HostActivationCache:
         if hgib <= 0:
             hgib = default_host_budget_gib()
         wgib = float(getattr(cfg, "copy_window_gib", 0.0) or 0.0)
-        return cls(device, min_bytes=1 << 20, min_layers_resident=cfg.min_layers_resident,
+        return cls(device, min_bytes=int(float(getattr(cfg, "min_kib", 1024)) * 1024),
+                   min_layers_resident=cfg.min_layers_resident,
                    prefetch_layers=int(getattr(cfg, "prefetch_layers", 2)), gpu_budget_bytes=budget,
                    host_budget_bytes=int(hgib * 2**30), copy_window_bytes=int(wgib * 2**30) if wgib > 0 else None,
                    recompute=getattr(cfg, "policy", "budget") == "recompute",

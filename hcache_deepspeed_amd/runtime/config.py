@@ -188,6 +188,8 @@ class HostActCacheConfig:
     allow_unlimited_blit: bool = False
     # refuse (BlitLimitError) instead of warning when spills would run as unlimited blit kernels
     strict_blit_limit: bool = False
+    # smallest saved tensor the cache moves (KiB); smaller ones stay on the device
+    min_kib: float = 1024.0
 
 
 AUTO = -1
@@ -221,6 +223,11 @@ class MI355XConfig:
     # several ranks share the host and the count was not set explicitly (torchrun forces OMP_NUM_THREADS=1), else
     # left alone; an int forces it
     cpu_threads_per_rank: object = "auto"
+    # FPDT (Ulysses-Offload) attention from the config (parallel/fpdt.py): {"enabled": bool, "chunk_size": global
+    # tokens per attention segment, "offload": park each segment's q/k/v/o/lse in pinned host memory between forward
+    # and backward, "ffn_chunks": > 1 also runs the MLPs in sequence chunks}; inputs in the FPDT layout
+    # (engine.fpdt_input_indices)
+    fpdt: Optional[dict] = None
     host_act_cache: HostActCacheConfig = field(default_factory=HostActCacheConfig)
 
 
@@ -346,6 +353,7 @@ class DeepSpeedConfig:
             zero_comm_transport=str(m.get("zero_comm_transport", "auto")),
             zero3_event_timers=bool(m.get("zero3_event_timers", False)),
             cpu_threads_per_rank=m.get("cpu_threads_per_rank", "auto"),
+            fpdt=dict(m["fpdt"]) if m.get("fpdt") else None,
             direct_wgrad=bool(m.get("direct_wgrad", True)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
             comm_high_priority=bool(m.get("comm_high_priority", True)),

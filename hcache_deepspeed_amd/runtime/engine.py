@@ -112,6 +112,16 @@ class DeepSpeedEngine(EngineApiMixin, nn.Module):
         if sp > 1:
             from ..parallel.ulysses import enable_sequence_parallel
             enable_sequence_parallel(model, self.seq_parallel_group)
+        fp = cfg.mi355x.fpdt or {}
+        self.fpdt_config = None
+        if fp.get("enabled", True) and fp.get("chunk_size"):
+            # FPDT from the config (reference sequence/fpdt_layer.py is wired by Megatron-DeepSpeed's model code; here
+            # the engine converts the Llama attention / MLP modules): chunked Ulysses attention over the SP group
+            from ..parallel.fpdt import enable_fpdt
+            self.fpdt_config = {"chunk_size": int(fp["chunk_size"]), "offload": bool(fp.get("offload", True)),
+                                "ffn_chunks": int(fp.get("ffn_chunks", 0)), "sp": sp}
+            enable_fpdt(model, self.seq_parallel_group if sp > 1 else None, self.fpdt_config["chunk_size"],
+                        offload=self.fpdt_config["offload"], ffn_chunks=self.fpdt_config["ffn_chunks"])
 
         # timers / monitoring
         self.wall_clock_breakdown_enabled = cfg.wall_clock_breakdown
@@ -355,6 +365,20 @@ class DeepSpeedEngine(EngineApiMixin, nn.Module):
         if forced is not None:
             return forced
         return (self.micro_steps + 1) % self.gradient_accumulation_steps() == 0
+
+    def sequence_shard_indices(self, seq_len):
+        """Global token positions of a length-``seq_len`` sequence this rank feeds the model: all of them without
+        sequence parallelism, its contiguous 1/sp slice under Ulysses, its load-balanced chunk set under FPDT
+        (parallel/fpdt.FPDTInputConstruct). Index both the inputs and the next-token targets with it."""
+        sp = int(self._config.sequence_parallel_size)
+        rank = dist.get_rank(self.seq_parallel_group) if sp > 1 else 0
+        if self.fpdt_config is not None:
+            from ..parallel.fpdt import fpdt_layout_indices
+            return fpdt_layout_indices(seq_len, self.fpdt_config["chunk_size"], sp, rank)
+        n = seq_len // sp
+        return torch.arange(rank * n, (rank + 1) * n)
+
+    fpdt_input_indices = sequence_shard_indices
 
     def get_data_parallel_world_size(self):
         return self.dp_world_size
