@@ -30,6 +30,7 @@ import torch
 
 from .. import comm as dist
 from ..ops.attention import attn_block_bwd, attn_block_fwd, merge_attn_out
+from ..ops.cross_entropy import _addmm_f32_
 from ..ops.rope import rope_
 from .ulysses import head_to_seq, qkv_head_permutation, seq_to_head
 
@@ -211,7 +212,7 @@ class _FPDTAttnFn(torch.autograd.Function):
             g2 = loc.reshape(B * cs, -1)
             xj = xv[:, j * cs:(j + 1) * cs].reshape(B * cs, H)
             dx[:, j * cs:(j + 1) * cs] = (g2 @ wp).view(B, cs, H)
-            dwp.addmm_(g2.t().float(), xj.float())
+            _addmm_f32_(dwp, g2.t(), xj)  # bf16 GEMM, fp32 accumulator folded in (no fp32 operand copies)
             if dbp is not None:
                 dbp += g2.float().sum(0)
             for n in ("q", "k", "v", "o", "lse", "do"):  # later kv segments only touch query segments > j
@@ -348,8 +349,14 @@ class _LogitsLossFn(torch.autograd.Function):
             valid = lab != -100
             p[torch.arange(p.shape[0], device=p.device)[valid], lab[valid]] -= 1.0
             p *= (g[idx] * valid)[:, None]
-            dh[idx] = (p @ weight.float()).to(h.dtype)
-            dw.addmm_(p.t(), h[idx].float())
+            if h.is_cuda and h.dtype != torch.float32:
+                # bf16 GEMMs with fp32 accumulation: no fp32 copy of the [V, H] LM-head weight per chunk
+                pl = p.to(h.dtype)
+                dh[idx] = pl @ weight
+                _addmm_f32_(dw, pl.t(), h[idx])
+            else:
+                dh[idx] = (p @ weight.float()).to(h.dtype)
+                dw.addmm_(p.t(), h[idx].float())
         return dh, dw.to(weight.dtype), None, None
 
 

@@ -133,3 +133,54 @@ def estimate_llama_training(cfg, micro_batch, seq, world, stage=3, prefetch_dept
     tot = gpu + act
     return {"params_b": total / 1e9, "states_gib": gpu / GB, "activations_gib": act / GB, "total_gib": tot / GB,
             "host_gib": cpu / GB, "fits": tot / GB <= hbm_gib}
+
+
+def long_context_plan(cfg, n_gpus=8, sp=8, host_ram_gib=2048.0, host_fraction=0.4, hbm_gib=268.0, stash=True,
+                      max_tokens=1 << 26):
+    """Largest sequence length S one node trains with Ulysses SP + the host activation cache (``ckpt_offload``) and
+    ZeRO-3 over all ``n_gpus`` ranks (dp = n_gpus / sp sequences in flight), and what it costs in host DRAM.
+
+    Per rank (S_loc = S / sp tokens):
+      * host (pinned): every block's checkpointed boundary (H bf16 per token and layer) and, with ``stash``, its
+        attention output + LSE (n_q*d bf16 + n_q fp32) -- ``host_fraction`` of the node's RAM is the pinned budget,
+        shared by the node's ranks (offload/activation_cache.default_host_budget_gib);
+      * HBM: ZeRO-3 states sharded n_gpus ways + the gathered working set, a fixed workspace (MLP run in 64k-row
+        chunks, LM-head CE chunks, copy window: 40 GiB), one block's recompute transients for S_loc tokens
+        (~12 H bf16 values per token incl. gradients), and the all-to-all'ed attention of the FULL sequence for this
+        rank's n_q/sp heads (q, k, v, o and their gradients).
+    Calibration against the one-GPU 512k run (profiles/r5/ckoff512k_r5d.json): the plan's HBM at n_gpus = sp = 1,
+    S = 512k is 227.7 GiB (measured peak 221.5 GiB with 10 blocks' stash kept on the device); its host bytes without
+    the stash are 128 GiB of boundaries (measured 156.6 GiB pinned: the boundaries plus the stash of the 9 blocks that
+    fit the budget -- the cache stashes only what the pinned budget holds, so ``stash`` True / False bracket it).
+    Returns {"max_seq": S, "host_gib_node": ..., "hbm_gib_rank": ..., "limited_by": "host" | "hbm"}."""
+    H, L = cfg.hidden_size, cfg.num_hidden_layers
+    nq, nkv, d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    gpu_states, _ = estimate(cfg.num_params(include_embedding=True) if hasattr(cfg, "num_params") else 8.03e9, 3,
+                             n_gpus, H * (nq * d + 2 * nkv * d) + nq * d * H + 3 * H * cfg.intermediate_size)
+    host_per_tok_rank = L * (2 * H + ((2 * nq * d + 4 * nq) if stash else 0))
+    lq, lkv = max(1, nq // sp), max(1, nkv // sp)
+    full_attn_per_tok = 2 * 2 * (2 * lq + 2 * lkv) * d  # q,k,v,o + grads for this rank's heads over the full S
+    dev_per_loc_tok = 12 * 2 * H
+    fixed = 40 * GB
+    budget_host = host_fraction * host_ram_gib * GB
+    dp = max(1, n_gpus // sp)
+
+    def need(S):
+        s_loc = S // sp
+        host = host_per_tok_rank * s_loc * n_gpus  # every rank of the node holds its slice (dp groups: own sequences)
+        dev = gpu_states + fixed + dev_per_loc_tok * s_loc + full_attn_per_tok * S
+        return host, dev
+
+    lo, hi = 0, max_tokens
+    while hi - lo > 1024:
+        mid = (lo + hi) // 2 // 1024 * 1024
+        host, dev = need(mid)
+        if host <= budget_host and dev <= hbm_gib * GB:
+            lo = mid
+        else:
+            hi = mid
+    host, dev = need(lo)
+    h2, d2 = need(lo + 1024 * sp)
+    return {"max_seq": lo, "n_gpus": n_gpus, "sp": sp, "dp": dp, "host_gib_node": round(host / GB, 1),
+            "host_budget_gib_node": round(budget_host / GB, 1), "hbm_gib_rank": round(dev / GB, 1),
+            "limited_by": "host" if h2 > budget_host else "hbm", "stash_attention": stash}

@@ -102,3 +102,17 @@ def test_bench_sp8_ckpt_offload_torchrun_dry_run():
     assert c["global_batch"] == 2 and out["value"] > 0
     assert out["extra"]["act_cache"]["recomputed_layers"] == 2  # every block checkpointed (ckpt_offload)
     assert out["extra"]["comm"]["ranks"] == W
+
+
+def test_node_long_context_plan():
+    """The per-node plan (README: planned max S at 8 GPUs): host-bound at SP 8, monotone in host RAM, the stash
+    halves the reach, HBM stays far below a MI355X's at the planned S, and 512k at one GPU reproduces the measured
+    run's scale (227.7 GiB planned vs 221.5 GiB measured peak; 128 GiB of boundaries)."""
+    from hcache_deepspeed_amd.models.llama import llama3_8b
+    from hcache_deepspeed_amd.runtime.zero.mem_estimators import long_context_plan
+    c = llama3_8b()
+    p1, p2 = long_context_plan(c, 8, 8, host_ram_gib=1024), long_context_plan(c, 8, 8, host_ram_gib=2048)
+    assert p1["limited_by"] == "host" and p2["max_seq"] > 1.9 * p1["max_seq"]
+    ns = long_context_plan(c, 8, 8, host_ram_gib=2048, stash=False)
+    assert ns["max_seq"] > 1.9 * p2["max_seq"] and ns["max_seq"] >= 2 * 2**20  # >= 2M tokens on one 2 TiB node
+    assert ns["hbm_gib_rank"] < 200
