@@ -90,8 +90,10 @@ def main():
     ap.add_argument("--fpdt-ffn-chunks", type=int, default=0, help="FPDT: also run the MLPs in this many chunks")
     ap.add_argument("--offload-opt-states", action="store_true",
                     help="DeepCompile offload_adam_states: Adam moments + fp32 master on pinned host between steps")
-    ap.add_argument("--offload-states-ratio", type=float, default=1.0,
-                    help="with --offload-opt-states: fraction of every moved state (its tail) kept on the host between steps")
+    ap.add_argument("--offload-states-ratio", type=lambda v: v if v == "auto" else float(v), default=1.0,
+                    help="with --offload-opt-states: fraction of every moved state (its tail) kept on the host between "
+                         "steps; 'auto': everything on the host for the first step, then the ratio that the first "
+                         "step's measured peak leaves room for")
     ap.add_argument("--offload-states-host-step", action="store_true",
                     help="with --offload-opt-states: the host tails stay on the host and step there (host Adam)")
     ap.add_argument("--offload-params-compile", type=float, default=None, metavar="BUDGET_GIB",

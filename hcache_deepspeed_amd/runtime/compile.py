@@ -96,7 +96,9 @@ def compile_engine(engine, backend="native", compile_kwargs=None, schedule=None)
             "offload_opt_states needs the ZeRO optimizer"
         kw = compile_kwargs or {}
         engine.optimizer.enable_state_offload(include_master=bool(kw.get("offload_master", True)),
-                                              ratio=float(kw.get("offload_states_ratio", 1.0)),
+                                              ratio=(kw.get("offload_states_ratio", 1.0)
+                                                     if str(kw.get("offload_states_ratio", 1.0)) == "auto"
+                                                     else float(kw.get("offload_states_ratio", 1.0))),
                                               chunk_mb=float(kw.get("offload_states_chunk_mb", 1024)),
                                               host_step=bool(kw.get("offload_states_host_step", False)))
     times["offload_adam_states"] = time.perf_counter() - t0

@@ -779,6 +779,8 @@ class ZeroOptimizer:
                 self._record_and_prefetch(u)
                 if self.state_offload is not None:  # pace the forward to the post-step state offload's drains
                     self.state_offload.on_forward_position()
+            if self.state_offload is not None:  # this unit's host-stepped pieces (async host step) are on the device
+                self.state_offload.wait_unit(u)
             self._fetch(u, "forward")
 
         return pre
@@ -799,6 +801,8 @@ class ZeroOptimizer:
     def _make_ext_pre(self, u):
 
         def pre(module, args):
+            if self.state_offload is not None:
+                self.state_offload.wait_unit(u)
             self._gather(u, wait=True)  # external parameter: kept until its own unit's release
 
         return pre
@@ -1159,6 +1163,11 @@ class ZeroOptimizer:
         return dist.reduce_scatter_tensor(out, inp, group=group, async_op=True)
 
     def _gather(self, u, wait=True):
+        so = self.state_offload
+        if so is not None and u.status == NOT_AVAILABLE and u.uid in so._unit_pieces:
+            if not wait:
+                return  # a prefetch of a unit whose host-stepped shard is not back yet: fetched on demand instead
+            so.wait_unit(u)
         if u.status == NOT_AVAILABLE:
             dev = getattr(u, "dev_shard", None)
             if dev is not None and u.world == 1:
@@ -1470,6 +1479,8 @@ class ZeroOptimizer:
         self.boundary = boundary
         self.in_backward = True
         so = self.state_offload
+        if so is not None:
+            so.before_backward()  # the tail gradients were copied out (and zeroed) on the copy stream
         if so is not None and boundary:
             # no compiled position: reload what fits now; the rest follows state by state as backward frees HBM
             # (state_offload.on_backward_position) and step() waits for everything
@@ -1518,6 +1529,13 @@ class ZeroOptimizer:
         self._last_pre_uid = None
         self._trace_pos = 0
         self._trace_ok = bool(self._fwd_trace) and not self._recording
+        so = self.state_offload
+        if so is not None and so.async_pending:
+            if self.stage != 3:
+                so.join()  # no per-unit hooks below ZeRO-3: every piece before the forward
+            else:
+                for u in self.root_units:
+                    so.wait_unit(u)  # stepped first: the embeddings / LM head
         for u in self.root_units:
             self._gather(u, wait=True)
 
@@ -1541,6 +1559,26 @@ class ZeroOptimizer:
         return self.loss_scaler.loss_scale
 
     def zero_grad(self, set_to_none=True):
+        so = self.state_offload
+        if so is not None and so.async_pending:
+            # async host step: the tail [a, n) is zeroed on the copy stream behind its own D2H; only the head here
+            a = so.a
+            if self._store_zero_plan is not None:
+                key = ("head", a)
+                if getattr(self, "_head_zero_plan", (None, None))[0] != key:
+                    self._head_zero_plan = (key, _ZeroPlan([(lo, min(hi, a)) for lo, hi in self._store_zero_ranges
+                                                             if lo < a], self.device))
+                self._head_zero_plan[1].apply(self.store.grad)
+                for u in self.units:
+                    if u.direct:
+                        self._mark_fresh(u)
+            else:
+                self.store.grad[:a].zero_()
+            for u in self.units:
+                if u.grad_full is not None and not u.direct:
+                    self._reset_grad_buffer(u)
+            self.micro_in_window = 0
+            return
         if self._store_zero_plan is not None:
             # in-place weight gradients overwrite their ranges: zero only the rest, mark the weights fresh
             self._store_zero_plan.apply(self.store.grad)
@@ -1613,6 +1651,7 @@ class ZeroOptimizer:
                 store_ranges += [(lo + u.store_off, hi + u.store_off) for lo, hi in gaps]
             else:
                 store_ranges.append((u.store_off, u.store_off + u.shard))
+        self._store_zero_ranges = store_ranges
         if any(u.direct for u in self.units):
             self._store_zero_plan = _ZeroPlan(store_ranges, dev)
         for u in self.units:
@@ -1679,6 +1718,7 @@ class ZeroOptimizer:
             # off the device from the start: the first forward is the one that needs the HBM when the states and
             # the activations do not fit together
             self.state_offload.offload()
+            self.state_offload.start_profile()
         return self.state_offload
 
     def _states_resident(self):
@@ -1786,6 +1826,14 @@ class ZeroOptimizer:
                                            g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
             if hosted:
                 so.step_on_host(hosted, coef, lp_flat, found_inf=found_inf, lp_cur=s.lp)
+                if so.async_pending:
+                    # the post-step gathers below read the shards: stage 1/2 all of them, stage 3 the persistent ones
+                    if self.stage != 3 and any(u.world > 1 for u in self.units):
+                        so.join()
+                    else:
+                        for u in self.units:
+                            if u.persistent and u.world > 1:
+                                so.wait_unit(u)
         tmp = self.__dict__.pop("_step_lp", None)
         if tmp is not None:
             self._publish_lp(tmp)
@@ -1793,6 +1841,10 @@ class ZeroOptimizer:
         self.zero_grad()
         if self.state_offload is not None:
             self.state_offload.offload()  # D2H overlaps the next forward
+            if self.state_offload.auto_ratio and self.state_offload.auto_info is None:
+                r = self.state_offload.autotune_ratio()
+                if r is not None:
+                    log_dist(f"offload_adam_states: ratio auto -> {r} ({self.state_offload.auto_info})", ranks=[0])
         return True
 
     def layout_world_for_avg(self):

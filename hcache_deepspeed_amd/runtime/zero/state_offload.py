@@ -55,7 +55,16 @@ class OptimizerStateOffload:
         self.include_master = bool(include_master)
         self.host_step = bool(host_step) and self.include_master and zopt.kind == "adam"
         self._h_grad = self._h_lp = None  # host-step staging (pinned, double-buffered)
-        self.ratio = min(1.0, max(0.0, float(ratio)))
+        self._h_grad_full = self._h_lp_full = None  # async host step: pinned staging of the whole tail
+        self._async = None  # the in-flight async host step (see step_on_host)
+        self._unit_pieces = {}
+        self._thread = None
+        # "auto" (reference compile/passes/offload_adam_states.py:253 decides from profiled memory): the first step
+        # runs with everything on the host, then ``autotune_ratio`` keeps on the device what its measured peak leaves
+        # room for
+        self.auto_ratio = str(ratio) == "auto"
+        self.auto_info = None
+        self.ratio = 1.0 if self.auto_ratio else min(1.0, max(0.0, float(ratio)))
         self.chunk_bytes = max(256, int(float(chunk_mb) * 2**20))
         dev = zopt.device
         self.cuda = dev.type == "cuda"
@@ -216,6 +225,59 @@ class OptimizerStateOffload:
             total[st] += nb
         return [(ev, total[st]) for j, (ev, _, st) in enumerate(issued) if last[st] == j]
 
+    def start_profile(self):
+        """Reset the allocator peak once the states have left the device (the first step's peak is then the
+        activations' and the step's, which ``autotune_ratio`` sizes the resident heads against)."""
+        if self.cuda and self.auto_ratio:
+            torch.cuda.synchronize(self.z.device)
+            torch.cuda.reset_peak_memory_stats(self.z.device)
+
+    def autotune_ratio(self, margin_gib=6.0):
+        """After the first (all-offloaded) step: the fraction of the states that must stay off the device so the
+        resident heads plus the measured peak fit ``mem_fraction`` of HBM with ``margin_gib`` to spare, rounded up
+        to 5 %. The heads move back to the device once; the tails keep stepping where they were."""
+        if not self.auto_ratio or self.auto_info is not None or not self.cuda:
+            return None
+        self.join()
+        dev = self.z.device
+        torch.cuda.synchronize(dev)
+        peak = torch.cuda.max_memory_allocated(dev)
+        limit = int(self.mem_fraction * torch.cuda.get_device_properties(dev).total_memory)
+        state_bytes = sum(h.numel() * h.element_size() for h in self.host.values())
+        free = max(0, limit - peak - int(margin_gib * 2**30))
+        import math
+        r = 1.0 - (free / state_bytes if state_bytes else 0.0)
+        r = min(1.0, max(0.0, math.ceil(r * 20 - 1e-9) / 20))
+        self.auto_info = {"peak_gib_step1": round(peak / 2**30, 1), "limit_gib": round(limit / 2**30, 1),
+                          "state_gib": round(state_bytes / 2**30, 1), "ratio": r}
+        if r < 1.0:
+            self._resplit(r)
+        return r
+
+    def _resplit(self, ratio):
+        """Move the split point from a = 0 (everything on the host) to (1 - ratio) * n: the heads [0, a') come back to
+        the device (one H2D each), the host tails become views past a' of the same pinned buffers."""
+        assert self.split and self.a == 0 and self.offloaded
+        n = self.z.store.numel
+        a = int(round((1.0 - ratio) * n))
+        a = min(n, (a + 63) // 64 * 64)
+        for k in list(self.host):
+            h = self.host[k]
+            head = torch.empty(a, dtype=h.dtype, device=self.z.device)
+            head.copy_(h[:a])
+            self._set(k, head)
+            self.host[k] = h[a:]
+        es = 4
+        c = max(64, self.chunk_bytes // es // 64 * 64)
+        self.a, self.ratio = a, ratio
+        self.bounds = [(lo, min(n, lo + c)) for lo in range(a, n, c)]
+        self.tail = {k: [None] * len(self.bounds) for k in self.host}
+        self.events = {}
+        self._h_grad_full = self._h_lp_full = None
+        self._h_grad = self._h_lp = None
+        if self.cuda:
+            torch.cuda.synchronize(self.z.device)
+
     def on_forward_position(self):
         """Before a forward unit runs: retire the drained chunks and, if the HBM the allocator can hand out does not
         hold this unit's activation growth (measured on the previous forward), wait for the oldest draining chunks --
@@ -310,15 +372,22 @@ class OptimizerStateOffload:
                 and all(k in self.host for k, v in self.z.store.states.items() if v is not None))
 
     def step_on_host(self, pieces, coef, lp_flat, found_inf=None, lp_cur=None):
-        """Host Adam over the tail pieces [(lo, hi, group)]: D2H of piece i + 1's gradient and H2D of piece i - 1's
-        bf16 parameters overlap the host update of piece i; the device kernels of the heads (already queued) run
-        meanwhile. The bf16 parameters land in ``lp_flat`` ordered before the current stream on return.
+        """Host Adam over the tail pieces [(lo, hi, group)]; the device kernels of the heads (already queued) run
+        meanwhile. The bf16 parameters land in ``lp_flat``.
 
         ``found_inf`` (device flag: fp16 dynamic loss scaling, or a symmetric-memory skip) is the same skip the device
         kernels fold: when it is set the host tails are left untouched (and ``lp_flat``, if it is not the live
-        parameter buffer ``lp_cur``, receives the current parameters of the pieces)."""
-        from ...ops.cpu_optimizers import cpu_adam_flat
-        z, s = self.z, self.z.store
+        parameter buffer ``lp_cur``, receives the current parameters of the pieces).
+
+        On the GPU with ``lp_flat`` the live parameter buffer the host step is ASYNCHRONOUS (``async_host_step``):
+        every tail gradient goes D2H at once (pieces in the order the next forward needs their units: the persistent
+        root unit -- embeddings, LM head -- first, then the blocks in forward order), each piece's tail is zeroed on
+        the copy stream right after its D2H, and a worker thread runs the host Adam piece by piece and issues each
+        piece's bf16 H2D with its own event. ``step()`` returns at once; the next forward waits only for the pieces
+        of the unit it is about to run (``wait_unit``), so the host Adam of the last blocks hides behind the forward
+        of the first ones (reference stage3.py:2082-2144 overlaps the CPU step with the parameter swap-in the same
+        way). Otherwise the pieces are stepped in place, D2H of piece i + 1 and H2D of piece i - 1 around the host
+        update of piece i."""
         cur = torch.cuda.current_stream() if self.cuda else None
         if found_inf is not None and float(found_inf.reshape(-1)[0].item()) != 0.0:  # one sync, only when a flag exists
             if lp_cur is not None and lp_flat.data_ptr() != lp_cur.data_ptr():
@@ -326,11 +395,49 @@ class OptimizerStateOffload:
                     lp_flat[lo:hi].copy_(lp_cur[lo:hi])
             self.host_skips = getattr(self, "host_skips", 0) + 1
             return
+        coef = float(coef) if not torch.is_tensor(coef) else float(coef.item())
+        if self.cuda and self.async_host_step and lp_cur is not None and lp_flat.data_ptr() == lp_cur.data_ptr():
+            self._step_on_host_async(pieces, coef, lp_flat, cur)
+        else:
+            self._step_on_host_sync(pieces, coef, lp_flat, cur)
+        self.host_steps = getattr(self, "host_steps", 0) + 1
+
+    # async host step (GPU): see step_on_host
+    async_host_step = os.environ.get("HDS_ASYNC_HOST_STEP", "1") == "1"
+
+    def _adam_piece(self, lo, hi, g, grad, out, coef):
+        from ...ops.cpu_optimizers import cpu_adam_flat
+        z, s, a = self.z, self.z.store, self.a
+        st = {k: self.host[k][lo - a:hi - a] for k in s.states if s.states[k] is not None}
+        cpu_adam_flat(self.host["master"][lo - a:hi - a], grad, st["exp_avg"], st["exp_avg_sq"],
+                      g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))),
+                      g.get("eps", 1e-8), g.get("weight_decay", 0.0), z.adamw, g.get("bias_correction", True),
+                      bf16_out=out if out.dtype == torch.bfloat16 else None, grad_scale=coef)
+        if out.dtype != torch.bfloat16:
+            out.copy_(self.host["master"][lo - a:hi - a])
+
+    def _forward_order(self, pieces):
+        """Piece indices in the order the next forward reaches them: pieces of persistent (root) units first, then
+        by the earliest forward position of any unit they overlap (the recorded trace, else store order)."""
+        z = self.z
+        trace = list(dict.fromkeys(getattr(z, "_fwd_trace", None) or []))
+        pos = {uid: i for i, uid in enumerate(trace)}
+        units = [(u.store_off, u.store_off + u.shard, -1 if u.persistent else pos.get(u.uid, len(pos) + u.uid))
+                 for u in z.units if u.shard]
+
+        def key(i):
+            lo, hi, _ = pieces[i]
+            ranks = [r for a0, b0, r in units if a0 < hi and lo < b0]
+            return (min(ranks) if ranks else 1 << 30, lo)
+
+        return sorted(range(len(pieces)), key=key)
+
+    def _step_on_host_sync(self, pieces, coef, lp_flat, cur):
+        s = self.z.store
         big = max(hi - lo for lo, hi, _ in pieces)
         if self._h_grad is None or self._h_grad[0].numel() < big:
             self._h_grad = [torch.empty(big, dtype=s.grad.dtype, pin_memory=self.cuda) for _ in range(2)]
             self._h_lp = [torch.empty(big, dtype=lp_flat.dtype, pin_memory=self.cuda) for _ in range(2)]
-        coef = float(coef) if not torch.is_tensor(coef) else float(coef.item())
         d2h, h2d = [None, None], [None, None]
 
         def issue_d2h(i):
@@ -356,15 +463,8 @@ class OptimizerStateOffload:
                 d2h[b].synchronize()
                 if h2d[b] is not None:
                     h2d[b].synchronize()  # staging buffer b is free again
-            a = self.a
-            st = {k: self.host[k][lo - a:hi - a] for k in s.states if s.states[k] is not None}
             out = self._h_lp[b][:n]
-            cpu_adam_flat(self.host["master"][lo - a:hi - a], self._h_grad[b][:n], st["exp_avg"], st["exp_avg_sq"],
-                          g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))),
-                          g.get("eps", 1e-8), g.get("weight_decay", 0.0), z.adamw, g.get("bias_correction", True),
-                          bf16_out=out if out.dtype == torch.bfloat16 else None, grad_scale=coef)
-            if out.dtype != torch.bfloat16:
-                out.copy_(self.host["master"][lo - a:hi - a])
+            self._adam_piece(lo, hi, g, self._h_grad[b][:n], out, coef)
             if self.cuda:
                 with torch.cuda.stream(self.reload_stream):
                     lp_flat[lo:hi].copy_(out, non_blocking=True)
@@ -375,13 +475,121 @@ class OptimizerStateOffload:
         if self.cuda:
             cur.wait_stream(self.reload_stream)
             cur.wait_stream(self.stream)  # the gradient buffer is zeroed after step()
-        self.host_steps = getattr(self, "host_steps", 0) + 1
+
+    def _step_on_host_async(self, pieces, coef, lp_flat, cur):
+        import threading
+        s, a = self.z.store, self.a
+        n_tail = s.numel - a
+        if self._h_grad_full is None or self._h_grad_full.numel() != n_tail or self._h_grad_full.dtype != s.grad.dtype:
+            self._h_grad_full = torch.empty(n_tail, dtype=s.grad.dtype, pin_memory=True)
+            self._h_lp_full = torch.empty(n_tail, dtype=lp_flat.dtype, pin_memory=True)
+        order = self._forward_order(pieces)
+        d2h = [None] * len(pieces)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ev)
+            for i in order:
+                lo, hi, _ = pieces[i]
+                self._h_grad_full[lo - a:hi - a].copy_(s.grad[lo:hi], non_blocking=True)
+                d2h[i] = torch.cuda.Event()
+                d2h[i].record(self.stream)
+                s.grad[lo:hi].zero_()  # the tail's zero_grad, behind its own D2H (zero_grad skips the tail)
+            self._tail_grads_free = torch.cuda.Event()
+            self._tail_grads_free.record(self.stream)
+        ready = [threading.Event() for _ in pieces]
+        h2d = [None] * len(pieces)
+        dev = self.z.device
+        self._async = {"pieces": pieces, "ready": ready, "h2d": h2d, "err": None}
+        # unit -> the pieces it overlaps (the forward waits for exactly those)
+        self._unit_pieces = {}
+        for u in self.z.units:
+            lo_u, hi_u = u.store_off, u.store_off + u.shard
+            idx = [i for i, (lo, hi, _) in enumerate(pieces) if lo < hi_u and lo_u < hi]
+            if idx:
+                self._unit_pieces[u.uid] = idx
+        rec = self._async
+
+        def run():
+            try:
+                torch.cuda.set_device(dev)
+                for i in order:
+                    lo, hi, g = pieces[i]
+                    d2h[i].synchronize()
+                    out = self._h_lp_full[lo - a:hi - a]
+                    self._adam_piece(lo, hi, g, self._h_grad_full[lo - a:hi - a], out, coef)
+                    with torch.cuda.stream(self.reload_stream):
+                        lp_flat[lo:hi].copy_(out, non_blocking=True)
+                        e = torch.cuda.Event()
+                        e.record(self.reload_stream)
+                    h2d[i] = e
+                    ready[i].set()
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the training thread at the next wait
+                rec["err"] = e
+                for r in ready:
+                    r.set()
+
+        self._thread = threading.Thread(target=run, name="hds-host-step", daemon=True)
+        self._thread.start()
+        self.async_steps = getattr(self, "async_steps", 0) + 1
+
+    def _wait_pieces(self, idx, stream=None):
+        rec = self._async
+        if rec is None:
+            return
+        for i in idx:
+            rec["ready"][i].wait()
+            if rec["err"] is not None:
+                raise RuntimeError("host-step optimizer thread failed") from rec["err"]
+            e = rec["h2d"][i]
+            if e is not None:
+                (stream or torch.cuda.current_stream()).wait_event(e)
+
+    def wait_unit(self, u):
+        """Before unit ``u`` computes (its forward pre-hook, the root units at the forward start): order the current
+        stream after the H2D of the host-stepped pieces holding its parameters."""
+        if self._async is None:
+            return
+        idx = self._unit_pieces.pop(u.uid, None)
+        if idx:
+            self._wait_pieces(idx)
+        if not self._unit_pieces:
+            self.join()
+
+    def before_backward(self):
+        """The backward writes gradients into the tail: after the tail's D2H and zeroing (copy stream)."""
+        ev = self.__dict__.pop("_tail_grads_free", None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
+    def join(self):
+        """Wait for the host-step thread (every piece issued) and order the current stream after all its H2D: before
+        the next step, a checkpoint, or any reader of the host states."""
+        t = self.__dict__.get("_thread")
+        rec = self._async
+        if t is not None:
+            t.join()
+            self._thread = None
+        if rec is not None:
+            self._async = None
+            self._unit_pieces = {}
+            if rec["err"] is not None:
+                raise RuntimeError("host-step optimizer thread failed") from rec["err"]
+            cur = torch.cuda.current_stream()
+            for e in rec["h2d"]:
+                if e is not None:
+                    cur.wait_event(e)
+
+    @property
+    def async_pending(self):
+        return self._async is not None
 
     def wait_tails(self):
         """Before ``step()``: every tail chunk on the device and ordered before the current stream (states stay
         split). Host-step tails stay where they are."""
         if not self.offloaded:
             return
+        self.join()  # an async host step of the previous step must have issued every piece
         if self.host_step:
             return
         self.reload()
@@ -396,6 +604,7 @@ class OptimizerStateOffload:
     def wait(self):
         """Whole flat states on the device (checkpoint save / load, fp32 fragment access): reload the tails and
         concatenate each state; they stay whole until the next step's ``offload()``."""
+        self.join()
         if self.host_step and self.offloaded:
             self.reload()
             self.host_step, hs = False, True
@@ -445,5 +654,7 @@ class OptimizerStateOffload:
                 "reload_pos": self.reload_pos, "ratio": self.ratio, "split_element": self.a,
                 "chunks": len(self.bounds), "chunk_mb": round(self.chunk_bytes / 2**20, 3),
                 "host_step": self.host_step, "host_steps": getattr(self, "host_steps", 0),
+                "async_host_steps": getattr(self, "async_steps", 0),
                 "fwd_waits": self.fwd_waits, "fwd_wait_s": round(self.fwd_wait_s, 3),
+                **({"auto_ratio": self.auto_info} if self.auto_ratio else {}),
                 "states": sorted(self.host) if self.host else sorted(self._keys())}

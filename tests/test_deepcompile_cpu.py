@@ -294,6 +294,44 @@ def test_offload_adam_states_host_step_fp16_dynamic(world):
     run_distributed(_state_host_step_fp16_run, world)
 
 
+def _resplit_run(rank, world):
+    import hcache_deepspeed_amd as ds
+    from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, tiny
+    res = {}
+    for mode in ("resident", "resplit"):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(tiny(**TINY))
+        cfg = {"train_micro_batch_size_per_gpu": 2, "bf16": {"enabled": True},
+               "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}, "zero_optimization": {"stage": 3},
+               "compile": {"offload_opt_states": mode != "resident"}}
+        eng, _, _, _ = ds.initialize(model=m, config=cfg)
+        if mode != "resident":
+            eng.compile(compile_kwargs={"offload_states_ratio": 1.0, "offload_states_chunk_mb": 0.05,
+                                        "offload_states_host_step": True})
+        g = torch.Generator().manual_seed(5 + rank)
+        losses = []
+        for step in range(4):
+            x = torch.randint(0, TINY["vocab_size"], (2, 12), generator=g)
+            loss = eng(x, labels=x)
+            eng.backward(loss)
+            eng.step()
+            losses.append(float(loss))
+            if mode != "resident" and step == 0:  # what autotune_ratio does after the first (all-host) step
+                so = eng.optimizer.state_offload
+                assert so.a == 0
+                so._resplit(0.4)
+                assert 0 < so.a < eng.optimizer.store.numel and eng.optimizer.store.master.numel() == so.a
+        res[mode] = losses
+    assert res["resplit"] == pytest.approx(res["resident"], rel=1e-3, abs=1e-3)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_state_offload_resplit_after_first_step(world):
+    """offload_states_ratio "auto": the first step runs with every state on the host, then the split point moves to
+    the ratio the measured peak leaves room for (heads back on the device, tails stay): the trajectory continues."""
+    run_distributed(_resplit_run, world)
+
+
 def test_param_offload_plan():
     """offload_parameters pass: units fetched in both phases are kept on the device first, then the smallest, within
     the budget; units with no fetch are ignored."""

@@ -318,7 +318,8 @@ def test_chunked_state_offload_matches_resident_gpu():
 
 
 @pytest.mark.gpu
-def test_state_offload_host_step_gpu():
+@pytest.mark.parametrize("async_step", [True, False])
+def test_state_offload_host_step_gpu(async_step):
     """``offload_states_host_step`` on the GPU: the tails stay in pinned host memory and step there (gradient D2H,
     host Adam, bf16 H2D on the copy streams) while the fused kernels step the heads; no reload before any step, and
     the losses and weights follow the resident run."""
@@ -340,6 +341,9 @@ def test_state_offload_host_step_gpu():
             eng.compile(compile_kwargs={"offload_states_ratio": 0.55, "offload_states_chunk_mb": 0.05,
                                         "offload_states_host_step": True})
             so = eng.optimizer.state_offload
+            # async: a worker thread steps the tails in forward order and each unit's forward waits for its own
+            # pieces only (the root unit first); sync: the pieces step inside step()
+            so.async_host_step = async_step
         g = torch.Generator(device="cuda").manual_seed(5)
         losses = []
         for _ in range(4):
@@ -352,6 +356,7 @@ def test_state_offload_host_step_gpu():
         if off:
             st = so.stats()
             assert st["host_step"] and st["host_steps"] == 4 and st["reloads"] == 0, st
+            assert st["async_host_steps"] == (4 if async_step else 0), st
             assert all(c is None for cs in so.tail.values() for c in cs)
             so.wait()
         from hcache_deepspeed_amd.utils.tensor_fragment import safe_get_full_fp32_param
