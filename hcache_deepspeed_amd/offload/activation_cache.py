@@ -161,6 +161,8 @@ class HostActivationCache:
         self._capped_this_step = 0
         self._attached = []
         self._wrapped = []  # blocks whose forward attach() wrapped (restored by detach)
+        self._cal_recompute = set()  # blocks checkpointed during the calibration step (pinned budget used up)
+        self._last_layer_bytes = 0
         self._cal_bytes = {}  # per-layer eligible bytes measured by the calibration step
         self._turn_peak = None  # max allocation at the forward/backward turn-around of the last step
         self.plan_adjustments = 0
@@ -292,7 +294,7 @@ class HostActivationCache:
         from ..runtime.activation_checkpointing import checkpointing as ck
 
         def run(*args, **kwargs):
-            if i in self.recompute and torch.is_grad_enabled():
+            if (i in self.recompute or i in self._cal_recompute) and torch.is_grad_enabled():
                 return ck.checkpoint(fwd, *args, **kwargs)
             return fwd(*args, **kwargs)
 
@@ -301,6 +303,13 @@ class HostActivationCache:
     def _enter(self, i):
         if torch.is_grad_enabled():
             self.cur_layer = i
+            # calibration of the recompute policies spills every eligible tensor; once the pinned-host budget is
+            # nearly used up the remaining blocks of that step are checkpointed instead -- kept on the device their
+            # activations would overflow the HBM (32k x mb2: ~290 GB of saved activations against a 160 GiB host
+            # budget). Their per-layer bytes are filled in from the measured blocks when the plan is made.
+            if (self._calibrating and self.policy_recompute and self.host_budget is not None
+                    and self.host_in_use + self._last_layer_bytes >= self.host_budget):
+                self._cal_recompute.add(i)
 
     def _peak_fold(self):
         """The allocator's peak since its last reset, folded into the running max of this step."""
@@ -361,6 +370,15 @@ class HostActivationCache:
                 # tensors the host cap kept on the GPU were all alive at the forward/backward turn-around, so the
                 # "everything spilled" peak is the measured one minus them (plan_offload adds kept layers back)
                 peak = self.last_step_peak - self._capped_this_step
+                if self._cal_recompute:
+                    # blocks the calibration checkpointed (host budget used up) saved only their inputs: plan them
+                    # with the bytes the fully measured blocks saved (transformer blocks are alike)
+                    full = [b for li, b in self.layer_bytes.items() if li not in self._cal_recompute]
+                    if full:
+                        mean = sum(full) // len(full)
+                        for li in self._cal_recompute:
+                            self.layer_bytes[li] = max(self.layer_bytes.get(li, 0), mean)
+                    self._cal_recompute = set()
                 self.plan = calibrated_plan(self.layer_bytes, peak + self._capped_this_step, self._capped_this_step,
                                             self.plan_budget())
                 self._calibrating = False
@@ -483,6 +501,7 @@ class HostActivationCache:
             return _Tagged(t, self.cur_layer) if self.by_layer else t
         nbytes = t.numel() * t.element_size()
         self.layer_bytes[self.cur_layer] = self.layer_bytes.get(self.cur_layer, 0) + nbytes
+        self._last_layer_bytes = max(self._last_layer_bytes, self.layer_bytes[self.cur_layer])
         if self.plan is not None and self.cur_layer not in self.plan:
             if torch.cuda.memory_allocated(self.device) + nbytes <= self.budget:
                 return _Tagged(t, self.cur_layer) if self.by_layer else t  # tag only when something was spilled
