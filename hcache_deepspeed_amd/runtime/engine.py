@@ -547,12 +547,21 @@ class DeepSpeedEngine(EngineApiMixin, nn.Module):
     # ------------------------------------------------------------------------------------
     # checkpointing (layout: runtime/checkpointing.py)
     # ------------------------------------------------------------------------------------
+    def _settle_host_step(self):
+        """An asynchronous host step (state offload host_step) may still be writing parameters: finish it before
+        anything reads the parameters or states outside the forward's per-unit waits."""
+        so = getattr(self.optimizer, "state_offload", None)
+        if so is not None and hasattr(so, "join"):
+            so.join()
+
     def save_checkpoint(self, save_dir, tag=None, client_state=None, save_latest=True, exclude_frozen_parameters=False):
+        self._settle_host_step()
         from .checkpointing import save_checkpoint
         return save_checkpoint(self, save_dir, tag, client_state or {}, save_latest, exclude_frozen_parameters)
 
     def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
                         load_lr_scheduler_states=True, load_module_only=False, custom_load_fn=None):
+        self._settle_host_step()
         from .checkpointing import load_checkpoint
         return load_checkpoint(self, load_dir, tag, load_module_strict, load_optimizer_states,
                                load_lr_scheduler_states, load_module_only)
@@ -561,6 +570,7 @@ class DeepSpeedEngine(EngineApiMixin, nn.Module):
         """Consolidated 16-bit weights. Under ZeRO-3 this needs ``stage3_gather_16bit_weights_on_model_save``, as in
         the reference (engine.py:3835): without it nothing is gathered and False is returned."""
         from .checkpointing import save_16bit_model
+        self._settle_host_step()
         if self.zero_optimization_partition_weights() and getattr(self.optimizer, "partitioned", False) and \
                 not self.zero_gather_16bit_weights_on_model_save():
             logger.warning("Did not save the model: zero_optimization.stage3_gather_16bit_weights_on_model_save is "
@@ -569,6 +579,7 @@ class DeepSpeedEngine(EngineApiMixin, nn.Module):
         return save_16bit_model(self, save_dir, save_filename)
 
     def module_state_dict(self, destination=None, prefix="", keep_vars=False, exclude_frozen_parameters=False):
+        self._settle_host_step()
         if self.zero_optimization_stage() == 3 and self.optimizer.partitioned:
             return None
         return self.module.state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)

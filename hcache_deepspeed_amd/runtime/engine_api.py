@@ -725,7 +725,10 @@ class EngineApiMixin:
                     pass
             if hasattr(z, "_hook_handles"):
                 z._hook_handles = []
-            if getattr(z, "state_offload", None) is not None:
+            so = getattr(z, "state_offload", None)
+            if so is not None:
+                if hasattr(so, "join"):
+                    so.join()  # an async host step still writing parameters
                 z.state_offload = None
             if self.zero_optimization_stage() == 3 and hasattr(z, "release_all"):
                 try:
