@@ -104,6 +104,8 @@ class HostActivationCache:
         self._cal_copy = [None, None, 0]  # calibration copies: first-start event, last-end event, bytes
         self.pcie_gbps = None
         self.recompute = set()  # blocks whose forward is checkpointed (policy "recompute")
+        self.resident_block_bytes = 0  # measured device footprint of a block kept resident (recompute policies)
+        self._blk_mark = None
         # D2H copy window: spilled bytes the host may have queued on the copy stream and not yet seen copied.
         # Autograd runs far ahead of the GPU on the host, and a spilled tensor's HBM is recycled only once its D2H
         # drained (record_stream) -- with PCIe slower than a layer's forward the backlog grows layer by layer. Left
@@ -218,6 +220,7 @@ class HostActivationCache:
         for i, b in enumerate(blocks):
             self._attached.append(b.register_forward_pre_hook(lambda mod, args, i=i: self._enter(i)))
             if self.policy_recompute:
+                self._attached.append(b.register_forward_hook(lambda mod, args, out, i=i: self._exit(i, out)))
                 b.forward = self._recompute_wrapper(b.forward, i)
                 self._wrapped.append(b)
             elif self.ckpt_offload:
@@ -308,8 +311,36 @@ class HostActivationCache:
             # activations would overflow the HBM (32k x mb2: ~290 GB of saved activations against a 160 GiB host
             # budget). Their per-layer bytes are filled in from the measured blocks when the plan is made.
             if (self._calibrating and self.policy_recompute and self.host_budget is not None
+                    and i < self.n_layers - self.keep
                     and self.host_in_use + self._last_layer_bytes >= self.host_budget):
                 self._cal_recompute.add(i)
+            if self.policy_recompute and self.device.type == "cuda":
+                self._blk_mark = (i, torch.cuda.memory_allocated(self.device))
+
+    def _exit(self, i, out):
+        """End of a block's forward (recompute policies): what a block kept on the device -- the growth of the
+        allocation over its forward minus its output (which a checkpointed block holds too) -- measured on the blocks
+        that were NOT checkpointed. The recompute plans price a block they stop recomputing with it: the bytes
+        ``_pack`` counts miss what a block keeps outside the saved-tensor hooks, and at 32k x mb2 a plan sized from
+        those counts kept 16 blocks resident and ran out of HBM in the next forward."""
+        mark = getattr(self, "_blk_mark", None)
+        self._blk_mark = None
+        if mark is None or mark[0] != i or not torch.is_grad_enabled() or self.device.type != "cuda":
+            return
+        if i in self.recompute or i in self._cal_recompute or (self.plan and i in self.plan):
+            return
+        if self._calibrating and i < self.n_layers - self.keep:
+            return  # spilled during calibration: its saved tensors left for the host
+        outs = out if isinstance(out, (tuple, list)) else (out, )
+        ob = sum(o.numel() * o.element_size() for o in outs if torch.is_tensor(o))
+        kept = torch.cuda.memory_allocated(self.device) - mark[1] - ob
+        self.resident_block_bytes = max(self.resident_block_bytes, kept)
+
+    def _rc_bytes(self):
+        """Per-block bytes the recompute plans use: the counted saved bytes, raised to the measured footprint of a
+        resident block (``_exit``)."""
+        rb = self.resident_block_bytes
+        return {li: max(b, rb) for li, b in self._cal_bytes.items()}
 
     def _peak_fold(self):
         """The allocator's peak since its last reset, folded into the running max of this step."""
@@ -379,10 +410,11 @@ class HostActivationCache:
                         for li in self._cal_recompute:
                             self.layer_bytes[li] = max(self.layer_bytes.get(li, 0), mean)
                     self._cal_recompute = set()
-                self.plan = calibrated_plan(self.layer_bytes, peak + self._capped_this_step, self._capped_this_step,
+                self._cal_bytes = dict(self.layer_bytes)
+                lb = self._rc_bytes() if self.policy_recompute else self.layer_bytes
+                self.plan = calibrated_plan(lb, peak + self._capped_this_step, self._capped_this_step,
                                             self.plan_budget())
                 self._calibrating = False
-                self._cal_bytes = dict(self.layer_bytes)
                 if self.policy_recompute:  # the same over-budget layers, recomputed instead of spilled
                     self.recompute, self.plan = set(self.plan), set()
                     if self.hybrid:
@@ -397,7 +429,8 @@ class HostActivationCache:
                 self._hybrid_split()
             elif self._turn_peak is not None:
                 cur = self.recompute if self.policy_recompute else self.plan
-                new = refine_plan(cur, self._cal_bytes, self._turn_peak, self.plan_budget())
+                new = refine_plan(cur, self._rc_bytes() if self.policy_recompute else self._cal_bytes,
+                                  self._turn_peak, self.plan_budget())
                 if new != cur:
                     self.plan_adjustments += 1
                     if self.policy_recompute:
@@ -640,7 +673,8 @@ class HostActivationCache:
                 "peak_gib_all_steps": round(self.peak_seen / 2**30, 1),
                 "last_step_peak_gib": round(self.last_step_peak / 2**30, 2),
                 "step_peaks_gib": [round(x / 2**30, 1) for x in self.step_peak_history[-16:]],
-                "bwd_extra_gib": round(self.bwd_extra / 2**30, 2)}
+                "bwd_extra_gib": round(self.bwd_extra / 2**30, 2),
+                "resident_block_gib": round(self.resident_block_bytes / 2**30, 2)}
 
 
 def refine_plan(plan, layer_bytes, turn_peak, budget, margin=1 << 30):

@@ -281,6 +281,40 @@ def test_refine_plan_closed_loop():
     assert refine_plan({5, 6}, lb, turn_peak=100, budget=85 + G) == {5, 6, 7}            # runs out of layers
 
 
+def test_recompute_plans_price_blocks_at_measured_footprint(monkeypatch):
+    """Recompute policies: a block that was not checkpointed reports what it kept on the device (allocation growth
+    minus its outputs); the plans price every block at least that, so a refinement cannot keep more blocks
+    resident than the HBM holds (32k x mb2 ran out of memory when priced at the hook-counted bytes)."""
+    import types
+    from hcache_deepspeed_amd.offload.activation_cache import HostActivationCache, refine_plan
+    cache = HostActivationCache(torch.device("cpu"), recompute=True)
+    cache.n_layers, cache.keep = 8, 2
+    cache.device = types.SimpleNamespace(type="cuda")
+    alloc = [0]
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda dev=None: alloc[0])
+    out = (torch.zeros(4, dtype=torch.bfloat16), torch.zeros(4, dtype=torch.bfloat16))  # 16 B of outputs
+    cache.recompute = {0, 1, 2}
+    for i, grew in [(1, 1000), (5, 96)]:  # block 1 checkpointed: ignored; block 5 resident: kept 96 - 16 B
+        cache._enter(i)
+        alloc[0] += grew
+        cache._exit(i, out)
+    assert cache.resident_block_bytes == 80
+    cache._cal_bytes = {i: 50 for i in range(6)}
+    assert cache._rc_bytes() == {i: 80 for i in range(6)}
+    G = 1 << 30
+    # 170 B of slack: 3 blocks at the counted 50 B, but only 2 at the measured 80 B
+    assert refine_plan(set(range(6)), cache._cal_bytes, turn_peak=100, budget=270 + G) == {0, 1, 2}
+    assert refine_plan(set(range(6)), cache._rc_bytes(), turn_peak=100, budget=270 + G) == {0, 1, 2, 3}
+    # calibration: spilled blocks are not measured, the always-resident last blocks are and are never checkpointed
+    cache.resident_block_bytes, cache._calibrating, cache.recompute = 0, True, set()
+    cache.host_budget, cache.host_in_use, cache._last_layer_bytes = 10, 10, 5
+    for i, grew in [(3, 500), (6, 116)]:
+        cache._enter(i)
+        alloc[0] += grew
+        cache._exit(i, out)
+    assert cache._cal_recompute == {3} and cache.resident_block_bytes == 100
+
+
 def test_recompute_policy_wraps_planned_blocks():
     """policy "recompute": the planned blocks run under activation checkpointing (same outputs and gradients,
     no saved activations of their internals), the others are untouched."""
