@@ -123,8 +123,17 @@ def _permuted_weight(w, b, n_q, n_kv, D, P):
 class _FPDTAttnFn(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, x, w, b, cos, sin, n_q, n_kv, D, group, B, num_chunks, offload, scale):
-        """x [B*Sl, H] (FPDT layout) -> attention output [B*Sl, n_q*D] (before the output projection)."""
+    def forward(ctx, x, w, b, cos, sin, n_q, n_kv, D, group, B, num_chunks, offload, scale, keep=True):
+        """x [B*Sl, H] (FPDT layout) -> attention output [B*Sl, n_q*D] (before the output projection).
+
+        ``keep`` False (a no-grad forward, e.g. the first pass of a checkpointed block): nothing goes to the
+        segment store -- no backward will read it -- and the previous segments' K/V stay on the device (GQA: 2 GiB
+        at 512k tokens), so the forward moves no bytes over PCIe. Inside a checkpointed block with the attention
+        stash (``ops.attention.AttnStash``), "record" keeps every segment's merged (o, lse) and "replay" -- the
+        backward's recompute -- takes them back instead of re-running the segment-pair attention (at 512k tokens
+        about a sixth of the step)."""
+        from ..ops.attention import AttnStash
+        mode = AttnStash.mode
         P = dist.get_world_size(group) if group is not None else 1
         T, H = x.shape
         Sl = T // B
@@ -134,7 +143,7 @@ class _FPDTAttnFn(torch.autograd.Function):
         L = P * cs  # global segment length
         wp, bp, perm = _permuted_weight(w, b, n_q, n_kv, D, P)
         xv = x.view(B, Sl, H)
-        store = _HostChunks(offload, x.device)
+        store = _HostChunks(offload and keep, x.device)
         out = torch.empty(B, Sl, n_q * D, device=x.device, dtype=x.dtype)
         ks, vs = [], []  # previous segments' K/V (device-resident unless offloading)
         for i in range(num_chunks):
@@ -145,27 +154,34 @@ class _FPDTAttnFn(torch.autograd.Function):
             q = full[:, :nql].contiguous()
             k = full[:, nql:nql + nkvl].contiguous()
             v = full[:, nql + nkvl:].contiguous()
-            o, lse = None, None
-            for j in range(i):
-                if store.offload:
-                    if j + 1 < i:
-                        store.prefetch(("k", j + 1), x.device)
-                        store.prefetch(("v", j + 1), x.device)
-                    kj, vj = store.get(("k", j), x.device), store.get(("v", j), x.device)
-                else:
-                    kj, vj = ks[j], vs[j]
-                ob, lb = attn_block_fwd(q, kj, vj, False, scale, L)
+            if mode == "replay":
+                o, lse = AttnStash.items.pop(0)
+                assert o.shape == q.shape and lse.shape == (nql, q.shape[0]), "FPDT attention stash out of order"
+            else:
+                o, lse = None, None
+                for j in range(i):
+                    if store.offload:
+                        if j + 1 < i:
+                            store.prefetch(("k", j + 1), x.device)
+                            store.prefetch(("v", j + 1), x.device)
+                        kj, vj = store.get(("k", j), x.device), store.get(("v", j), x.device)
+                    else:
+                        kj, vj = ks[j], vs[j]
+                    ob, lb = attn_block_fwd(q, kj, vj, False, scale, L)
+                    o, lse = merge_attn_out(o, lse, ob, lb)
+                ob, lb = attn_block_fwd(q, k, v, True, scale, L)
                 o, lse = merge_attn_out(o, lse, ob, lb)
-            ob, lb = attn_block_fwd(q, k, v, True, scale, L)
-            o, lse = merge_attn_out(o, lse, ob, lb)
-            if not store.offload:
-                ks.append(k)
-                vs.append(v)
-            o = o.to(x.dtype)
+                if not store.offload:
+                    ks.append(k)
+                    vs.append(v)
+                o = o.to(x.dtype)
+                if mode == "record":
+                    AttnStash.items.append((o, lse))
             oo = head_to_seq(o, group, B) if P > 1 else o  # [B*cs, n_q, D]
             out[:, i * cs:(i + 1) * cs] = oo.view(B, cs, n_q * D)
-            for key, t in (("q", q), ("k", k), ("v", v), ("o", o), ("lse", lse)):
-                store.put((key, i), t)
+            if keep:
+                for key, t in (("q", q), ("k", k), ("v", v), ("o", o), ("lse", lse)):
+                    store.put((key, i), t)
         ctx.save_for_backward(x, wp, bp)
         ctx.store, ctx.perm, ctx.has_b = store, perm, b is not None
         ctx.meta = (n_q, n_kv, D, group, B, num_chunks, scale, P, cs, L)
@@ -222,15 +238,16 @@ class _FPDTAttnFn(torch.autograd.Function):
         dw = dwp.view(n_q + 2 * n_kv, D, H).index_select(0, inv).reshape(wp.shape).to(wp.dtype)
         db = None if dbp is None else dbp.view(n_q + 2 * n_kv, D).index_select(0, inv).reshape(-1).to(bp.dtype)
         ctx.store = None
-        return dx.view(T, H), dw, db, None, None, None, None, None, None, None, None, None, None
+        return dx.view(T, H), dw, db, None, None, None, None, None, None, None, None, None, None, None
 
 
 def fpdt_attention(x, qkv_weight, qkv_bias, cos, sin, n_q, n_kv, head_dim, group, batch, num_chunks,
                    offload=False, softmax_scale=None):
     """Causal FPDT attention core: [B*Sl, H] (FPDT layout) -> [B*Sl, n_q*head_dim]."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(head_dim)
+    keep = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (x, qkv_weight, qkv_bias))
     return _FPDTAttnFn.apply(x, qkv_weight, qkv_bias, cos, sin, n_q, n_kv, head_dim, group, batch, num_chunks,
-                             offload, scale)
+                             offload, scale, keep)
 
 
 class FPDT_Attention(torch.nn.Module):

@@ -35,6 +35,47 @@ def test_fpdt_attention_single_rank_chunks():
         assert torch.allclose(gw, gw0, atol=1e-4), nc
 
 
+def test_fpdt_attention_replays_checkpoint_stash(monkeypatch):
+    """Inside a checkpointed block with the attention stash, the recompute takes every segment's (o, lse) back
+    instead of re-running the segment-pair attention; outputs and gradients are unchanged, and a no-grad forward
+    gives the same output without filling the segment store."""
+    from hcache_deepspeed_amd.ops import attention as A
+    from hcache_deepspeed_amd.ops.rope import rope_tables
+    from hcache_deepspeed_amd.parallel import fpdt as F
+    from hcache_deepspeed_amd.runtime.activation_checkpointing.checkpointing import checkpoint_saved_inputs
+    torch.manual_seed(0)
+    B, S, H, n_q, n_kv, D, nc = 2, 48, 64, 4, 2, 16, 3
+    x = torch.randn(B * S, H, requires_grad=True)
+    w = (torch.randn((n_q + 2 * n_kv) * D, H) * 0.1).requires_grad_(True)
+    cos, sin = rope_tables(S, D)
+
+    def block(xx):
+        return F.fpdt_attention(xx, w, None, cos, sin, n_q, n_kv, D, None, B, nc).square()
+
+    y0 = block(x)
+    g = torch.randn_like(y0)
+    gx0, gw0 = torch.autograd.grad(y0, (x, w), g)
+    calls = []
+    real = F.attn_block_fwd
+    monkeypatch.setattr(F, "attn_block_fwd", lambda *a: calls.append(1) or real(*a))
+    puts = []
+    real_put = F._HostChunks.put
+    monkeypatch.setattr(F._HostChunks, "put", lambda self, k, t: puts.append(k) or real_put(self, k, t))
+    y = checkpoint_saved_inputs(block, x, stash_attention=True)
+    n_fwd = len(calls)
+    assert n_fwd == nc * (nc + 1) // 2 and not puts  # the no-grad first pass: every pair once, nothing stored
+    y.backward(g)  # the weight is closed over: its gradient accumulates in .grad (reentrant-style checkpoint)
+    gx, gw = x.grad, w.grad
+    assert len(calls) == n_fwd  # the recompute replayed the stash
+    assert len([k for k in puts if k[0] != "do"]) == 5 * nc  # q, k, v, o, lse of every segment (recompute)
+    torch.testing.assert_close(y, y0)
+    torch.testing.assert_close(gx, gx0)
+    torch.testing.assert_close(gw, gw0)
+    assert A.AttnStash.mode is None
+    with torch.no_grad():
+        torch.testing.assert_close(block(x), y0.detach())
+
+
 def test_chunked_ffn_and_logits_loss():
     from hcache_deepspeed_amd.parallel.fpdt import FPDT_FFN, FPDT_LogitsLoss, fpdt_gated_ffn
     torch.manual_seed(1)
