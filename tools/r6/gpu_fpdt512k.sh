@@ -5,5 +5,5 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r6fpdt
 mkdir -p $O
-HDS_BENCH_PROGRESS=1 timeout -k 10 1100 python bench.py --steps 1 --warmup 1 --seq 524288 --micro-batch 1 --fpdt-chunk ${CHUNK:-65536} --host-act-cache --act-cache-policy ckpt_offload > $O/fpdt512k.json 2> $O/fpdt512k.err || { echo failed; tail -30 $O/fpdt512k.err; exit 1; }
-cat $O/fpdt512k.json
+HDS_BENCH_PROGRESS=1 timeout -k 10 1100 python bench.py --steps 1 --warmup 1 --seq 524288 --micro-batch 1 --fpdt-chunk ${CHUNK:-65536} ${FPDT_EXTRA:-} --host-act-cache --act-cache-policy ckpt_offload > $O/fpdt512k${TAG:-}.json 2> $O/fpdt512k${TAG:-}.err || { echo failed; tail -30 $O/fpdt512k${TAG:-}.err; exit 1; }
+cat $O/fpdt512k${TAG:-}.json
