@@ -28,9 +28,11 @@ if ROOT not in sys.path:
 
 
 def _use_tuned_gemms():
-    """Read the committed hipBLASLt/rocBLAS solution table (PyTorch TunableOp, tuned on MI355X for exactly the
-    bench's GEMM shapes by tools/gpu_tunableop.sh). Tuning is off: shapes missing from the table keep the
-    library heuristic. Must run before torch initialises its BLAS handles; HDS_TUNABLEOP=0 disables it."""
+    """Read the committed hipBLASLt/rocBLAS solution table (PyTorch TunableOp, tuned on MI355X for the bench's
+    GEMM shapes: tools/r6/gpu_tunableop_ab.sh; +0.5 % in an interleaved A/B, profiles/r6/tunableop_ab). TunableOp
+    reads one file per device ordinal (%d); the eight copies are identical. Tuning is off: shapes missing from the
+    table keep the library heuristic. Must run before torch initialises its BLAS handles; HDS_TUNABLEOP=0 disables
+    it."""
     table = os.path.join(ROOT, "tuning", "tunableop_results%d.csv")
     if os.environ.get("HDS_TUNABLEOP", "1") != "1" or not os.path.exists(table % 0):
         return False

@@ -8,9 +8,17 @@ db = sys.argv[1]
 c = sqlite3.connect(db)
 rows = c.execute("select name, start, end from kernels order by start").fetchall()
 adam = [r for r in rows if "adam_flat" in r[0]]
-if len(adam) < 2:
+# one optimizer step may launch several fused-Adam kernels (e.g. dense + expert parameter groups): dispatches closer
+# than 50 ms apart belong to the same step, whose end is its last dispatch
+ends = []
+for r in adam:
+    if ends and r[1] - ends[-1] < 50e6:
+        ends[-1] = r[2]
+    else:
+        ends.append(r[2])
+if len(ends) < 2:
     raise SystemExit("fewer than two optimizer steps in the trace")
-t0, t1 = adam[-2][2], adam[-1][2]
+t0, t1 = ends[-2], ends[-1]
 tot = defaultdict(float)
 cnt = defaultdict(int)
 for n, s, e in rows:
