@@ -40,7 +40,7 @@ for M, K, N in shapes:
     fl = 2 * M * N * K
     print(json.dumps({"M": M, "K": K, "N": N, "heuristic_ms": round(base, 4), "tuned_ms": round(tuned, 4),
                       "heuristic_tflops": round(fl / base / 1e9, 1), "tuned_tflops": round(fl / tuned / 1e9, 1),
-                      "results": {str(k): str(v) for k, v in (tun.get_results() or {}).items()} if hasattr(tun, "get_results") else None}),
+                      "results": [list(map(str, r)) for r in (tun.get_results() or ())]}),  # tuple of rows
           flush=True)
 tun.write_file()
 print("wrote", tun.get_filename())
