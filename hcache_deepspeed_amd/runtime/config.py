@@ -206,6 +206,12 @@ class MI355XConfig:
     zero3_max_reduce_inflight: int = 2
     zero3_unit_bucket_mb: float = 128  # per-submodule ZeRO-3 units of ModuleList-free models are bucketed to this
     direct_wgrad: bool = True  # weight-gradient GEMMs write into the flat gradient buffer (runtime/zero/linear.py)
+    # ZeRO-3 with device-resident optimizer states: step() queues the fused update unit by unit (forward order) on a
+    # side HIP stream and returns; each unit's forward waits only for its own piece (runtime/zero/optimizer.py
+    # ``_overlap_ok``). Off by default: on one MI355X the headline ran 24,837 / 24,883 tok/s with it against 24,909 /
+    # 24,913 without -- hipBLASLt's GEMM workgroups leave no room on a CU for the update's waves, so the two take
+    # turns instead of overlapping (profiles/r6/overlap_step/)
+    overlap_step: bool = False
     fused_lm_head_ce: bool = True
     # ZeRO-3 all-gather / reduce-scatter communicators run their RCCL kernels on high-priority HIP streams, so
     # the few workgroups a collective needs are dispatched ahead of queued GEMM tiles (overlap under full load)
@@ -355,6 +361,7 @@ class DeepSpeedConfig:
             cpu_threads_per_rank=m.get("cpu_threads_per_rank", "auto"),
             fpdt=dict(m["fpdt"]) if m.get("fpdt") else None,
             direct_wgrad=bool(m.get("direct_wgrad", True)),
+            overlap_step=bool(m.get("overlap_step", False)),
             fused_lm_head_ce=bool(m.get("fused_lm_head_ce", True)),
             comm_high_priority=bool(m.get("comm_high_priority", True)),
             host_act_cache=HostActCacheConfig(**{f.name: hac[f.name]

@@ -548,11 +548,15 @@ class DeepSpeedEngine(EngineApiMixin, nn.Module):
     # checkpointing (layout: runtime/checkpointing.py)
     # ------------------------------------------------------------------------------------
     def _settle_host_step(self):
-        """An asynchronous host step (state offload host_step) may still be writing parameters: finish it before
-        anything reads the parameters or states outside the forward's per-unit waits."""
+        """An asynchronous host step (state offload host_step) or an overlapped device step may still be writing
+        parameters: finish it before anything reads the parameters or states outside the forward's per-unit
+        waits."""
         so = getattr(self.optimizer, "state_offload", None)
         if so is not None and hasattr(so, "join"):
             so.join()
+        join = getattr(self.optimizer, "_join_step", None)
+        if join is not None:
+            join()  # an overlapped device step (ZeRO-3) may still be updating shards on its stream
 
     def save_checkpoint(self, save_dir, tag=None, client_state=None, save_latest=True, exclude_frozen_parameters=False):
         self._settle_host_step()

@@ -781,6 +781,7 @@ class ZeroOptimizer:
                     self.state_offload.on_forward_position()
             if self.state_offload is not None:  # this unit's host-stepped pieces (async host step) are on the device
                 self.state_offload.wait_unit(u)
+            self._wait_step(u)  # its piece of an overlapped step
             self._fetch(u, "forward")
 
         return pre
@@ -803,6 +804,7 @@ class ZeroOptimizer:
         def pre(module, args):
             if self.state_offload is not None:
                 self.state_offload.wait_unit(u)
+            self._wait_step(u)
             self._gather(u, wait=True)  # external parameter: kept until its own unit's release
 
         return pre
@@ -1173,6 +1175,7 @@ class ZeroOptimizer:
             if dev is not None and u.world == 1:
                 full = dev  # resident shard IS the unit: bind it, nothing to fetch
             else:
+                self._wait_step(u)  # the gather reads the shard an overlapped step may still be updating
                 full = torch.empty(u.padded, dtype=self.dtype, device=self.device)
             u.post_gather = None
             if dev is not None and u.world == 1:
@@ -1478,6 +1481,7 @@ class ZeroOptimizer:
     def prepare_backward(self, boundary):
         self.boundary = boundary
         self.in_backward = True
+        self._join_step()  # the overlapped step zeroes the gradient buffers on its stream
         so = self.state_offload
         if so is not None:
             so.before_backward()  # the tail gradients were copied out (and zeroed) on the copy stream
@@ -1537,6 +1541,7 @@ class ZeroOptimizer:
                 for u in self.root_units:
                     so.wait_unit(u)  # stepped first: the embeddings / LM head
         for u in self.root_units:
+            self._wait_step(u)  # overlapped step: the root units' pieces went first
             self._gather(u, wait=True)
 
     def post_forward(self):
@@ -1558,7 +1563,9 @@ class ZeroOptimizer:
     def cur_scale(self):
         return self.loss_scaler.loss_scale
 
-    def zero_grad(self, set_to_none=True):
+    def zero_grad(self, set_to_none=True, _in_step=False):
+        if not _in_step:
+            self._join_step()  # an overlapped step may still read (and then zero) the gradients on its stream
         so = self.state_offload
         if so is not None and so.async_pending:
             # async host step: the tail [a, n) is zeroed on the copy stream behind its own D2H; only the head here
@@ -1722,6 +1729,7 @@ class ZeroOptimizer:
         return self.state_offload
 
     def _states_resident(self):
+        self._join_step()
         if self.state_offload is not None:
             self.state_offload.wait()
 
@@ -1756,8 +1764,77 @@ class ZeroOptimizer:
         self._symm_flag_ev = torch.cuda.Event()
         self._symm_flag_ev.record()
 
+    # ------------------------------------------------------------------------------------
+    # overlapped step: the fused update runs unit by unit on a side stream under the next forward
+    # ------------------------------------------------------------------------------------
+    def _overlap_ok(self, so, lp_flat):
+        """ZeRO-3 with device-resident states, parameters and fused update: every reader of a unit's updated shard
+        goes through a per-unit hook (forward pre-hooks, gathers) that can wait for that unit's piece alone."""
+        on = getattr(self, "_overlap_on", None)
+        if on is None:
+            env = os.environ.get("HDS_OVERLAP_STEP")  # "1" / "0" overrides the config
+            on = self._overlap_on = (env == "1") if env in ("0", "1") else bool(getattr(self.mi, "overlap_step", False))
+        return (on and so is None and lp_flat is self.store.lp and self.stage == 3 and self.device.type == "cuda"
+                and self.kind in ("adam", "lion", "adagrad") and not self.offload_param and not self.nvme_param)
+
+    def _step_pieces(self):
+        """[(uid, lo, hi, segment)] of the store in the order the next forward reads it: the root units (embeddings,
+        LM head: needed first), then the units in recorded forward order, then the rest; a unit spanning several
+        parameter groups gets one piece per group. Store ranges no unit covers trail with uid None."""
+        key = tuple(self._fwd_trace or ())
+        cached = getattr(self, "_pieces_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        s = self.store
+        by_uid = {u.uid: u for u in self.units}
+        order = list(self.root_units)
+        seen = {u.uid for u in order}
+        for uid in key:
+            if uid not in seen and uid in by_uid:
+                order.append(by_uid[uid])
+                seen.add(uid)
+        order += [u for u in self.units if u.uid not in seen]
+        pieces, covered = [], []
+        for u in order:
+            a, b = u.store_off, u.store_off + u.shard
+            covered.append((a, b))
+            for sg in s.segments:
+                lo, hi = max(a, sg.store_off), min(b, sg.store_off + sg.numel)
+                if lo < hi:
+                    pieces.append((u.uid, lo, hi, sg))
+        covered.sort()
+        for sg in s.segments:
+            pos, end = sg.store_off, sg.store_off + sg.numel
+            for a, b in covered:
+                if b <= pos or a >= end:
+                    continue
+                if a > pos:
+                    pieces.append((None, pos, a, sg))
+                pos = max(pos, b)
+            if pos < end:
+                pieces.append((None, pos, end, sg))
+        self._pieces_cache = (key, pieces)
+        return pieces
+
+    def _wait_step(self, u):
+        """Order the current stream after ``u``'s piece of an overlapped step (no-op once waited)."""
+        evs = getattr(self, "_step_ev", None)
+        if evs:
+            ev = evs.pop(u.uid, None)
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def _join_step(self):
+        """Order the current stream after the whole overlapped step (every piece and its gradient zeroing): before
+        the backward writes gradients, the next step, or any reader of the flat store outside the unit hooks."""
+        ev = self.__dict__.pop("_step_done", None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+        self._step_ev = {}
+
     @torch.no_grad()
     def step(self, closure=None):
+        self._join_step()
         s = self.store
         symm = bool(getattr(self, "_symm", None))
         if symm:
@@ -1785,6 +1862,7 @@ class ZeroOptimizer:
         found_inf = self._inf_buf if self.loss_scaler.dynamic else (self._symm_skip if symm else None)
         for gi, group in enumerate(self.param_groups):
             group["step"] = group.get("step", 0) + 1
+        side = None  # the overlapped step's stream (set below when the update runs there)
         if self.kind == "generic":
             for mp, sg in self._generic_params:
                 mp.grad = s.seg(s.grad, sg).float() * coef
@@ -1802,28 +1880,50 @@ class ZeroOptimizer:
                     return so.view(k, lo, hi)
                 return (s.master if k == "master" else s.states[k])[lo:hi]
 
+            def update(lo, hi, g):  # one fused-optimizer launch over [lo, hi) of the store
+                p32, gr, lp = sv("master", lo, hi), s.grad[lo:hi], lp_flat[lo:hi]
+                if self.kind == "adam":
+                    fused.adam_flat(p32, gr, sv("exp_avg", lo, hi), sv("exp_avg_sq", lo, hi),
+                                    g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
+                                    g.get("weight_decay", 0.0), self.adamw, g.get("bias_correction", True),
+                                    lp_out=lp, grad_scale=1.0, dev_scale=coef, found_inf=found_inf)
+                elif self.kind == "lion":
+                    fused.lion_flat(p32, gr, sv("exp_avg", lo, hi), g["lr"] * g.get("lr_mult", 1.0),
+                                    tuple(g.get("betas", (0.9, 0.99))), g.get("weight_decay", 0.0), lp_out=lp,
+                                    dev_scale=coef, found_inf=found_inf)
+                elif self.kind == "adagrad":
+                    fused.adagrad_flat(p32, gr, sv("sum", lo, hi), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
+                                       g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
+
             hosted = []  # host-step tails of the state offload: updated on the host after the device pieces are queued
-            for sg in s.segments:
-                g = self._seg_group(sg)
-                lo0, hi0 = sg.store_off, sg.store_off + sg.numel
-                bounds = [lo0] + [c for c in cuts if lo0 < c < hi0] + [hi0]
-                for lo, hi in zip(bounds[:-1], bounds[1:]):
-                    if so is not None and so.hosted(lo):  # host-step tails never come back: step them there
-                        hosted.append((lo, hi, g))
-                        continue
-                    p32, gr, lp = sv("master", lo, hi), s.grad[lo:hi], lp_flat[lo:hi]
-                    if self.kind == "adam":
-                        fused.adam_flat(p32, gr, sv("exp_avg", lo, hi), sv("exp_avg_sq", lo, hi),
-                                        g["step"], g["lr"] * g.get("lr_mult", 1.0), tuple(g.get("betas", (0.9, 0.999))), g.get("eps", 1e-8),
-                                        g.get("weight_decay", 0.0), self.adamw, g.get("bias_correction", True),
-                                        lp_out=lp, grad_scale=1.0, dev_scale=coef, found_inf=found_inf)
-                    elif self.kind == "lion":
-                        fused.lion_flat(p32, gr, sv("exp_avg", lo, hi), g["lr"] * g.get("lr_mult", 1.0),
-                                        tuple(g.get("betas", (0.9, 0.99))), g.get("weight_decay", 0.0), lp_out=lp,
-                                        dev_scale=coef, found_inf=found_inf)
-                    elif self.kind == "adagrad":
-                        fused.adagrad_flat(p32, gr, sv("sum", lo, hi), g["lr"] * g.get("lr_mult", 1.0), g.get("eps", 1e-10),
-                                           g.get("weight_decay", 0.0), lp_out=lp, dev_scale=coef, found_inf=found_inf)
+            if self._overlap_ok(so, lp_flat):
+                # per unit, in the order the next forward reads them, on a side stream; each unit's forward pre-hook
+                # (or gather) waits for its own piece only (_wait_step), the backward for the whole step (_join_step)
+                cur = torch.cuda.current_stream(self.device)
+                side = getattr(self, "_step_stream", None)
+                if side is None:
+                    side = self._step_stream = torch.cuda.Stream(self.device)
+                side.wait_stream(cur)
+                evs = {}
+                with torch.cuda.stream(side):
+                    for uid, lo, hi, sg in self._step_pieces():
+                        update(lo, hi, self._seg_group(sg))
+                        if uid is not None:  # a unit's last piece covers its earlier ones (one stream)
+                            evs[uid] = torch.cuda.Event()
+                            evs[uid].record(side)
+                self._step_ev = evs
+                self.overlapped_steps = getattr(self, "overlapped_steps", 0) + 1
+            else:
+                side = None
+                for sg in s.segments:
+                    g = self._seg_group(sg)
+                    lo0, hi0 = sg.store_off, sg.store_off + sg.numel
+                    bounds = [lo0] + [c for c in cuts if lo0 < c < hi0] + [hi0]
+                    for lo, hi in zip(bounds[:-1], bounds[1:]):
+                        if so is not None and so.hosted(lo):  # host-step tails never come back: step them there
+                            hosted.append((lo, hi, g))
+                            continue
+                        update(lo, hi, g)
             if hosted:
                 so.step_on_host(hosted, coef, lp_flat, found_inf=found_inf, lp_cur=s.lp)
                 if so.async_pending:
@@ -1838,7 +1938,13 @@ class ZeroOptimizer:
         if tmp is not None:
             self._publish_lp(tmp)
         self._post_step_gather(tmp)
-        self.zero_grad()
+        if side is not None:
+            with torch.cuda.stream(side):  # behind the pieces that read the gradients
+                self.zero_grad(_in_step=True)
+                self._step_done = torch.cuda.Event()
+                self._step_done.record(side)
+        else:
+            self.zero_grad(_in_step=True)
         if self.state_offload is not None:
             self.state_offload.offload()  # D2H overlaps the next forward
             if self.state_offload.auto_ratio and self.state_offload.auto_info is None:
@@ -1905,6 +2011,7 @@ class ZeroOptimizer:
                 continue  # aliased / re-gathered on demand by the next forward
             if u.full is None:
                 continue
+            self._wait_step(u)
             w = dist.all_gather_into_tensor(u.full, u.shard_tensor, group=u.ag_group, async_op=True)
             if self.comm_stats is not None:
                 self.comm_stats.issued("all_gather", u.full.numel() * u.full.element_size(), u.world, w)

@@ -289,3 +289,22 @@ def _direct_wgrad_equiv(rank, world, stage, gas):
 @pytest.mark.parametrize("stage,gas", [(1, 2), (2, 1), (2, 2), (3, 1), (3, 2)])
 def test_direct_wgrad_matches_autograd_world2(stage, gas):
     run_distributed(_direct_wgrad_equiv, 2, stage, gas)
+
+
+def test_overlapped_step_piece_plan():
+    """The overlapped step's update order: root units first, then the recorded forward order, then the rest; one
+    piece per (unit, parameter group) overlap; store ranges no unit covers trail. Every element exactly once."""
+    from types import SimpleNamespace as NS
+    from hcache_deepspeed_amd.runtime.zero.optimizer import ZeroOptimizer
+    units = [NS(uid=i, store_off=off, shard=n) for i, (off, n) in enumerate([(0, 10), (10, 20), (30, 5), (40, 8)])]
+    segs = [NS(store_off=0, numel=25, group=0), NS(store_off=25, numel=25, group=1)]  # [35, 40) and [48, 50): no unit
+    opt = NS(units=units, root_units=[units[3]], _fwd_trace=[2, 0, 2], store=NS(segments=segs))
+    pieces = ZeroOptimizer._step_pieces(opt)
+    assert [(p[0], p[1], p[2]) for p in pieces] == [(3, 40, 48), (2, 30, 35), (0, 0, 10), (1, 10, 25), (1, 25, 30),
+                                                   (None, 35, 40), (None, 48, 50)]
+    hit = torch.zeros(50, dtype=torch.int32)
+    for _, lo, hi, sg in pieces:
+        assert sg.store_off <= lo < hi <= sg.store_off + sg.numel
+        hit[lo:hi] += 1
+    assert bool((hit == 1).all())
+    assert ZeroOptimizer._step_pieces(opt) is pieces  # cached for the same forward trace
