@@ -1,5 +1,7 @@
 # headline bench with the full TunableOp table (tuning/, 22 signatures) vs the partial one of the first tuning run
-# (profiles/r6/tunableop_partial_r6c.csv, 9 signatures; +0.5 % over no table), interleaved on one box
+# (profiles/r6/tunableop_partial_r6c.csv, 9 signatures; +0.5 % over no table), interleaved on one box.
+# NOTE: profiles/ is in .gpurunignore, so the cp below failed on the box and the "partial" runs had no table at all
+# (the library heuristic): the recorded A/B is full table vs none.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
