@@ -184,6 +184,13 @@ def _b2_useful(N, K):
     return _B2 and 0.2 < frac < 0.8
 
 
+def _rows_bucket(t):
+    """Token-row count as the layout tuners key it: rounded up to 2048, so GEMMs whose row count moves a little
+    from step to step (MoE experts over their occupied capacity slots) reuse one timing instead of re-timing every
+    new size inside the step."""
+    return -(-int(t) // 2048) * 2048
+
+
 _NT_BY_N = {}  # dy columns -> True if the timed choice for that gradient width was an "nt" form
 
 
@@ -209,7 +216,7 @@ def wgrad(dy2, x2, out, accumulate=False, dyt=None, xt=None):
                 and dy2.stride(1) == 1 and (x2 is None or x2.stride(1) == 1)):
             layout = "direct" if x2 is not None else "nt"
         else:
-            key = (tuple(dy2.shape), K, out.dtype, bool(accumulate), x2 is None, dyt is not None)
+            key = (_rows_bucket(T), N, K, out.dtype, bool(accumulate), x2 is None, dyt is not None)
             layout = _WGRAD_CHOICE.get(key)
             if layout is None:
                 b2 = ("_b2", ) if _b2_useful(N, K) else ()
@@ -265,7 +272,7 @@ def dgrad(dy2, w, out=None, cache=None):
                 and w.stride(1) == 1):
             layout = "direct"
         else:
-            key = (tuple(dy2.shape), tuple(w.shape))
+            key = (_rows_bucket(dy2.shape[0]), dy2.shape[1], tuple(w.shape))
             layout = _DGRAD_CHOICE.get(key)
             if layout is None:
                 times = {}

@@ -15,6 +15,7 @@ all-gathers its experts' slots from the TP peers, runs column/row-sharded expert
 the token drop into ONE reduce-scatter before the return all-to-all.
 """
 import copy
+import os
 
 import torch
 import torch.nn as nn
@@ -24,6 +25,9 @@ from .. import comm as dist
 from ..ops.activations import glu
 from ..ops.moe import moe_combine, moe_dispatch, topk_route
 from ..utils import groups
+
+# MOELayer: run the grouped experts over the occupied capacity slots only (HDS_MOE_EXACT_ROWS=0: every slot)
+_EXACT_ROWS = os.environ.get("HDS_MOE_EXACT_ROWS", "1") != "0"
 
 
 class _AllToAll(torch.autograd.Function):
@@ -180,17 +184,28 @@ class _ExpertLinear(torch.autograd.Function):
     of one output (and, in backward, of one dX and one dW). Batched ``torch.bmm`` with the transposed stacked weight
     hits a hipBLASLt failure on MI355X at Mixtral-8x7B shapes (HIPBLAS_STATUS_INTERNAL_ERROR for the strided batched
     TN problem m 4096 n 1280 k 14336, then an illegal access in the rocBLAS fallback); the 2-D forms are the
-    projection GEMMs the dense model runs every step (NT forward, layout-timed dgrad / wgrad from ops/gemm.py)."""
+    projection GEMMs the dense model runs every step (NT forward, layout-timed dgrad / wgrad from ops/gemm.py).
+
+    ``rows`` (host ints, one per expert): only the first rows[e] capacity slots of expert e hold tokens (dispatch
+    fills each expert's slots densely from 0 and zeroes the rest), so the GEMMs run over those rows only and the
+    remaining rows of every output are zeroed -- exactly what the full GEMMs would give for the zero slots. With
+    capacity factor 1.25 a quarter of the expert GEMM work was on empty slots."""
 
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, rows=None):
         E, C, K = x.shape
         y = x.new_empty(E, C, w.shape[1])
+        rows = tuple(C for _ in range(E)) if rows is None else tuple(rows)
         for e in range(E):
-            torch.mm(x[e], w[e].t(), out=y[e])
+            m = rows[e]
+            if m > 0:
+                torch.mm(x[e, :m], w[e].t(), out=y[e, :m])
+            if m < C:
+                y[e, m:].zero_()
         # like runtime/zero/linear.py: keep the Parameter object, not its (ZeRO-3 gathered) data, for backward
         ctx.save_for_backward(x)
         ctx.weight = w
+        ctx.rows = rows
         return y
 
     @staticmethod
@@ -198,28 +213,37 @@ class _ExpertLinear(torch.autograd.Function):
         from ..ops.gemm import dgrad, wgrad
         from ..runtime.zero.linear import write_weight_grad
         (x, ) = ctx.saved_tensors
-        w = ctx.weight
+        w, rows = ctx.weight, ctx.rows
+        C = x.shape[1]
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             for e in range(x.shape[0]):
-                dgrad(dy[e], w[e], out=dx[e])
+                m = rows[e]
+                if m > 0:
+                    dgrad(dy[e, :m], w[e], out=dx[e, :m])
+                if m < C:
+                    dx[e, m:].zero_()
         if ctx.needs_input_grad[1]:
 
             def gemm(out, accumulate):  # straight into the ZeRO gradient buffer (no AccumulateGrad add)
                 for e in range(x.shape[0]):
-                    wgrad(dy[e], x[e], out[e], accumulate)
+                    m = rows[e]
+                    if m > 0:
+                        wgrad(dy[e, :m], x[e, :m], out[e], accumulate)
+                    elif not accumulate:
+                        out[e].zero_()  # no token reached this expert: its gradient is zero
 
             if not write_weight_grad(w, gemm):
                 dw = torch.empty_like(w)
                 gemm(dw, False)
-        return dx, dw
+        return dx, dw, None
 
 
-def expert_linear(x, w):
+def expert_linear(x, w, rows=None):
     if torch.is_grad_enabled() or x.is_cuda:  # the same Function on CPU, so gloo tests exercise the GPU path's logic
-        return _ExpertLinear.apply(x.contiguous(), w)
+        return _ExpertLinear.apply(x.contiguous(), w, None if rows is None else tuple(rows))
     return torch.bmm(x, w.transpose(1, 2))
 
 
@@ -261,9 +285,9 @@ class GroupedSwiGLUExperts(nn.Module):
         self.w13.copy_(torch.cat([w13[:, lo:lo + i], w13[:, i_full + lo:i_full + lo + i]], 1))
         self.w2.copy_(w2[:, :, lo:lo + i])
 
-    def forward(self, x):
-        h = expert_linear(x, self.w13)
-        return expert_linear(glu(h, self.act), self.w2)
+    def forward(self, x, rows=None):
+        h = expert_linear(x, self.w13, rows)
+        return expert_linear(glu(h, self.act), self.w2, rows)
 
 
 class MOELayer(nn.Module):
@@ -311,8 +335,16 @@ class MOELayer(nn.Module):
         if sharded:  # TP-sharded experts see every slot of their experts (gathered over the TP ranks)
             local = gather_tokens(local, 2, partial_grad=isinstance(self.experts, GroupedSwiGLUExperts))
         Cx = local.shape[2]
-        y = self.experts(local.reshape(self.num_local_experts, self.ep_size * Cx, H)).view(
-            self.num_local_experts, self.ep_size, Cx, H)
+        xe = local.reshape(self.num_local_experts, self.ep_size * Cx, H)
+        if self.ep_size == 1 and not sharded and isinstance(self.experts, GroupedSwiGLUExperts) and _EXACT_ROWS:
+            # the experts' GEMMs skip the empty capacity slots: each expert's tokens sit in its first
+            # min(count, C) slots (one host read of the E counts per layer; rounded up to 128 rows so the GEMM
+            # shapes -- and the per-shape layout timings of ops/gemm.py -- stay few)
+            rows = [min(C, -(-min(int(n), C) // 128) * 128) for n in counts.tolist()]
+            y = self.experts(xe, rows=rows)
+        else:
+            y = self.experts(xe)
+        y = y.view(self.num_local_experts, self.ep_size, Cx, H)
         if sharded:
             if isinstance(self.experts, GroupedSwiGLUExperts):
                 y = _ReduceScatterTokens.apply(y, 2)  # partial sums -> this rank's summed slots

@@ -298,3 +298,34 @@ def GroupedSwiGLUExperts_shard(full, e0, tp_rank, tp=2):
 @pytest.mark.parametrize("cf", [16.0, 0.6])  # no drops / drops with a capacity padded to the TP size
 def test_expert_tensor_parallel_matches_unsharded(cf):
     run_distributed(_expert_tp, 4, cf)
+
+
+def test_moe_experts_skip_empty_capacity_slots(monkeypatch):
+    """The grouped experts run their GEMMs over each expert's occupied capacity slots only (rounded up to 128
+    rows) and zero the rest: outputs and gradients match running every slot."""
+    import hcache_deepspeed_amd.parallel.moe as M
+    torch.manual_seed(3)
+    H, I, E, T = 16, 24, 4, 600
+    res = {}
+    real = M._ExpertLinear.forward
+    calls = []
+    monkeypatch.setattr(M._ExpertLinear, "forward",
+                        staticmethod(lambda ctx, a, w, rows=None: calls.append(rows) or real(ctx, a, w, rows)))
+    for exact in (True, False):
+        monkeypatch.setattr(M, "_EXACT_ROWS", exact)
+        calls.clear()
+        torch.manual_seed(3)
+        moe = M.MoE(H, None, E, 1, k=2, capacity_factor=2.0, eval_capacity_factor=2.0, expert_intermediate_size=I)
+        x = torch.randn(T, H, requires_grad=True)
+        out, _, counts = moe(x)
+        (out * torch.linspace(-1, 1, out.numel()).view_as(out)).sum().backward()
+        ex = moe.deepspeed_moe.experts
+        res[exact] = (out.detach(), x.grad, ex.w13.grad, ex.w2.grad)
+        if exact:
+            C = 600  # ceil(T * k / E * capacity_factor)
+            assert calls[0] is not None and all(r % 128 == 0 or r == C for r in calls[0])
+            assert max(calls[0]) < C  # the path skipped empty slots
+        else:
+            assert calls[0] is None
+    for a, b in zip(res[True], res[False]):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r6mx
+O=gpurun_out/r6mx${TAG:-}
 mkdir -p $O
 MB=${MB:-4}
 timeout -k 10 500 python -u bench.py --model mixtral-8x7b --layers 8 --micro-batch $MB --steps 4 --warmup 2 > $O/mixtral_l8_mb$MB.json 2> $O/mixtral_l8_mb$MB.err || { echo bench failed; tail -20 $O/mixtral_l8_mb$MB.err; exit 1; }
