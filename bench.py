@@ -82,6 +82,9 @@ def main():
                          "ZeRO-Offload++); the rest keeps the on-device fused Adam")
     ap.add_argument("--nvme-path", default="/tmp/hds_nvme", help="swap folder of the NVMe tier (--offload nvme)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (MoE models)")
+    ap.add_argument("--moe-dropless", action="store_true",
+                    help="MoE models: no token dropping (capacity = the largest expert load of the step; the expert "
+                         "GEMMs run over the occupied slots only)")
     ap.add_argument("--sp", type=int, default=1,
                     help="Ulysses sequence-parallel size: each rank holds seq/sp tokens of every sequence (ZeRO shards "
                          "over the dp x sp ranks; tokens/s counts each sequence once)")
@@ -153,6 +156,8 @@ def main():
     elif args.model in ("mixtral-8x7b", "tiny-moe"):
         if args.layers:
             overrides["num_hidden_layers"] = args.layers
+        if args.moe_dropless:
+            overrides["drop_tokens"] = False
         cfg_model = {"mixtral-8x7b": mixtral.mixtral_8x7b, "tiny-moe": mixtral.tiny_moe}[args.model](
             ep_size=args.ep, **overrides)
         build = mixtral.MixtralForCausalLM
@@ -422,7 +427,8 @@ def main():
                        **({"sequence_parallel_size": sp} if sp > 1 else {}),
                        **({"fpdt": engine.fpdt_config} if getattr(engine, "fpdt_config", None) else {}),
                        "stage3_max_reuse_distance": ds_config["zero_optimization"].get("stage3_max_reuse_distance"),
-                       "activation_checkpointing": bool(args.ckpt), "deepcompile": bool(args.deepcompile)},
+                       "activation_checkpointing": bool(args.ckpt), "deepcompile": bool(args.deepcompile),
+                       **({"moe_dropless": True} if args.moe_dropless else {})},
             "extra": {"mfu_bf16_dense_2.5PF": round(mfu, 4), "tflops_per_gpu": round(flops / dt / world / 1e12, 1),
                       "mfu_causal": round(mfu_c, 4), "tflops_causal_per_gpu": round(flops_c / dt / world / 1e12, 1),
                       "host_threads": getattr(engine, "host_threads", None),
