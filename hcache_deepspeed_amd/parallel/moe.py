@@ -186,26 +186,26 @@ class _ExpertLinear(torch.autograd.Function):
     TN problem m 4096 n 1280 k 14336, then an illegal access in the rocBLAS fallback); the 2-D forms are the
     projection GEMMs the dense model runs every step (NT forward, layout-timed dgrad / wgrad from ops/gemm.py).
 
-    ``rows`` (host ints, one per expert): only the first rows[e] capacity slots of expert e hold tokens (dispatch
-    fills each expert's slots densely from 0 and zeroes the rest), so the GEMMs run over those rows only and the
-    remaining rows of every output are zeroed -- exactly what the full GEMMs would give for the zero slots. With
-    capacity factor 1.25 a quarter of the expert GEMM work was on empty slots."""
+    ``segs`` (host ints): per expert, the (start, rows) row ranges that hold tokens -- dispatch fills each expert's
+    capacity slots densely from 0 and zeroes the rest, so an expert's tokens are one prefix per source rank (one
+    segment at EP 1, one per EP rank behind the all-to-all). The GEMMs run over those rows only and every other row
+    of each output is zeroed -- exactly what the full GEMMs give for zero slots. With capacity factor 1.25 a fifth of
+    the expert GEMM rows were empty."""
 
     @staticmethod
-    def forward(ctx, x, w, rows=None):
+    def forward(ctx, x, w, segs=None):
         E, C, K = x.shape
         y = x.new_empty(E, C, w.shape[1])
-        rows = tuple(C for _ in range(E)) if rows is None else tuple(rows)
+        segs = tuple(((0, C), ) for _ in range(E)) if segs is None else segs
         for e in range(E):
-            m = rows[e]
-            if m > 0:
-                torch.mm(x[e, :m], w[e].t(), out=y[e, :m])
-            if m < C:
-                y[e, m:].zero_()
+            for s0, m in segs[e]:
+                torch.mm(x[e, s0:s0 + m], w[e].t(), out=y[e, s0:s0 + m])
+            for a, b in _gaps(segs[e], C):
+                y[e, a:b].zero_()
         # like runtime/zero/linear.py: keep the Parameter object, not its (ZeRO-3 gathered) data, for backward
         ctx.save_for_backward(x)
         ctx.weight = w
-        ctx.rows = rows
+        ctx.segs = segs
         return y
 
     @staticmethod
@@ -213,26 +213,26 @@ class _ExpertLinear(torch.autograd.Function):
         from ..ops.gemm import dgrad, wgrad
         from ..runtime.zero.linear import write_weight_grad
         (x, ) = ctx.saved_tensors
-        w, rows = ctx.weight, ctx.rows
+        w, segs = ctx.weight, ctx.segs
         C = x.shape[1]
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             for e in range(x.shape[0]):
-                m = rows[e]
-                if m > 0:
-                    dgrad(dy[e, :m], w[e], out=dx[e, :m])
-                if m < C:
-                    dx[e, m:].zero_()
+                for s0, m in segs[e]:
+                    dgrad(dy[e, s0:s0 + m], w[e], out=dx[e, s0:s0 + m])
+                for a, b in _gaps(segs[e], C):
+                    dx[e, a:b].zero_()
         if ctx.needs_input_grad[1]:
 
             def gemm(out, accumulate):  # straight into the ZeRO gradient buffer (no AccumulateGrad add)
                 for e in range(x.shape[0]):
-                    m = rows[e]
-                    if m > 0:
-                        wgrad(dy[e, :m], x[e, :m], out[e], accumulate)
-                    elif not accumulate:
+                    acc = accumulate
+                    for s0, m in segs[e]:
+                        wgrad(dy[e, s0:s0 + m], x[e, s0:s0 + m], out[e], acc)
+                        acc = True
+                    if not acc:
                         out[e].zero_()  # no token reached this expert: its gradient is zero
 
             if not write_weight_grad(w, gemm):
@@ -241,9 +241,37 @@ class _ExpertLinear(torch.autograd.Function):
         return dx, dw, None
 
 
-def expert_linear(x, w, rows=None):
+def _gaps(segs, C):
+    """[a, b) row ranges of [0, C) outside the sorted, disjoint segments."""
+    out, pos = [], 0
+    for s0, m in segs:
+        if s0 > pos:
+            out.append((pos, s0))
+        pos = max(pos, s0 + m)
+    if pos < C:
+        out.append((pos, C))
+    return out
+
+
+def occupied_segments(counts, C, blocks=1, granule=128):
+    """Per local expert, the (start, rows) ranges holding tokens. ``counts``: [blocks][E_local] token counts (one row
+    per source rank behind the EP all-to-all); block r of an expert occupies rows [r*C, r*C + min(count, C)), rounded
+    up to ``granule`` rows (few distinct GEMM shapes) and capped at the block."""
+    n_local = len(counts[0])
+    segs = []
+    for j in range(n_local):
+        s = []
+        for r in range(blocks):
+            m = min(C, -(-min(int(counts[r][j]), C) // granule) * granule)
+            if m > 0:
+                s.append((r * C, m))
+        segs.append(tuple(s))
+    return tuple(segs)
+
+
+def expert_linear(x, w, segs=None):
     if torch.is_grad_enabled() or x.is_cuda:  # the same Function on CPU, so gloo tests exercise the GPU path's logic
-        return _ExpertLinear.apply(x.contiguous(), w, None if rows is None else tuple(rows))
+        return _ExpertLinear.apply(x.contiguous(), w, segs)
     return torch.bmm(x, w.transpose(1, 2))
 
 
@@ -285,9 +313,9 @@ class GroupedSwiGLUExperts(nn.Module):
         self.w13.copy_(torch.cat([w13[:, lo:lo + i], w13[:, i_full + lo:i_full + lo + i]], 1))
         self.w2.copy_(w2[:, :, lo:lo + i])
 
-    def forward(self, x, rows=None):
-        h = expert_linear(x, self.w13, rows)
-        return expert_linear(glu(h, self.act), self.w2, rows)
+    def forward(self, x, segs=None):
+        h = expert_linear(x, self.w13, segs)
+        return expert_linear(glu(h, self.act), self.w2, segs)
 
 
 class MOELayer(nn.Module):
@@ -336,12 +364,20 @@ class MOELayer(nn.Module):
             local = gather_tokens(local, 2, partial_grad=isinstance(self.experts, GroupedSwiGLUExperts))
         Cx = local.shape[2]
         xe = local.reshape(self.num_local_experts, self.ep_size * Cx, H)
-        if self.ep_size == 1 and not sharded and isinstance(self.experts, GroupedSwiGLUExperts) and _EXACT_ROWS:
-            # the experts' GEMMs skip the empty capacity slots: each expert's tokens sit in its first
-            # min(count, C) slots (one host read of the E counts per layer; rounded up to 128 rows so the GEMM
-            # shapes -- and the per-shape layout timings of ops/gemm.py -- stay few)
-            rows = [min(C, -(-min(int(n), C) // 128) * 128) for n in counts.tolist()]
-            y = self.experts(xe, rows=rows)
+        if not sharded and isinstance(self.experts, GroupedSwiGLUExperts) and _EXACT_ROWS:
+            # the experts' GEMMs skip the empty capacity slots: each expert's tokens from one source rank sit in the
+            # first min(count, C) slots of that rank's block (one host read of the counts per layer -- behind the EP
+            # all-to-all, of every source rank's counts, all-gathered; rounded up to 128 rows so the GEMM shapes and
+            # the per-shape layout timings of ops/gemm.py stay few)
+            if self.ep_size > 1:
+                allc = torch.empty(self.ep_size * E, dtype=counts.dtype, device=counts.device)
+                dist.all_gather_into_tensor(allc, counts.contiguous().view(-1), group=self.ep_group)
+                allc = allc.view(self.ep_size, E)
+                r0 = dist.get_rank(self.ep_group) * self.num_local_experts
+                cnt = allc[:, r0:r0 + self.num_local_experts].tolist()
+            else:
+                cnt = [counts.tolist()]
+            y = self.experts(xe, segs=occupied_segments(cnt, Cx, self.ep_size))
         else:
             y = self.experts(xe)
         y = y.view(self.num_local_experts, self.ep_size, Cx, H)

@@ -323,9 +323,42 @@ def test_moe_experts_skip_empty_capacity_slots(monkeypatch):
         res[exact] = (out.detach(), x.grad, ex.w13.grad, ex.w2.grad)
         if exact:
             C = 600  # ceil(T * k / E * capacity_factor)
-            assert calls[0] is not None and all(r % 128 == 0 or r == C for r in calls[0])
-            assert max(calls[0]) < C  # the path skipped empty slots
+            ms = [m for seg in calls[0] for _, m in seg]
+            assert calls[0] is not None and all(m % 128 == 0 or m == C for m in ms)
+            assert max(ms) < C  # the path skipped empty slots
         else:
             assert calls[0] is None
     for a, b in zip(res[True], res[False]):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+
+
+def _ep_segments(rank, world):
+    import hcache_deepspeed_amd.parallel.moe as M
+    H, I, E, T = 16, 24, 4, 600
+    res = {}
+    seen = []
+    real = M.occupied_segments
+    M.occupied_segments = lambda *a, **k: seen.append(real(*a, **k)) or seen[-1]
+    try:
+        for exact in (True, False):
+            M._EXACT_ROWS = exact
+            torch.manual_seed(3)
+            moe = M.MoE(H, None, E, ep_size=2, k=2, capacity_factor=2.0, eval_capacity_factor=2.0,
+                        expert_intermediate_size=I)
+            x = torch.randn(T, H, generator=torch.Generator().manual_seed(50 + rank), requires_grad=True)
+            out, _, _ = moe(x)
+            (out * torch.linspace(-1, 1, out.numel()).view_as(out)).sum().backward()
+            ex = moe.deepspeed_moe.experts
+            res[exact] = (out.detach(), x.grad, ex.w13.grad, ex.w2.grad)
+    finally:
+        M.occupied_segments = real
+        M._EXACT_ROWS = True
+    # one segment per source rank for each of the 2 local experts, each a rounded prefix of its 600-row block
+    assert len(seen) == 1 and all(len(s) == 2 for s in seen[0])
+    assert all(s0 % 600 == 0 and m % 128 == 0 and m < 600 for s in seen[0] for s0, m in s)
+    for a, b in zip(res[True], res[False]):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+
+
+def test_expert_parallel_skips_empty_slots_per_source_rank():
+    run_distributed(_ep_segments, 2)
