@@ -86,7 +86,196 @@ __global__ __launch_bounds__(256) void gemv_bf16_kernel(const bf16* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Fused decode GEMV: the pre-norm and the gated activation of a decoder layer folded into its projection GEMVs, so a
+// decode step launches neither the RMSNorm nor the GLU kernel (each ~4-5 us per call in a decode graph, i.e. about a
+// tenth of a Llama-3-8B B = 1 step, for kernels that move a few KB).
+//
+// NORM: the input rows are x = bf16(r * rstd * gamma), r = bf16(h + res) (or h without a residual) -- exactly the
+// arithmetic of norm.hip's RMSNorm forward. The workgroup's 256 threads first reduce sum(r^2) of its M rows once into
+// LDS; its 4 waves then stream their weight rows as gemv_bf16_kernel does, building each x chunk from r, rstd and gamma
+// (all L2-resident, K * 2 bytes) on the fly. Workgroup 0 also writes r (the new residual stream) and, when asked, x
+// (the normed rows: HCache's hidden-state latents).
+// GLU: the weight is [gate; up] ([2I, K]) and the output y[M, I] = bf16(act(bf16(x.g_j)) * bf16(x.u_j)) (silu): a wave
+// owns R output columns and streams their gate AND up rows, so the [M, 2I] intermediate never exists.
+__device__ __forceinline__ float silu_f(float v) { return v * __builtin_amdgcn_rcpf(1.f + __expf(-v)); }
+
+template <bool NORM>
+__device__ __forceinline__ bf16x8 load_x(const bf16* __restrict__ h, const bf16* __restrict__ res,
+                                         const bf16* __restrict__ gamma, float rstd, int64_t off, int k) {
+  bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + off + k);
+  if constexpr (!NORM) {
+    return hv;
+  } else {
+    const bf16x8 g = *reinterpret_cast<const bf16x8*>(gamma + k);
+    bf16x8 o;
+    if (res != nullptr) {
+      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + off + k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[j] = (bf16)((float)hv[j] + (float)rv[j]);  // round like the unfused add
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)hv[j] * rstd * (float)g[j]);
+    return o;
+  }
+}
+
+template <int MAXM, int R, bool NORM, bool GLU>
+__global__ __launch_bounds__(256) void gemv_fused_kernel(const bf16* __restrict__ h, const bf16* __restrict__ res,
+                                                         const bf16* __restrict__ gamma, float eps,
+                                                         const bf16* __restrict__ w, bf16* __restrict__ y,
+                                                         bf16* __restrict__ r_out, bf16* __restrict__ x_out, int M,
+                                                         int N, int K, int64_t ldh, int64_t ldy) {
+  __shared__ float s_part[4][MAXM];
+  __shared__ float s_rstd[MAXM];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  float rstd[MAXM];
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m) rstd[m] = 1.f;
+  if constexpr (NORM) {
+    float ss[MAXM];
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) ss[m] = 0.f;
+    for (int c = threadIdx.x * 8; c < K; c += 2048) {
+#pragma unroll
+      for (int m = 0; m < MAXM; ++m) {
+        if (m < M) {
+          bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + m * ldh + c);
+          if (res != nullptr) {
+            const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + m * ldh + c);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hv[j] = (bf16)((float)hv[j] + (float)rv[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss[m] += (float)hv[j] * (float)hv[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) {
+      const float t = wave_sum(ss[m]);
+      if (lane == 0) s_part[wid][m] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < MAXM)
+      s_rstd[threadIdx.x] = rsqrtf((s_part[0][threadIdx.x] + s_part[1][threadIdx.x] + s_part[2][threadIdx.x] +
+                                    s_part[3][threadIdx.x]) / (float)K + eps);
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) rstd[m] = s_rstd[m];
+    if (blockIdx.x == 0 && (r_out != nullptr || x_out != nullptr)) {
+      for (int c = threadIdx.x * 8; c < K; c += 2048) {
+#pragma unroll
+        for (int m = 0; m < MAXM; ++m) {
+          if (m < M) {
+            if (r_out != nullptr && res != nullptr) {
+              bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + m * ldh + c);
+              const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + m * ldh + c);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) hv[j] = (bf16)((float)hv[j] + (float)rv[j]);
+              *reinterpret_cast<bf16x8*>(r_out + m * ldh + c) = hv;
+            }
+            if (x_out != nullptr)
+              *reinterpret_cast<bf16x8*>(x_out + m * ldh + c) = load_x<true>(h, res, gamma, rstd[m], m * ldh, c);
+          }
+        }
+      }
+    }
+  }
+  const int n0 = (blockIdx.x * 4 + wid) * R;  // output columns [n0, n0 + R)
+  if (n0 >= N) return;
+  constexpr int RR = GLU ? 2 * R : R;  // weight rows streamed per wave: the gate rows, then the up rows
+  float acc[RR][MAXM];
+#pragma unroll
+  for (int r = 0; r < RR; ++r)
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) acc[r][m] = 0.f;
+  const bf16* wr[RR];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = min(n0 + r, N - 1);  // tail columns re-read column N-1 (unused)
+    wr[r] = w + (int64_t)n * K;
+    if constexpr (GLU) wr[R + r] = w + (int64_t)(N + n) * K;
+  }
+  int k0 = 8 * lane;
+  for (; k0 + 512 < K; k0 += 1024) {
+    bf16x8 wa[RR], wb[RR];
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+      wa[r] = *reinterpret_cast<const bf16x8*>(wr[r] + k0);
+      wb[r] = *reinterpret_cast<const bf16x8*>(wr[r] + k0 + 512);
+    }
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) {
+      if (m < M) {
+        const bf16x8 xa = load_x<NORM>(h, res, gamma, rstd[m], m * ldh, k0);
+        const bf16x8 xb = load_x<NORM>(h, res, gamma, rstd[m], m * ldh, k0 + 512);
+#pragma unroll
+        for (int r = 0; r < RR; ++r) acc[r][m] = dot8(xb, wb[r], dot8(xa, wa[r], acc[r][m]));
+      }
+    }
+  }
+  if (k0 < K) {
+    bf16x8 wa[RR];
+#pragma unroll
+    for (int r = 0; r < RR; ++r) wa[r] = *reinterpret_cast<const bf16x8*>(wr[r] + k0);
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) {
+      if (m < M) {
+        const bf16x8 xa = load_x<NORM>(h, res, gamma, rstd[m], m * ldh, k0);
+#pragma unroll
+        for (int r = 0; r < RR; ++r) acc[r][m] = dot8(xa, wa[r], acc[r][m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) {
+      if (m < M && n0 + r < N) {
+        const float v = wave_sum(acc[r][m]);
+        if constexpr (GLU) {
+          const float u = wave_sum(acc[R + r][m]);
+          if (lane == 0) y[m * ldy + n0 + r] = (bf16)(silu_f((float)(bf16)v) * (float)(bf16)u);
+        } else {
+          if (lane == 0) y[m * ldy + n0 + r] = (bf16)v;
+        }
+      }
+    }
+}
+
 }  // namespace
+
+// Fused decode GEMV (see gemv_fused_kernel): y[M, N] = norm(h (+ res)) . W^T, or with glu != 0, y[M, N] =
+// silu(x . Wg^T) * (x . Wu^T) for W = [Wg; Wu] of 2N rows (x normed when gamma is given, else h itself). r_out /
+// x_out (workgroup 0, with gamma): the new residual rows and the normed rows. ldh: row stride of h / res / r_out /
+// x_out (elements); ldy: row stride of y. Shapes: M <= 8, K % 8 == 0, 16-B aligned operands (checked by the caller).
+HDS_EXPORT int hds_gemv_fused_bf16(const void* h, const void* res, const void* gamma, float eps, const void* w,
+                                   void* y, void* r_out, void* x_out, int glu, int M, int N, int K, int64_t ldh,
+                                   int64_t ldy, hipStream_t st) {
+  if (M < 1 || M > 8 || N < 1 || K < 8 || K % 8 || ldh % 8) return hipErrorInvalidValue;
+  if (gamma == nullptr && (r_out != nullptr || x_out != nullptr || res != nullptr)) return hipErrorInvalidValue;
+  const int R = N >= 8192 ? (glu ? 2 : 4) : (N >= 4096 ? 2 : 1);
+#define HDS_GF(MM, RR, NN, GG)                                                                                   \
+  hipLaunchKernelGGL((gemv_fused_kernel<MM, RR, NN, GG>), dim3((N + 4 * RR - 1) / (4 * RR)), dim3(256), 0, st,  \
+                     (const bf16*)h, (const bf16*)res, (const bf16*)gamma, eps, (const bf16*)w, (bf16*)y,      \
+                     (bf16*)r_out, (bf16*)x_out, M, N, K, ldh, ldy)
+#define HDS_GFM(RR, NN, GG)                                                                                    \
+  if (M == 1) HDS_GF(1, RR, NN, GG); else if (M <= 2) HDS_GF(2, RR, NN, GG);                                   \
+  else if (M <= 4) HDS_GF(4, RR, NN, GG); else HDS_GF(8, RR, NN, GG);
+#define HDS_GFR(NN, GG)                                                                                        \
+  if (R == 4) { HDS_GFM(4, NN, GG) } else if (R == 2) { HDS_GFM(2, NN, GG) } else { HDS_GFM(1, NN, GG) }
+  if (gamma != nullptr) {
+    if (glu) { HDS_GFR(true, true) } else { HDS_GFR(true, false) }
+  } else {
+    if (glu) { HDS_GFR(false, true) } else { return hipErrorInvalidValue; }  // plain GEMV: hds_gemv_bf16
+  }
+#undef HDS_GFR
+#undef HDS_GFM
+#undef HDS_GF
+  return hipGetLastError();
+}
 
 // Shapes the kernel takes: M <= 8 rows, K a multiple of 8 (16-B rows), 16-B aligned operands (checked by the caller).
 HDS_EXPORT int hds_gemv_bf16_supported(int M, int N, int K) { return M >= 1 && M <= 8 && N >= 1 && K >= 8 && K % 8 == 0; }

@@ -30,6 +30,7 @@ HCache, as implemented here (with the defects fixed):
 * every family above implements the contract (the reference broke ``put`` for all non-Llama models).
 """
 import math
+import os as _os
 import types
 
 import torch
@@ -282,9 +283,9 @@ class RaggedTransformer:
     def _embed(self, batch):
         return self.embed_mod(batch, self.embed, self.pos_embed)
 
-    def _attn(self, i, L, x, batch, T, capture, lat, events, sink=None):
+    def _attn(self, i, L, x, batch, T, capture, lat, events, sink=None, qkv=None):
         nq, nkv, D = self.n_q, self.n_kv, self.d
-        qkv = self.qkv_lin(x, L["qkv.w"], L["qkv.b"]).view(T, nq + 2 * nkv, D)
+        qkv = (self.qkv_lin(x, L["qkv.w"], L["qkv.b"]) if qkv is None else qkv).view(T, nq + 2 * nkv, D)
         if capture and self.latent_mode == "kv":
             if sink is not None:  # stored in stream order before RoPE rotates K in place: no clone
                 sink(i, qkv[:, nq:].reshape(T, -1))
@@ -292,6 +293,27 @@ class RaggedTransformer:
                 self._d2h(qkv[:, nq:].reshape(T, -1).clone(), lat[i], events)  # pre-RoPE K|V
         o = self.attn_mod(qkv, self.kv_cache.get_cache(i), batch, self.cos, self.sin)
         return self.o_lin(o, L["o.w"], L["o.b"])
+
+    def _fused_decode_ok(self, T):
+        """Single-token decode steps of a plain pre-RMSNorm, SwiGLU-style dense model on the bf16 BLAS linears: the pre-norms
+        and the gated activation run inside the projection GEMVs (ops/gemv.fused_gemv), so a layer launches neither
+        the RMSNorm nor the GLU kernel (``HDS_V2_FUSED_DECODE=0``: the separate kernels)."""
+        ok = getattr(self, "_fused_static", None)
+        if ok is None:
+            from .modules.implementations import BlasFPLinear, DSPreRMSNorm
+            ok = (bool(self.layers) and _os.environ.get("HDS_V2_FUSED_DECODE", "1") == "1"
+                  and self.device.type == "cuda"
+                  and self.dtype == torch.bfloat16 and self.tp == 1 and self.spec.moe is None
+                  and self.spec.parallel not in ("shared_ln", "two_ln") and self.spec.gated
+                  and isinstance(self.norm_mod, DSPreRMSNorm) and self._act_name() == "silu"
+                  and all(isinstance(m, BlasFPLinear) for m in (self.qkv_lin, self.up_lin))
+                  and all(L[k] is None for L in self.layers for k in ("ln1.b", "ln2.b", "qkv.b", "up.b"))
+                  and all(L[k] is not None and L[k].dtype == torch.bfloat16 and torch.is_tensor(L[k])
+                          for L in self.layers for k in ("ln1.w", "ln2.w", "qkv.w", "up.w")))
+            self._fused_static = ok
+        # one token row only: at B = 4 the per-row normalisation inside the (already VALU-bound) GEMV made the step
+        # slower than the separate RMSNorm kernel (732 vs 773 tok/s); at B = 1: 247 vs 234 (profiles/r6/fused_decode/)
+        return ok and T == 1
 
     # ------------------------------------------------------------------------------------------
     def decode_graph_eligible(self, batch, capture_latents):
@@ -362,7 +384,24 @@ class RaggedTransformer:
         if capture_latents and sink is None:
             lat = self._latent_buffer(spec.num_hidden_layers, T)
         emit = sink if sink is not None else (lambda i, t: self._d2h(t, lat[i], events))
-        for i, L in enumerate(self.layers):
+        if self._fused_decode_ok(T):
+            from ...ops.gemv import fused_gemv
+            eps = spec.norm_eps
+            want_x = capture_latents and self.latent_mode in ("hidden", "hidden_fp8", "hidden_int8")
+            for i, L in enumerate(self.layers):
+                # pre-norm + qkv in one GEMV; the new residual stream (and the normed rows for hidden latents) too
+                qkv, residual, x = fused_gemv(h, L["qkv.w"], residual, L["ln1.w"], eps, want_x=want_x)
+                if capture_latents and self.latent_mode == "hidden":
+                    emit(i, x)
+                elif capture_latents and self.latent_mode == "hidden_fp8":
+                    emit(i, self._pack_fp8(x))
+                elif capture_latents and self.latent_mode == "hidden_int8":
+                    emit(i, self._pack_int8(x))
+                a = self._attn(i, L, None, batch, T, capture_latents, lat, events, sink, qkv=qkv)
+                # post-attention norm + gate|up + SwiGLU in one GEMV, then the down projection
+                g, residual, _ = fused_gemv(a, L["up.w"], residual, L["ln2.w"], eps, glu=True)
+                h = self.down_lin(g, L["down.w"], L["down.b"])
+        for i, L in (enumerate(self.layers) if not self._fused_decode_ok(T) else ()):
             if residual is None:
                 x = self._norm(h, L["ln1.w"], L["ln1.b"])
                 residual = h

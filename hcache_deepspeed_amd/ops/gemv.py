@@ -51,3 +51,59 @@ def linear(x, w, b=None):
         if gemv_ok(x2, w, b):
             return gemv(x2, w, b).view(*x.shape[:-1], w.shape[0])
     return F.linear(x, w, b)
+
+
+def fused_ok(h2, w, gamma=None, glu=False):
+    """Can ``fused_gemv`` take these decode rows on the HIP kernel (bf16, <= 8 rows, 16-B aligned rows)?"""
+    if not (native.use_native(h2) and h2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2):
+        return False
+    M, K = h2.shape
+    if M > 8 or w.shape[1] != K or K % 8 or not w.is_contiguous() or h2.stride(1) != 1 or h2.stride(0) != K:
+        return False
+    if glu and w.shape[0] % 2:
+        return False
+    if gamma is not None and (gamma.dtype != torch.bfloat16 or not gamma.is_contiguous() or gamma.numel() != K):
+        return False
+    return h2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and w.numel() <= max_numel(M)
+
+
+def _unfused(h2, w, res, gamma, eps, glu):
+    from .activations import glu as _glu
+    from .norm import rms_norm
+    r, x = h2, h2
+    if gamma is not None:
+        if res is None:
+            x = rms_norm(h2, gamma, eps)
+        else:
+            x, r = rms_norm(h2, gamma, eps, res)
+    y = linear(x, w)
+    return (_glu(y, "silu") if glu else y), r, x
+
+
+def fused_gemv(h, w, res=None, gamma=None, eps=1e-5, glu=False, want_x=False):
+    """Decode projection with the pre-norm and / or the gated activation folded in (csrc/kernels/gemv.hip
+    ``hds_gemv_fused_bf16``). With ``gamma``: the rows are RMSNorm(h + res) * gamma -- the new residual ``h + res`` is
+    returned too (``h`` itself without ``res``), and the normed rows when ``want_x`` (HCache hidden latents). With
+    ``glu``: ``w`` is [gate; up] and the result is silu(x . gate^T) * (x . up^T). Returns (y, residual, x or None);
+    rows or weights the fused kernel does not take run the unfused kernels (the same arithmetic)."""
+    shape = h.shape
+    h2 = h.reshape(-1, shape[-1])
+    res2 = None if res is None else res.reshape(-1, shape[-1])
+    N = w.shape[0] // 2 if glu else w.shape[0]
+    ok = (fused_ok(h2, w, gamma, glu) and (gamma is not None or glu)
+          and (res2 is None or (res2.dtype == h2.dtype and res2.stride() == h2.stride() and res2.data_ptr() % 16 == 0)))
+    if not ok:  # the unfused kernels (GEMV or hipBLASLt by the size rules, RMSNorm, GLU): the model's other path
+        y, r, x = _unfused(h2, w, res2, gamma, eps, glu)
+    else:
+        M, K = h2.shape
+        y = torch.empty(M, N, dtype=h2.dtype, device=h2.device)
+        r = h2 if res2 is None else torch.empty_like(h2)  # never in place: other workgroups still read res
+        x = torch.empty_like(h2) if (want_x and gamma is not None) else None
+        native.check(native.kernels().hds_gemv_fused_bf16(
+            h2.data_ptr(), native.ptr(res2), native.ptr(gamma), float(eps), w.data_ptr(), y.data_ptr(),
+            native.ptr(r if res2 is not None else None), native.ptr(x), int(bool(glu)), M, N, K, K, N,
+            native.stream()), "gemv_fused_bf16")
+        if gamma is None:
+            x = h2
+    lead = shape[:-1]
+    return (y.view(*lead, N), r.view(shape), None if x is None or not want_x else x.view(shape))

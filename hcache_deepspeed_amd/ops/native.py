@@ -71,6 +71,7 @@ _KERNEL_SIGS = {
     "hds_transpose_bf16_var": "pp" + "ii" + "l" + "i" + "s",
     "hds_gemv_bf16_supported": "iii",
     "hds_gemv_bf16": "pppp" + "iii" + "ll" + "s",
+    "hds_gemv_fused_bf16": "ppp" + "f" + "pppp" + "iiii" + "ll" + "s",
     "hds_wmix_splits": "iii",
     "hds_wmix_supported": "iiii",
     "hds_wmix_gemm": "pppppp" + "iiiiii" + "s",

@@ -291,3 +291,29 @@ def test_native_ragged_metadata_matches_python_reference():
             assert tables[i, :len(blocks[i])].tolist() == blocks[i] and (tables[i, len(blocks[i]):] == 0).all()
         if A:
             assert atoms.tolist() == ref_atoms.tolist()
+
+
+@pytest.mark.parametrize("latent_mode", ["hidden", "kv"])
+def test_fused_decode_flow_cpu(latent_mode, monkeypatch):
+    """The decode flow with the pre-norms and SwiGLU folded into the projection GEMVs (model._fused_decode_ok;
+    off the GPU ops/gemv.fused_gemv runs the same arithmetic in torch): logits, evict / restore and the decode
+    step's HCache latents match the unfused flow."""
+    from hcache_deepspeed_amd.inference.v2.model import RaggedTransformer
+    real = RaggedTransformer._fused_decode_ok
+    _run_consistency("cpu", torch.float32, latent_mode, 2e-4)  # unfused, for the record
+    monkeypatch.setattr(RaggedTransformer, "_fused_decode_ok", lambda self, T: T <= 2)
+    _run_consistency("cpu", torch.float32, latent_mode, 2e-4)
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(RaggedTransformer, "_fused_decode_ok", (lambda self, T: T <= 2) if fused else real)
+        m = _model("cpu", torch.float32)
+        eng = build_engine_from_model(m, {"latent_mode": latent_mode, "dtype": "fp32",
+                                          "state_manager": {"max_context": 256, "kv_block_size": 64}},
+                                      device=torch.device("cpu"), num_kv_blocks=16)
+        g = torch.Generator().manual_seed(2)
+        eng.put([1, 2], [torch.randint(0, 211, (20, ), generator=g), torch.randint(0, 211, (9, ), generator=g)])
+        lg, lats = eng.put([1, 2], [torch.tensor([5]), torch.tensor([7])])  # a 2-row decode step, latents on
+        outs.append((lg.float(), [l.float() for l in lats]))
+    torch.testing.assert_close(outs[0][0], outs[1][0], atol=2e-4, rtol=2e-4)
+    for a, b in zip(outs[0][1], outs[1][1]):
+        torch.testing.assert_close(a, b, atol=2e-4, rtol=2e-4)

@@ -763,6 +763,35 @@ def test_gemv_bf16_matches_fp32(M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,glu,res", [(1, 6144, 4096, False, True), (1, 14336, 4096, True, True),
+                                           (3, 4100, 4096, False, False), (8, 1000, 1032, True, True),
+                                           (5, 8192, 512, True, False)])
+def test_gemv_fused_norm_glu_matches_fp32(M, N, K, glu, res):
+    """The decode GEMV with the RMSNorm prologue (and the SwiGLU epilogue) against fp32 references of the same
+    arithmetic: the new residual is bit-exact (one bf16 add), the normed rows within a bf16 ulp, the outputs at
+    GEMV accuracy; the HIP path must be the one that ran."""
+    from hcache_deepspeed_amd.ops import gemv as G
+    g = torch.Generator(device="cuda").manual_seed(M * 11 + N)
+    rows = 2 * N if glu else N
+    w = (torch.randn(rows, K, device="cuda", generator=g) * K**-0.5).to(torch.bfloat16)
+    h = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    r0 = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16) if res else None
+    gamma = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).to(torch.bfloat16)
+    assert G.fused_ok(h, w, gamma, glu)
+    y, r, x = G.fused_gemv(h, w, r0, gamma, 1e-5, glu=glu, want_x=True)
+    rr = h if r0 is None else (h.float() + r0.float()).to(torch.bfloat16)
+    assert torch.equal(r, rr)
+    rf = rr.float()
+    xr = rf * torch.rsqrt(rf.square().mean(-1, keepdim=True) + 1e-5) * gamma.float()
+    assert ((x.float() - xr).abs() <= 1e-2 * xr.abs() + 1e-3).all()
+    yr = x.float() @ w.float().t()
+    if glu:
+        yr = torch.nn.functional.silu(yr[:, :N].to(torch.bfloat16).float()) * yr[:, N:].to(torch.bfloat16).float()
+    rel = ((y.float() - yr).norm() / yr.norm()).item()
+    assert rel < 1e-2, rel
+
+
+@pytest.mark.gpu
 def test_kv_append_matches_index_copy():
     """HIP KV append (slot read on the device) equals two index_copy_ calls, for strided K/V views of a fused qkv."""
     from hcache_deepspeed_amd.ops.decode_attention import kv_append

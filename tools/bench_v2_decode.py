@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--capture-latents", action="store_true")
     ap.add_argument("--latent-mode", default="hidden")
     ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--batches", default="1,4,8", help="comma-separated decode batch sizes")
     args = ap.parse_args()
     from hcache_deepspeed_amd.inference.v2 import build_engine_from_model
     from hcache_deepspeed_amd.models.llama import LlamaForCausalLM, llama3_8b
@@ -28,7 +29,7 @@ def main():
     with torch.device(dev):
         model = LlamaForCausalLM(llama3_8b()).to(torch.bfloat16).eval()
     P, steps = 512, args.steps
-    for B in (1, 4, 8):
+    for B in [int(b) for b in args.batches.split(",")]:
         for cap in ((False, True) if args.capture_latents else (False, )):
             econf = {"dtype": "bf16", "latent_mode": args.latent_mode,
                      "state_manager": {"max_ragged_batch_size": B * P, "max_context": P + 2 * steps + 64,
