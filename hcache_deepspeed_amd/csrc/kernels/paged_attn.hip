@@ -274,7 +274,25 @@ struct PagedDecodeParams {
   int max_blocks, block_size, hq, hkv, splits;
   float scale;
   int window;
+  // splits > 1: one int per (sequence, kv head), zero between launches. Non-null: the last workgroup of a
+  // (sequence, kv head) to finish merges the splits itself (no combine launch) and resets its counter to 0, so a
+  // HIP-graph replay finds it zeroed again.
+  int* counters;
 };
+
+template <int D>
+__device__ __forceinline__ void decode_merge_splits(const PagedDecodeParams& p, int b, int h, int d, int q_start) {
+  const float* pm = p.part_ml + ((int64_t)b * p.hq + h) * p.splits * 2;
+  float mm = -INFINITY;
+  for (int s = 0; s < p.splits; ++s) mm = fmaxf(mm, pm[2 * s]);
+  float ll = 0.f, oo = 0.f;
+  for (int s = 0; s < p.splits; ++s) {
+    const float a = mm == -INFINITY ? 0.f : __expf(pm[2 * s] - mm);
+    ll += pm[2 * s + 1] * a;
+    oo += p.part_o[(((int64_t)b * p.hq + h) * p.splits + s) * D + d] * a;
+  }
+  p.o[((int64_t)q_start * p.hq + h) * D + d] = (bf16)(ll > 0.f ? oo / ll : 0.f);
+}
 
 template <int D>
 __global__ __launch_bounds__(256) void paged_decode_kernel(PagedDecodeParams p) {
@@ -390,22 +408,25 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(PagedDecodeParams p) 
       }
     }
   }
+  if (p.splits > 1 && p.counters != nullptr) {
+    // release this split's partials (device scope: the splits run on every XCD), count it in; the last one in
+    // acquires all of them and merges
+    __shared__ int s_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(p.counters + b * p.hkv + hk, 1) == p.splits - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (int t = threadIdx.x; t < G * D; t += 256) decode_merge_splits<D>(p, b, hk * G + t / D, t % D, q_start);
+    if (threadIdx.x == 0) p.counters[b * p.hkv + hk] = 0;
+  }
 }
 
 template <int D>
 __global__ __launch_bounds__(D) void paged_decode_combine_kernel(PagedDecodeParams p) {
   const int bh = blockIdx.x, b = bh / p.hq, h = bh % p.hq;
-  const float* pm = p.part_ml + (int64_t)bh * p.splits * 2;
-  float mm = -INFINITY;
-  for (int s = 0; s < p.splits; ++s) mm = fmaxf(mm, pm[2 * s]);
-  const int d = threadIdx.x;
-  float ll = 0.f, oo = 0.f;
-  for (int s = 0; s < p.splits; ++s) {
-    const float a = mm == -INFINITY ? 0.f : __expf(pm[2 * s] - mm);
-    ll += pm[2 * s + 1] * a;
-    oo += p.part_o[((int64_t)bh * p.splits + s) * D + d] * a;
-  }
-  p.o[((int64_t)p.seq_meta[3 * b] * p.hq + h) * D + d] = (bf16)(ll > 0.f ? oo / ll : 0.f);
+  decode_merge_splits<D>(p, b, h, threadIdx.x, p.seq_meta[3 * b]);
 }
 
 }  // namespace
@@ -469,22 +490,25 @@ HDS_EXPORT int hds_paged_decode_splits(int n_seqs, int hkv, int max_ctx) {
   return splits < 1 ? 1 : (splits > 64 ? 64 : splits);
 }
 
+// counters: null -> the splits are merged by a second (combine) launch; else n_seqs * hkv zeroed ints and the last
+// workgroup of each (sequence, kv head) merges them in the same launch (see paged_decode_kernel)
 HDS_EXPORT int hds_paged_decode(const void* q, int64_t sq, const void* cache, void* o, float* part_o, float* part_ml,
                                 const int* seq_meta, const int* block_tables, int max_blocks, int block_size,
                                 int n_seqs, int hq, int hkv, int head_dim, int splits, float scale, int window,
-                                hipStream_t st) {
+                                int* counters, hipStream_t st) {
   if (n_seqs <= 0) return 0;
   if (hq % hkv || !hds_paged_decode_supported(head_dim, hq / hkv) || splits < 1 ||
       (splits > 1 && (!part_o || !part_ml)))
     return hipErrorInvalidValue;
   PagedDecodeParams p{(const bf16*)q, sq, (const bf16*)cache, (bf16*)o, part_o, part_ml, seq_meta, block_tables,
-                      max_blocks, block_size, hq, hkv, splits, scale, window};
+                      max_blocks, block_size, hq, hkv, splits, scale, window, counters};
   const dim3 grid(splits, hkv, n_seqs);
   switch (head_dim) {
 #define HDS_DEC(d)                                                                                            \
   case d:                                                                                                     \
     hipLaunchKernelGGL(paged_decode_kernel<d>, grid, dim3(256), 0, st, p);                                    \
-    if (splits > 1) hipLaunchKernelGGL(paged_decode_combine_kernel<d>, dim3(n_seqs * hq), dim3(d), 0, st, p); \
+    if (splits > 1 && counters == nullptr)                                                                    \
+      hipLaunchKernelGGL(paged_decode_combine_kernel<d>, dim3(n_seqs * hq), dim3(d), 0, st, p);               \
     break;
     HDS_DEC(64)
     HDS_DEC(128)

@@ -97,7 +97,7 @@ _KERNEL_SIGS = {
     "hds_nhwc_bias_add": "i" + "ppppp" + "l" + "ii" + "s",
     "hds_paged_decode_supported": "ii",
     "hds_paged_decode_splits": "iii",
-    "hds_paged_decode": "p" + "l" + "pppp" + "pp" + "iiiiiii" + "f" + "i" + "s",
+    "hds_paged_decode": "p" + "l" + "pppp" + "pp" + "iiiiiii" + "f" + "i" + "p" + "s",
     "hds_copy_d2h": "pp" + "l" + "i" + "s",
     "hds_latent_slot_store": "p" + "l" + "pp" + "l" + "i" + "l" + "s",
     "hds_slot_advance": "p" + "i" + "s",

@@ -75,6 +75,23 @@ def build_atoms(seq_meta_host, n_q, n_kv):
     return torch.tensor(atoms if atoms else [(0, 0, 0)], dtype=torch.int32), len(atoms)
 
 
+_COUNTERS = {}
+_MERGE_IN_KERNEL = __import__("os").environ.get("HDS_DECODE_MERGE_IN_KERNEL", "0") == "1"
+
+
+def _merge_counters(device, n):
+    """Per-device ints the split-K decode kernel counts finished splits in (the last workgroup of a (sequence, kv
+    head) merges the splits and zeroes its counter again): allocated once, zeroed, with room for 64K (sequence, kv
+    head) pairs, so a HIP-graph decode captures a stable address. ``HDS_DECODE_MERGE_IN_KERNEL=1`` turns it on;
+    by default the separate combine launch merges."""
+    if not _MERGE_IN_KERNEL or n > 65536:
+        return None
+    buf = _COUNTERS.get(device)
+    if buf is None:
+        buf = _COUNTERS[device] = torch.zeros(65536, dtype=torch.int32, device=device)
+    return buf.data_ptr()
+
+
 def paged_attention(q, cache, atoms, n_atoms, seq_meta, block_tables, n_q, n_kv, scale, window=0,
                     seq_meta_host=None, block_tables_host=None, decode=False):
     """q: [T, n_q, D] (token-strided view ok). Returns o [T, n_q, D]. ``decode``: every sequence of the batch has
@@ -98,7 +115,8 @@ def paged_attention(q, cache, atoms, n_atoms, seq_meta, block_tables, n_q, n_kv,
                 lib.hds_paged_decode(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(), native.ptr(part_o),
                                      native.ptr(part_ml), seq_meta.data_ptr(), block_tables.data_ptr(),
                                      block_tables.shape[1], cache.shape[1], n_seqs, n_q, n_kv, D, splits, float(scale),
-                                     int(window), native.stream()), "paged_decode")
+                                     int(window), _merge_counters(q.device, n_seqs * n_kv) if splits > 1 else None,
+                                     native.stream()), "paged_decode")
             return o
         native.check(
             lib.hds_paged_attn(q.data_ptr(), q.stride(0), cache.data_ptr(), o.data_ptr(), atoms.data_ptr(), n_atoms,
