@@ -83,7 +83,9 @@ def _merge_counters(device, n):
     """Per-device ints the split-K decode kernel counts finished splits in (the last workgroup of a (sequence, kv
     head) merges the splits and zeroes its counter again): allocated once, zeroed, with room for 64K (sequence, kv
     head) pairs, so a HIP-graph decode captures a stable address. ``HDS_DECODE_MERGE_IN_KERNEL=1`` turns it on;
-    by default the separate combine launch merges."""
+    by default the separate combine launch merges: the device-scope release each split workgroup needs (its L2
+    written back for the other XCDs) cost more than the saved launch -- v2 decode B = 1 200 vs 247 tok/s, B = 8
+    1,096 vs 1,490 (profiles/r6/decode_merge/)."""
     if not _MERGE_IN_KERNEL or n > 65536:
         return None
     buf = _COUNTERS.get(device)

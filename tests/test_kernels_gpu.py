@@ -404,10 +404,14 @@ def test_paged_attention_matches_reference(lens, seen, D):
 
 @pytest.mark.parametrize("D,G", [(128, 4), (64, 8), (256, 2), (128, 1)])
 @pytest.mark.parametrize("seen,window", [([100, 5, 700, 0], 0), ([1000, 33, 64, 63], 0), ([300, 2000, 7, 90], 50)])
-def test_paged_decode_matches_reference(seen, window, D, G):
+@pytest.mark.parametrize("merge", [False, True])
+def test_paged_decode_matches_reference(seen, window, D, G, merge, monkeypatch):
     """Split-K paged decode (one new token per sequence) against the torch reference over the same block tables,
-    incl. sliding window, a first-token sequence (seen 0) and splits that get no keys."""
+    incl. sliding window, a first-token sequence (seen 0) and splits that get no keys; ``merge``: the last workgroup
+    of each (sequence, kv head) merges the splits in the same launch (its counters must be back at zero after)."""
+    from hcache_deepspeed_amd.ops import paged as P
     from hcache_deepspeed_amd.ops.paged import build_atoms, paged_attention
+    monkeypatch.setattr(P, "_MERGE_IN_KERNEL", merge)
     Hkv = 2
     Hq = Hkv * G
     lens = [1] * len(seen)
@@ -422,6 +426,12 @@ def test_paged_decode_matches_reference(seen, window, D, G):
                           seq_meta_host=metas, block_tables_host=tab)
     assert _rel(o.cpu(), ref) < 1e-2
     assert _rel(o.cpu(), o_atom.cpu()) < 1e-2
+    if merge:
+        for _ in range(3):  # repeated launches reuse the counters: each must find them zeroed again
+            o2 = paged_attention(q, cache, atoms.cuda(), n, meta.cuda(), tab.cuda(), Hq, Hkv, 1 / math.sqrt(D), window,
+                                 decode=True)
+            assert torch.equal(o2, o)
+        assert int(P._COUNTERS[q.device].abs().sum()) == 0
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
