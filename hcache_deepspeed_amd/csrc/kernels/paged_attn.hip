@@ -423,10 +423,31 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(PagedDecodeParams p) 
   }
 }
 
+// One workgroup of D threads per (sequence, q head): the split maxima / sums are loaded once, one per thread, into LDS
+// (one memory round trip instead of a dependent walk over the splits), then every thread merges its output column
+// over the splits with the partial-o loads unrolled so several are in flight (splits <= 64 <= D).
 template <int D>
 __global__ __launch_bounds__(D) void paged_decode_combine_kernel(PagedDecodeParams p) {
+  __shared__ float s_m[64], s_l[64];
   const int bh = blockIdx.x, b = bh / p.hq, h = bh % p.hq;
-  decode_merge_splits<D>(p, b, h, threadIdx.x, p.seq_meta[3 * b]);
+  const int d = threadIdx.x;
+  const float* pm = p.part_ml + (int64_t)bh * p.splits * 2;
+  if (d < p.splits) {
+    s_m[d] = pm[2 * d];
+    s_l[d] = pm[2 * d + 1];
+  }
+  __syncthreads();
+  float mm = -INFINITY;
+  for (int s = 0; s < p.splits; ++s) mm = fmaxf(mm, s_m[s]);
+  const float* po = p.part_o + (int64_t)bh * p.splits * D + d;
+  float ll = 0.f, oo = 0.f;
+#pragma unroll 8
+  for (int s = 0; s < p.splits; ++s) {
+    const float a = mm == -INFINITY ? 0.f : __expf(s_m[s] - mm);
+    ll += s_l[s] * a;
+    oo += po[(int64_t)s * D] * a;
+  }
+  p.o[((int64_t)p.seq_meta[3 * b] * p.hq + h) * D + d] = (bf16)(ll > 0.f ? oo / ll : 0.f);
 }
 
 }  // namespace
@@ -497,8 +518,8 @@ HDS_EXPORT int hds_paged_decode(const void* q, int64_t sq, const void* cache, vo
                                 int n_seqs, int hq, int hkv, int head_dim, int splits, float scale, int window,
                                 int* counters, hipStream_t st) {
   if (n_seqs <= 0) return 0;
-  if (hq % hkv || !hds_paged_decode_supported(head_dim, hq / hkv) || splits < 1 ||
-      (splits > 1 && (!part_o || !part_ml)))
+  if (hq % hkv || !hds_paged_decode_supported(head_dim, hq / hkv) || splits < 1 || splits > 64 ||
+      (splits > 1 && (!part_o || !part_ml)))  // <= 64: the combine kernel stages the split stats in LDS
     return hipErrorInvalidValue;
   PagedDecodeParams p{(const bf16*)q, sq, (const bf16*)cache, (bf16*)o, part_o, part_ml, seq_meta, block_tables,
                       max_blocks, block_size, hq, hkv, splits, scale, window, counters};
