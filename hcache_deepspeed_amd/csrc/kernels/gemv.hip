@@ -245,7 +245,81 @@ __global__ __launch_bounds__(256) void gemv_fused_kernel(const bf16* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Skinny GEMM for 2..16 token rows on the matrix cores: y[M, N] = x[M, K] . W[N, K]^T (+ bias).
+// The VALU GEMV above spends 4 dot2 instructions per 16-B weight chunk PER ROW, so from a few rows on it is VALU-bound
+// (o projection at M = 8: 1.7 TB/s) and hipBLASLt's small-M tiles stream at 3.5-3.7 TB/s. Here one
+// mfma_f32_16x16x32_bf16 contracts a 16-column x 32-k weight tile with all (up to 16) token rows at once, so the
+// kernel is a pure weight stream: A = W rows (lane l: row n0 + (l & 15), k = 8 (l >> 4) .. +8, one 16-B load), B = x^T
+// (lane l: token l & 15, same k; zero past M), C: token = l & 15, column n0 + 4 (l >> 4) + reg. A workgroup owns 16
+// output columns; its 4 waves split K four ways with 8 weight loads per lane in flight, and the partial tiles are
+// summed through LDS.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void skinny_mfma_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                          const bf16* __restrict__ bias, bf16* __restrict__ y, int M,
+                                                          int N, int K, int64_t ldx, int64_t ldy) {
+  __shared__ f32x4 red[3][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int row = min(n0 + (lane & 15), N - 1);  // tail columns re-read column N-1 (not stored)
+  const int tok = lane & 15;
+  const int kq = K >> 2;  // this wave's quarter of K (K % 128 == 0)
+  const int kb = wid * kq + 8 * (lane >> 4);
+  const bf16* wp = w + (int64_t)row * K + kb;
+  const bf16* xp = x + (int64_t)min(tok, M - 1) * ldx + kb;
+  const bool tok_ok = tok < M;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 8;
+  int k = 0;
+  for (; k + 32 * U <= kq; k += 32 * U) {
+    bf16x8_t a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = *reinterpret_cast<const bf16x8_t*>(wp + k + 32 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      b[u] = *reinterpret_cast<const bf16x8_t*>(xp + k + 32 * u);
+      if (!tok_ok) b[u] = bf16x8_t{};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc, 0, 0, 0);
+  }
+  for (; k < kq; k += 32) {
+    const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(wp + k);
+    bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(xp + k);
+    if (!tok_ok) b = bf16x8_t{};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+  if (wid > 0) red[wid - 1][lane] = acc;
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int v = 0; v < 3; ++v) acc += red[v][lane];
+    if (tok_ok) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 4 * (lane >> 4) + r;
+        if (n < N) {
+          float v = acc[r];
+          if (bias) v += (float)bias[n];
+          y[(int64_t)tok * ldy + n] = (bf16)v;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// Skinny matrix-core GEMM (skinny_mfma_kernel): 1 <= M <= 16, K % 128 == 0, 16-B aligned rows
+HDS_EXPORT int hds_skinny_gemm_bf16(const void* x, const void* w, const void* bias, void* y, int M, int N, int K,
+                                    int64_t ldx, int64_t ldy, hipStream_t st) {
+  if (M < 1 || M > 16 || N < 1 || K < 128 || K % 128 || ldx % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(skinny_mfma_kernel, dim3((N + 15) / 16), dim3(256), 0, st, (const bf16*)x, (const bf16*)w,
+                     (const bf16*)bias, (bf16*)y, M, N, K, ldx, ldy);
+  return hipGetLastError();
+}
 
 // Fused decode GEMV (see gemv_fused_kernel): y[M, N] = norm(h (+ res)) . W^T, or with glu != 0, y[M, N] =
 // silu(x . Wg^T) * (x . Wu^T) for W = [Wg; Wu] of 2N rows (x normed when gamma is given, else h itself). r_out /

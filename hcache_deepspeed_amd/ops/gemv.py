@@ -44,10 +44,39 @@ def gemv(x2, w, b=None):
     return y
 
 
+# 2..16 token rows: the matrix-core skinny GEMM (csrc/kernels/gemv.hip skinny_mfma_kernel) instead of the VALU GEMV /
+# hipBLASLt's small-M tiles (HDS_SKINNY_GEMM=0: those)
+SKINNY = _os.environ.get("HDS_SKINNY_GEMM", "1") == "1"
+
+
+def skinny_ok(x2, w, b=None):
+    if not (SKINNY and native.use_native(x2) and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and w.dim() == 2):
+        return False
+    M, K = x2.shape
+    if not 2 <= M <= 16 or w.shape[1] != K or K % 128 or not w.is_contiguous() or x2.stride(1) != 1 or x2.stride(0) % 8:
+        return False
+    if x2.data_ptr() % 16 or w.data_ptr() % 16:
+        return False
+    return b is None or (b.dtype == torch.bfloat16 and b.is_contiguous())
+
+
+def skinny(x2, w, b=None):
+    M, K = x2.shape
+    N = w.shape[0]
+    y = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
+    native.check(native.kernels().hds_skinny_gemm_bf16(x2.data_ptr(), w.data_ptr(), native.ptr(b), y.data_ptr(), M, N,
+                                                       K, x2.stride(0), N, native.stream()), "skinny_gemm_bf16")
+    return y
+
+
 def linear(x, w, b=None):
-    """``F.linear(x, w, b)``; decode-sized bf16 inputs run the HIP GEMV."""
+    """``F.linear(x, w, b)``; decode-sized bf16 inputs run the HIP GEMV (one row) or the skinny matrix-core GEMM
+    (2..16 rows)."""
     if x.dim() >= 1 and x.is_cuda:
         x2 = x.reshape(-1, x.shape[-1])
+        if skinny_ok(x2, w, b):
+            return skinny(x2, w, b).view(*x.shape[:-1], w.shape[0])
         if gemv_ok(x2, w, b):
             return gemv(x2, w, b).view(*x.shape[:-1], w.shape[0])
     return F.linear(x, w, b)

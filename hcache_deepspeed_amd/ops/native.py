@@ -72,6 +72,7 @@ _KERNEL_SIGS = {
     "hds_gemv_bf16_supported": "iii",
     "hds_gemv_bf16": "pppp" + "iii" + "ll" + "s",
     "hds_gemv_fused_bf16": "ppp" + "f" + "pppp" + "iiii" + "ll" + "s",
+    "hds_skinny_gemm_bf16": "pppp" + "iii" + "ll" + "s",
     "hds_wmix_splits": "iii",
     "hds_wmix_supported": "iiii",
     "hds_wmix_gemm": "pppppp" + "iiiiii" + "s",

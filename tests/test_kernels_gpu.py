@@ -773,6 +773,25 @@ def test_gemv_bf16_matches_fp32(M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(2, 6144, 4096), (8, 28672, 4096), (16, 4096, 14336), (5, 1000, 1024),
+                                   (3, 7, 128)])
+def test_skinny_gemm_matches_fp32(M, N, K):
+    """The matrix-core skinny GEMM (2..16 token rows) against an fp32 reference, incl. an N tail, bias and a strided
+    activation view; the HIP path must be the one that ran."""
+    from hcache_deepspeed_amd.ops.gemv import linear, skinny, skinny_ok
+    g = torch.Generator(device="cuda").manual_seed(M * 13 + N)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K**-0.5).to(torch.bfloat16)
+    big = torch.randn(M, K + 8, device="cuda", generator=g).to(torch.bfloat16)
+    x = big[:, :K]  # row stride K + 8
+    b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    assert skinny_ok(x, w, b)
+    ref = x.float() @ w.float().t() + b.float()
+    for y in (skinny(x, w, b), linear(x, w, b)):
+        rel = ((y.float() - ref).norm() / ref.norm()).item()
+        assert rel < 8e-3, rel
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,glu,res", [(1, 6144, 4096, False, True), (1, 14336, 4096, True, True),
                                            (3, 4100, 4096, False, False), (8, 1000, 1032, True, True),
                                            (5, 8192, 512, True, False)])

@@ -2,11 +2,11 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r6dec
+O=gpurun_out/r6dec${B:-1}
 mkdir -p $O
-timeout -k 10 300 python tools/bench_v2_decode.py --batches 1 --steps 64 > $O/decode_b1.jsonl 2> $O/decode_b1.err || { echo failed; tail -20 $O/decode_b1.err; exit 1; }
-cat $O/decode_b1.jsonl
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/bench_v2_decode.py --batches 1 --steps 64 > $O/prof.log 2>&1 || { echo prof failed; tail -20 $O/prof.log; exit 1; }
+timeout -k 10 300 python tools/bench_v2_decode.py --batches ${B:-1} --steps 64 > $O/decode_b${B:-1}.jsonl 2> $O/decode_b${B:-1}.err || { echo failed; tail -20 $O/decode_b${B:-1}.err; exit 1; }
+cat $O/decode_b${B:-1}.jsonl
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/bench_v2_decode.py --batches ${B:-1} --steps 64 > $O/prof.log 2>&1 || { echo prof failed; tail -20 $O/prof.log; exit 1; }
 DB=$(find $O/prof -name "*.db" | head -1)
 python - "$DB" <<'PY' > $O/decode_kernels.txt
 import sqlite3, sys
