@@ -257,6 +257,7 @@ __global__ __launch_bounds__(256) void gemv_fused_kernel(const bf16* __restrict_
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+template <int U>
 __global__ __launch_bounds__(256) void skinny_mfma_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                           const bf16* __restrict__ bias, bf16* __restrict__ y, int M,
                                                           int N, int K, int64_t ldx, int64_t ldy) {
@@ -271,7 +272,6 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(const bf16* __restrict
   const bf16* xp = x + (int64_t)min(tok, M - 1) * ldx + kb;
   const bool tok_ok = tok < M;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  constexpr int U = 8;
   int k = 0;
   for (; k + 32 * U <= kq; k += 32 * U) {
     bf16x8_t a[U], b[U];
@@ -310,15 +310,31 @@ __global__ __launch_bounds__(256) void skinny_mfma_kernel(const bf16* __restrict
   }
 }
 
+int g_skinny_u = 16;
+
 }  // namespace
 
 // Skinny matrix-core GEMM (skinny_mfma_kernel): 1 <= M <= 16, K % 128 == 0, 16-B aligned rows
 HDS_EXPORT int hds_skinny_gemm_bf16(const void* x, const void* w, const void* bias, void* y, int M, int N, int K,
                                     int64_t ldx, int64_t ldy, hipStream_t st) {
   if (M < 1 || M > 16 || N < 1 || K < 128 || K % 128 || ldx % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(skinny_mfma_kernel, dim3((N + 15) / 16), dim3(256), 0, st, (const bf16*)x, (const bf16*)w,
-                     (const bf16*)bias, (bf16*)y, M, N, K, ldx, ldy);
+  if (g_skinny_u == 32 && (K >> 2) % 1024 == 0)
+    hipLaunchKernelGGL(skinny_mfma_kernel<32>, dim3((N + 15) / 16), dim3(256), 0, st, (const bf16*)x,
+                       (const bf16*)w, (const bf16*)bias, (bf16*)y, M, N, K, ldx, ldy);
+  else if (g_skinny_u >= 16)
+    hipLaunchKernelGGL(skinny_mfma_kernel<16>, dim3((N + 15) / 16), dim3(256), 0, st, (const bf16*)x,
+                       (const bf16*)w, (const bf16*)bias, (bf16*)y, M, N, K, ldx, ldy);
+  else
+    hipLaunchKernelGGL(skinny_mfma_kernel<8>, dim3((N + 15) / 16), dim3(256), 0, st, (const bf16*)x,
+                       (const bf16*)w, (const bf16*)bias, (bf16*)y, M, N, K, ldx, ldy);
   return hipGetLastError();
+}
+
+// weight loads per lane in flight in the skinny GEMM (8, 16 or 32); returns the previous value
+HDS_EXPORT int hds_skinny_set_unroll(int u) {
+  const int prev = g_skinny_u;
+  g_skinny_u = u >= 32 ? 32 : (u >= 16 ? 16 : 8);
+  return prev;
 }
 
 // Fused decode GEMV (see gemv_fused_kernel): y[M, N] = norm(h (+ res)) . W^T, or with glu != 0, y[M, N] =

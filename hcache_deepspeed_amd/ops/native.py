@@ -73,6 +73,7 @@ _KERNEL_SIGS = {
     "hds_gemv_bf16": "pppp" + "iii" + "ll" + "s",
     "hds_gemv_fused_bf16": "ppp" + "f" + "pppp" + "iiii" + "ll" + "s",
     "hds_skinny_gemm_bf16": "pppp" + "iii" + "ll" + "s",
+    "hds_skinny_set_unroll": "i",
     "hds_wmix_splits": "iii",
     "hds_wmix_supported": "iiii",
     "hds_wmix_gemm": "pppppp" + "iiiiii" + "s",
@@ -167,6 +168,8 @@ def load_kernels(build_if_missing=True):
         check(lib.hds_attn_fwd_variant(fwd_variant_default()), "hds_attn_fwd_variant")
         # FlashAttention backward dQ kernel (hds_attn_bwd_dq_variant; 1 = one wave per SIMD, 64 rows per wave)
         lib.hds_attn_bwd_dq_variant(int(os.environ.get("HDS_ATTN_DQ_VAR", "0")))
+        # skinny GEMM weight loads in flight per lane (16: B = 4 decode 925 vs 881 tok/s with 8, profiles/r6/skinny_u)
+        lib.hds_skinny_set_unroll(int(os.environ.get("HDS_SKINNY_U", "16")))
         _klib = lib
         return _klib
 
