@@ -47,6 +47,7 @@ def gemv(x2, w, b=None):
 # 2..16 token rows: the matrix-core skinny GEMM (csrc/kernels/gemv.hip skinny_mfma_kernel) instead of the VALU GEMV /
 # hipBLASLt's small-M tiles (HDS_SKINNY_GEMM=0: those)
 SKINNY = _os.environ.get("HDS_SKINNY_GEMM", "1") == "1"
+SKINNY_MIN_M = int(_os.environ.get("HDS_SKINNY_MIN_M", "2"))  # 1: one-row linears too (instead of the VALU GEMV)
 
 
 def skinny_ok(x2, w, b=None):
@@ -54,7 +55,7 @@ def skinny_ok(x2, w, b=None):
             and w.dim() == 2):
         return False
     M, K = x2.shape
-    if not 2 <= M <= 16 or w.shape[1] != K or K % 128 or not w.is_contiguous() or x2.stride(1) != 1 or x2.stride(0) % 8:
+    if not SKINNY_MIN_M <= M <= 16 or w.shape[1] != K or K % 128 or not w.is_contiguous() or x2.stride(1) != 1 or x2.stride(0) % 8:
         return False
     if x2.data_ptr() % 16 or w.data_ptr() % 16:
         return False
