@@ -388,10 +388,18 @@ class RaggedTransformer:
             from ...ops.gemv import fused_gemv
             eps = spec.norm_eps
             want_x = capture_latents and self.latent_mode in ("hidden", "hidden_fp8", "hidden_int8")
+            ring = getattr(sink, "__self__", None) if sink is not None else None
+            stage = ring.stage() if (capture_latents and self.latent_mode == "hidden"
+                                     and isinstance(ring, _LatentRing)) else None
             for i, L in enumerate(self.layers):
-                # pre-norm + qkv in one GEMV; the new residual stream (and the normed rows for hidden latents) too
-                qkv, residual, x = fused_gemv(h, L["qkv.w"], residual, L["ln1.w"], eps, want_x=want_x)
-                if capture_latents and self.latent_mode == "hidden":
+                # pre-norm + qkv in one GEMV; the new residual stream (and the normed rows for hidden latents) too --
+                # in a decode graph written straight into the step's latent stage
+                qkv, residual, x = fused_gemv(h, L["qkv.w"], residual, L["ln1.w"], eps, want_x=want_x,
+                                              x_out=None if stage is None else stage[i])
+                if stage is not None:
+                    if x.data_ptr() != stage[i].data_ptr():
+                        stage[i].copy_(x.view_as(stage[i]))
+                elif capture_latents and self.latent_mode == "hidden":
                     emit(i, x)
                 elif capture_latents and self.latent_mode == "hidden_fp8":
                     emit(i, self._pack_fp8(x))
@@ -401,6 +409,8 @@ class RaggedTransformer:
                 # post-attention norm + gate|up + SwiGLU in one GEMV, then the down projection
                 g, residual, _ = fused_gemv(a, L["up.w"], residual, L["ln2.w"], eps, glu=True)
                 h = self.down_lin(g, L["down.w"], L["down.b"])
+            if stage is not None:
+                ring.flush_stage()  # every layer's latent rows into the ring slot, one store
         for i, L in (enumerate(self.layers) if not self._fused_decode_ok(T) else ()):
             if residual is None:
                 x = self._norm(h, L["ln1.w"], L["ln1.b"])
@@ -602,6 +612,20 @@ class _LatentRing:
     def sink(self, i, rows):
         from ...ops.hostcopy import latent_slot_store
         latent_slot_store(rows, self.dev, self.slot, i)
+
+    def stage(self):
+        """[L, B, W] device buffer the fused decode projections write every layer's latent rows into directly (the
+        normed rows are produced there, no per-layer store kernel); ``flush_stage`` moves it into the ring slot with
+        one store at the end of the step."""
+        st = getattr(self, "_stage", None)
+        if st is None:
+            st = self._stage = torch.empty(self.shape, dtype=self.dtype, device=self.dev.device)
+        return st
+
+    def flush_stage(self):
+        from ...ops.hostcopy import latent_slot_store
+        L, B, W = self.shape
+        latent_slot_store(self._stage.view(L * B, W), self.dev.view(2 * self.R, 1, L * B, W), self.slot, 0)
 
     def advance(self):
         from ...ops.hostcopy import slot_advance

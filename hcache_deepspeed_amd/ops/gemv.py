@@ -110,12 +110,13 @@ def _unfused(h2, w, res, gamma, eps, glu):
     return (_glu(y, "silu") if glu else y), r, x
 
 
-def fused_gemv(h, w, res=None, gamma=None, eps=1e-5, glu=False, want_x=False):
+def fused_gemv(h, w, res=None, gamma=None, eps=1e-5, glu=False, want_x=False, x_out=None):
     """Decode projection with the pre-norm and / or the gated activation folded in (csrc/kernels/gemv.hip
     ``hds_gemv_fused_bf16``). With ``gamma``: the rows are RMSNorm(h + res) * gamma -- the new residual ``h + res`` is
     returned too (``h`` itself without ``res``), and the normed rows when ``want_x`` (HCache hidden latents). With
     ``glu``: ``w`` is [gate; up] and the result is silu(x . gate^T) * (x . up^T). Returns (y, residual, x or None);
-    rows or weights the fused kernel does not take run the unfused kernels (the same arithmetic)."""
+    rows or weights the fused kernel does not take run the unfused kernels (the same arithmetic). ``x_out``: a
+    contiguous [rows, K] buffer the normed rows are written into (``want_x``; the unfused fallback returns its own)."""
     shape = h.shape
     h2 = h.reshape(-1, shape[-1])
     res2 = None if res is None else res.reshape(-1, shape[-1])
@@ -128,7 +129,11 @@ def fused_gemv(h, w, res=None, gamma=None, eps=1e-5, glu=False, want_x=False):
         M, K = h2.shape
         y = torch.empty(M, N, dtype=h2.dtype, device=h2.device)
         r = h2 if res2 is None else torch.empty_like(h2)  # never in place: other workgroups still read res
-        x = torch.empty_like(h2) if (want_x and gamma is not None) else None
+        x = None
+        if want_x and gamma is not None:
+            ok_out = (x_out is not None and x_out.dtype == h2.dtype and x_out.is_contiguous()
+                      and x_out.numel() == h2.numel() and x_out.data_ptr() % 16 == 0)
+            x = x_out.view(h2.shape) if ok_out else torch.empty_like(h2)
         native.check(native.kernels().hds_gemv_fused_bf16(
             h2.data_ptr(), native.ptr(res2), native.ptr(gamma), float(eps), w.data_ptr(), y.data_ptr(),
             native.ptr(r if res2 is not None else None), native.ptr(x), int(bool(glu)), M, N, K, K, N,
