@@ -91,31 +91,45 @@ __global__ __launch_bounds__(256) void gemv_bf16_kernel(const bf16* __restrict__
 // decode step launches neither the RMSNorm nor the GLU kernel (each ~4-5 us per call in a decode graph, i.e. about a
 // tenth of a Llama-3-8B B = 1 step, for kernels that move a few KB).
 //
-// NORM: the input rows are x = bf16(r * rstd * gamma), r = bf16(h + res) (or h without a residual) -- exactly the
-// arithmetic of norm.hip's RMSNorm forward. The workgroup's 256 threads first reduce sum(r^2) of its M rows once into
-// LDS; its 4 waves then stream their weight rows as gemv_bf16_kernel does, building each x chunk from r, rstd and gamma
-// (all L2-resident, K * 2 bytes) on the fly. Workgroup 0 also writes r (the new residual stream) and, when asked, x
-// (the normed rows: HCache's hidden-state latents).
+// NORM: the input rows are x = bf16(r * rstd * gamma), r = bf16(h + res) (or h without a residual) -- the arithmetic
+// of norm.hip's RMSNorm forward. rstd is one scalar per row, so x . w = rstd * (bf16(r * gamma) . w): a wave streams
+// its weight rows against bf16(r * gamma) chunks built on the fly (r and gamma are L2-resident, K * 2 bytes) and, since
+// its 64 lanes together walk the whole row, accumulates sum(r^2) in the same loop; rstd scales the reduced dot
+// products at the end. No workgroup-wide prologue (row reduction, LDS, barriers) sits ahead of the weight stream: that
+// serial prologue cost what a separate RMSNorm launch did (fused qkv 15.4 us vs 10.9 us plain GEMV + 4.6 us norm).
+// Workgroup 0 also writes r (the new residual stream) and, when asked, x (the normed rows: HCache's hidden-state
+// latents) once its waves know rstd.
 // GLU: the weight is [gate; up] ([2I, K]) and the output y[M, I] = bf16(act(bf16(x.g_j)) * bf16(x.u_j)) (silu): a wave
 // owns R output columns and streams their gate AND up rows, so the [M, 2I] intermediate never exists.
 __device__ __forceinline__ float silu_f(float v) { return v * __builtin_amdgcn_rcpf(1.f + __expf(-v)); }
 
+// r = bf16(h + res) (h without res) for 8 elements at k
+__device__ __forceinline__ bf16x8 load_r(const bf16* __restrict__ h, const bf16* __restrict__ res, int64_t off, int k) {
+  bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + off + k);
+  if (res != nullptr) {
+    const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + off + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[j] = (bf16)((float)hv[j] + (float)rv[j]);  // round like the unfused add
+  }
+  return hv;
+}
+
+// the GEMV operand chunk: bf16(r * gamma) with sum(r^2) accumulated into ss (NORM), else h itself
 template <bool NORM>
 __device__ __forceinline__ bf16x8 load_x(const bf16* __restrict__ h, const bf16* __restrict__ res,
-                                         const bf16* __restrict__ gamma, float rstd, int64_t off, int k) {
-  bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + off + k);
+                                         const bf16* __restrict__ gamma, int64_t off, int k, float& ss) {
   if constexpr (!NORM) {
-    return hv;
+    return *reinterpret_cast<const bf16x8*>(h + off + k);
   } else {
+    const bf16x8 r = load_r(h, res, off, k);
     const bf16x8 g = *reinterpret_cast<const bf16x8*>(gamma + k);
     bf16x8 o;
-    if (res != nullptr) {
-      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + off + k);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) hv[j] = (bf16)((float)hv[j] + (float)rv[j]);  // round like the unfused add
+    for (int j = 0; j < 8; ++j) {
+      const float v = (float)r[j];
+      ss += v * v;
+      o[j] = (bf16)(v * (float)g[j]);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)hv[j] * rstd * (float)g[j]);
     return o;
   }
 }
@@ -126,71 +140,19 @@ __global__ __launch_bounds__(256) void gemv_fused_kernel(const bf16* __restrict_
                                                          const bf16* __restrict__ w, bf16* __restrict__ y,
                                                          bf16* __restrict__ r_out, bf16* __restrict__ x_out, int M,
                                                          int N, int K, int64_t ldh, int64_t ldy) {
-  __shared__ float s_part[4][MAXM];
-  __shared__ float s_rstd[MAXM];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  float rstd[MAXM];
-#pragma unroll
-  for (int m = 0; m < MAXM; ++m) rstd[m] = 1.f;
-  if constexpr (NORM) {
-    float ss[MAXM];
-#pragma unroll
-    for (int m = 0; m < MAXM; ++m) ss[m] = 0.f;
-    for (int c = threadIdx.x * 8; c < K; c += 2048) {
-#pragma unroll
-      for (int m = 0; m < MAXM; ++m) {
-        if (m < M) {
-          bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + m * ldh + c);
-          if (res != nullptr) {
-            const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + m * ldh + c);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) hv[j] = (bf16)((float)hv[j] + (float)rv[j]);
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ss[m] += (float)hv[j] * (float)hv[j];
-        }
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < MAXM; ++m) {
-      const float t = wave_sum(ss[m]);
-      if (lane == 0) s_part[wid][m] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x < MAXM)
-      s_rstd[threadIdx.x] = rsqrtf((s_part[0][threadIdx.x] + s_part[1][threadIdx.x] + s_part[2][threadIdx.x] +
-                                    s_part[3][threadIdx.x]) / (float)K + eps);
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < MAXM; ++m) rstd[m] = s_rstd[m];
-    if (blockIdx.x == 0 && (r_out != nullptr || x_out != nullptr)) {
-      for (int c = threadIdx.x * 8; c < K; c += 2048) {
-#pragma unroll
-        for (int m = 0; m < MAXM; ++m) {
-          if (m < M) {
-            if (r_out != nullptr && res != nullptr) {
-              bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + m * ldh + c);
-              const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + m * ldh + c);
-#pragma unroll
-              for (int j = 0; j < 8; ++j) hv[j] = (bf16)((float)hv[j] + (float)rv[j]);
-              *reinterpret_cast<bf16x8*>(r_out + m * ldh + c) = hv;
-            }
-            if (x_out != nullptr)
-              *reinterpret_cast<bf16x8*>(x_out + m * ldh + c) = load_x<true>(h, res, gamma, rstd[m], m * ldh, c);
-          }
-        }
-      }
-    }
-  }
   const int n0 = (blockIdx.x * 4 + wid) * R;  // output columns [n0, n0 + R)
-  if (n0 >= N) return;
-  constexpr int RR = GLU ? 2 * R : R;  // weight rows streamed per wave: the gate rows, then the up rows
-  float acc[RR][MAXM];
+  const bool writes_rows = NORM && blockIdx.x == 0 && (r_out != nullptr || x_out != nullptr);
+  if (n0 >= N && !writes_rows) return;  // (workgroup 0's waves all run: they share the row writes below)
+  constexpr int RR = GLU ? 2 * R : R;   // weight rows streamed per wave: the gate rows, then the up rows
+  float acc[RR][MAXM], ss[MAXM];
 #pragma unroll
-  for (int r = 0; r < RR; ++r)
+  for (int m = 0; m < MAXM; ++m) {
+    ss[m] = 0.f;
 #pragma unroll
-    for (int m = 0; m < MAXM; ++m) acc[r][m] = 0.f;
+    for (int r = 0; r < RR; ++r) acc[r][m] = 0.f;
+  }
   const bf16* wr[RR];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -209,8 +171,8 @@ __global__ __launch_bounds__(256) void gemv_fused_kernel(const bf16* __restrict_
 #pragma unroll
     for (int m = 0; m < MAXM; ++m) {
       if (m < M) {
-        const bf16x8 xa = load_x<NORM>(h, res, gamma, rstd[m], m * ldh, k0);
-        const bf16x8 xb = load_x<NORM>(h, res, gamma, rstd[m], m * ldh, k0 + 512);
+        const bf16x8 xa = load_x<NORM>(h, res, gamma, m * ldh, k0, ss[m]);
+        const bf16x8 xb = load_x<NORM>(h, res, gamma, m * ldh, k0 + 512, ss[m]);
 #pragma unroll
         for (int r = 0; r < RR; ++r) acc[r][m] = dot8(xb, wb[r], dot8(xa, wa[r], acc[r][m]));
       }
@@ -223,9 +185,30 @@ __global__ __launch_bounds__(256) void gemv_fused_kernel(const bf16* __restrict_
 #pragma unroll
     for (int m = 0; m < MAXM; ++m) {
       if (m < M) {
-        const bf16x8 xa = load_x<NORM>(h, res, gamma, rstd[m], m * ldh, k0);
+        const bf16x8 xa = load_x<NORM>(h, res, gamma, m * ldh, k0, ss[m]);
 #pragma unroll
         for (int r = 0; r < RR; ++r) acc[r][m] = dot8(xa, wa[r], acc[r][m]);
+      }
+    }
+  }
+  float rstd[MAXM];
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m) rstd[m] = NORM ? rsqrtf(wave_sum(ss[m]) / (float)K + eps) : 1.f;
+  if (writes_rows) {  // the 4 waves of workgroup 0 split the rows' chunks
+    for (int c = (wid * 64 + lane) * 8; c < K; c += 2048) {
+#pragma unroll
+      for (int m = 0; m < MAXM; ++m) {
+        if (m < M) {
+          const bf16x8 r = load_r(h, res, m * ldh, c);
+          if (r_out != nullptr && res != nullptr) *reinterpret_cast<bf16x8*>(r_out + m * ldh + c) = r;
+          if (x_out != nullptr) {
+            const bf16x8 g = *reinterpret_cast<const bf16x8*>(gamma + c);
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)r[j] * rstd[m] * (float)g[j]);
+            *reinterpret_cast<bf16x8*>(x_out + m * ldh + c) = o;
+          }
+        }
       }
     }
   }
@@ -234,9 +217,9 @@ __global__ __launch_bounds__(256) void gemv_fused_kernel(const bf16* __restrict_
 #pragma unroll
     for (int m = 0; m < MAXM; ++m) {
       if (m < M && n0 + r < N) {
-        const float v = wave_sum(acc[r][m]);
+        const float v = rstd[m] * wave_sum(acc[r][m]);
         if constexpr (GLU) {
-          const float u = wave_sum(acc[R + r][m]);
+          const float u = rstd[m] * wave_sum(acc[R + r][m]);
           if (lane == 0) y[m * ldy + n0 + r] = (bf16)(silu_f((float)(bf16)v) * (float)(bf16)u);
         } else {
           if (lane == 0) y[m * ldy + n0 + r] = (bf16)v;
