@@ -425,12 +425,19 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(PagedDecodeParams p) 
 
 // One workgroup of D threads per (sequence, q head): the split maxima / sums are loaded once, one per thread, into LDS
 // (one memory round trip instead of a dependent walk over the splits), then every thread merges its output column
-// over the splits with the partial-o loads unrolled so several are in flight (splits <= 64 <= D).
+// over the splits from partial-o values it requested before the barrier (splits <= 64 <= D).
 template <int D>
 __global__ __launch_bounds__(D) void paged_decode_combine_kernel(PagedDecodeParams p) {
   __shared__ float s_m[64], s_l[64];
   const int bh = blockIdx.x, b = bh / p.hq, h = bh % p.hq;
   const int d = threadIdx.x;
+  // every load is issued before the barrier: the partial-o column (its addresses need no split stat) and the output
+  // row overlap the stats' round trip instead of following it
+  const float* po = p.part_o + (int64_t)bh * p.splits * D + d;
+  float pov[64];
+#pragma unroll
+  for (int s = 0; s < 64; ++s) pov[s] = s < p.splits ? po[(int64_t)s * D] : 0.f;
+  const int row = p.seq_meta[3 * b];
   const float* pm = p.part_ml + (int64_t)bh * p.splits * 2;
   if (d < p.splits) {
     s_m[d] = pm[2 * d];
@@ -439,15 +446,16 @@ __global__ __launch_bounds__(D) void paged_decode_combine_kernel(PagedDecodePara
   __syncthreads();
   float mm = -INFINITY;
   for (int s = 0; s < p.splits; ++s) mm = fmaxf(mm, s_m[s]);
-  const float* po = p.part_o + (int64_t)bh * p.splits * D + d;
   float ll = 0.f, oo = 0.f;
-#pragma unroll 8
-  for (int s = 0; s < p.splits; ++s) {
-    const float a = mm == -INFINITY ? 0.f : __expf(s_m[s] - mm);
-    ll += s_l[s] * a;
-    oo += po[(int64_t)s * D] * a;
+#pragma unroll
+  for (int s = 0; s < 64; ++s) {
+    if (s < p.splits) {
+      const float a = mm == -INFINITY ? 0.f : __expf(s_m[s] - mm);
+      ll += s_l[s] * a;
+      oo += pov[s] * a;
+    }
   }
-  p.o[((int64_t)p.seq_meta[3 * b] * p.hq + h) * D + d] = (bf16)(ll > 0.f ? oo / ll : 0.f);
+  p.o[((int64_t)row * p.hq + h) * D + d] = (bf16)(ll > 0.f ? oo / ll : 0.f);
 }
 
 }  // namespace
